@@ -1,0 +1,265 @@
+/*
+ * avrecode oracle — CPU restatement of the reference's recode hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (avrecode_amd/, include/) links,
+ * imports or executes this code.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may use it, and there only as the checker / CPU baseline.
+ *
+ * What it restates (reference = /root/reference, read-only, ddkang/avrecode):
+ *   - arithmetic_code.h:31-320        generic binary arithmetic coder (encoder, decoder, finish)
+ *   - cabac_code.h:16-86              CABAC re-encoder on top of the generic coder
+ *   - recode.cpp:233-471, 615-1100    h264_model predictor, scan geometry, h264_symbol::execute
+ *   - recode.cpp:1102-1624            compressor / decompressor drivers, surrogates, roundtrip
+ *   - recode.proto                    Recoded container (hand-written proto2 wire codec)
+ * and, because the libavcodec-hooks FFmpeg fork (submodule ffmpeg/, pinned commit unknowable,
+ * FFmpeg 2.8-3.0 API era) is absent from the reference, the parts of it the hot path calls:
+ *   - ITU-T H.264 9.3 CABAC decoding engine (ff_get_cabac / _bypass / _terminate)
+ *   - ITU-T H.264 7.3.4/7.3.5 CABAC slice_data()/macroblock_layer() parse that drives the hooks
+ *   - H.264 NAL / SPS / PPS / slice header parsing, MP4 (avcC) and Annex-B demux.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - the generic coder is pinned bit-exactly against arithmetic_code.h compiled as-is
+ *     (oracle/ref_arith_driver.cpp -> oracle/_ref/ref_arith, goldens in tests/golden/);
+ *   - the CABAC engine + parser are pinned by real x264 streams (tests/fixtures): every slice must
+ *     parse to end_of_slice at the last MB with the CABAC decoder ending exactly on the
+ *     rbsp_stop_one_bit, and re-encoding the parsed bins must regenerate the original bytes;
+ *   - the predictor (h264_model) is unpinned against a reference build (recode.cpp needs the
+ *     fork's headers, protoc and libprotobuf: unbuildable here) and is a line-by-line restatement.
+ */
+#ifndef AVR_ORACLE_H
+#define AVR_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------------ */
+/* growable byte buffer                                                                        */
+typedef struct {
+  uint8_t *data;
+  size_t len, cap;
+} obuf_t;
+void ob_init(obuf_t *b);
+void ob_free(obuf_t *b);
+void ob_put(obuf_t *b, uint8_t v);
+void ob_append(obuf_t *b, const uint8_t *p, size_t n);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Generic arithmetic coder, arithmetic_code.h:31-299.                                          */
+/* One struct serves both instantiations used by the reference:                                */
+/*   recoded:  <uint64_t, uint8_t, 0>        (recode.cpp:315-316)                               */
+/*   cabac:    <uint32_t, uint16_t, 0x200> with uint8_t output digits (cabac_code.h:24,83)      */
+typedef struct {
+  uint64_t fixed_one;     /* 2^(bits-1) */
+  int digit_bits;         /* CompressedDigit width in bits (8 or 16) */
+  int out_bits;           /* OutputDigit width in bits (8) */
+  uint64_t min_range;
+  uint64_t low, range;
+  uint16_t *overflow;     /* deferred CompressedDigits (arith:200) */
+  size_t novf, capovf;
+  size_t bytes_emitted;
+  obuf_t *out;
+} ac_enc_t;
+
+void ac_enc_init(ac_enc_t *e, obuf_t *out, int fixed_bits, int digit_bits, uint64_t min_range,
+                 uint64_t initial_range);
+/* put(symbol, range_of_1) — range_of_1 must be computed by the caller from e->range. */
+size_t ac_enc_put(ac_enc_t *e, int symbol, uint64_t range_of_1);
+void ac_enc_finish(ac_enc_t *e);
+void ac_enc_free(ac_enc_t *e);
+
+typedef struct {
+  uint64_t fixed_one, min_range, digit_base, digit_alignment;
+  int digit_bytes;
+  uint64_t low, range, next_digit;
+  const uint8_t *in, *end;
+} ac_dec_t;
+void ac_dec_init(ac_dec_t *d, const uint8_t *in, const uint8_t *end, int fixed_bits, int digit_bits,
+                 uint64_t min_range);
+int ac_dec_get(ac_dec_t *d, uint64_t range_of_1);
+
+/* recoded coder helpers: recode.cpp:816-820 probability (range/total)*pos */
+static inline uint64_t rc_p1(uint64_t range, int pos, int neg) {
+  return (range / (uint64_t)(pos + neg)) * (uint64_t)pos;
+}
+void rc_enc_init(ac_enc_t *e, obuf_t *out);
+void rc_dec_init(ac_dec_t *d, const uint8_t *in, size_t n);
+
+/* ------------------------------------------------------------------------------------------ */
+/* CABAC tables (ITU-T H.264 Tables 9-12..9-33, 9-44, 9-45) in FFmpeg layout                   */
+extern uint8_t avr_lps_range[4 * 128];    /* [q*128 + state], state=(pStateIdx<<1)|valMPS  */
+extern uint8_t avr_mlps_state[256];         /* [128+s] after MPS, [127-s] after LPS          */
+/* init state bytes for 1024 contexts; init_idc = -1 for I/SI slices, 0..2 otherwise           */
+void avr_cabac_init_states(uint8_t state[1024], int init_idc, int slice_qp);
+
+/* CABAC re-encoder, cabac_code.h:27-80 */
+typedef struct {
+  ac_enc_t e;
+} cabac_enc_t;
+void cabac_enc_init(cabac_enc_t *c, obuf_t *out);
+size_t cabac_enc_put(cabac_enc_t *c, int symbol, uint8_t *state);
+size_t cabac_enc_put_bypass(cabac_enc_t *c, int symbol);
+size_t cabac_enc_put_terminate(cabac_enc_t *c, int symbol);
+void cabac_enc_free(cabac_enc_t *c);
+
+/* CABAC decoding engine, ITU-T H.264 9.3.1.2 / 9.3.3.2 (ff_get_cabac & co, fork) */
+typedef struct {
+  const uint8_t *buf;
+  size_t nbits;     /* payload size in bits */
+  size_t pos;       /* next bit to read */
+  uint32_t range, offset;
+  int overrun;      /* bits read past the end */
+} cabac_dec_t;
+void cabac_dec_init(cabac_dec_t *d, const uint8_t *buf, size_t n);
+int cabac_dec_decision(cabac_dec_t *d, uint8_t *state);
+int cabac_dec_bypass(cabac_dec_t *d);
+int cabac_dec_terminate(cabac_dec_t *d);
+
+/* ------------------------------------------------------------------------------------------ */
+/* H.264 front end                                                                             */
+typedef struct {
+  int valid;
+  int profile_idc, chroma_format_idc, separate_colour_plane, bit_depth_luma, bit_depth_chroma;
+  int log2_max_frame_num, poc_type, log2_max_poc_lsb, delta_pic_order_always_zero;
+  int frame_mbs_only, mb_aff, direct_8x8_inference;
+  int mb_width, mb_height; /* in MBs (frame) */
+} avr_sps_t;
+
+typedef struct {
+  int valid;
+  int sps_id, entropy_coding_mode, bottom_field_pic_order_present, num_slice_groups;
+  int num_ref_idx_default[2], weighted_pred, weighted_bipred_idc, pic_init_qp;
+  int deblocking_filter_control_present, constrained_intra_pred, redundant_pic_cnt_present;
+  int transform_8x8_mode;
+} avr_pps_t;
+
+enum { AVR_SLICE_P = 0, AVR_SLICE_B = 1, AVR_SLICE_I = 2, AVR_SLICE_SP = 3, AVR_SLICE_SI = 4 };
+
+typedef struct {
+  int nal_unit_type, nal_ref_idc;
+  int first_mb, slice_type, pps_id, frame_num, field_pic, bottom_field, idr_pic_id, poc_lsb;
+  int direct_spatial, num_ref_idx_active[2], cabac_init_idc, slice_qp;
+  int mbaff;
+  /* derived */
+  int chroma_array_type, transform_8x8_mode, direct_8x8_inference, mb_width, mb_height;
+  int constrained_intra_pred;
+  int x264_build;      /* from the x264 SEI user data, -1 if absent (FFmpeg h->x264_build) */
+  size_t cabac_start;  /* byte offset of slice_data() in the unescaped RBSP */
+  int supported;       /* 0 = the walker cannot parse this slice (MBAFF, field, FMO, ...) */
+} avr_slice_hdr_t;
+
+/* unescape an H.264 NAL payload (emulation prevention), FFmpeg 2.8 ff_h264_decode_nal rules */
+size_t avr_nal_unescape(const uint8_t *src, size_t n, uint8_t *dst);
+/* FFmpeg RBSP bit length rule: trailing zero bytes stripped, stop bit excluded */
+size_t avr_rbsp_bit_length(const uint8_t *rbsp, size_t n);
+
+typedef struct {
+  avr_sps_t sps[32];
+  avr_pps_t pps[256];
+} avr_param_sets_t;
+int avr_parse_sps(avr_param_sets_t *ps, const uint8_t *rbsp, size_t n);
+int avr_parse_pps(avr_param_sets_t *ps, const uint8_t *rbsp, size_t n);
+/* FFmpeg decode_unregistered_user_data: "x264 - core %d" in an SEI user_data_unregistered */
+int avr_parse_sei_x264_build(const uint8_t *rbsp, size_t n);
+int avr_parse_slice_header(const avr_param_sets_t *ps, const uint8_t *rbsp, size_t n,
+                           int nal_unit_type, int nal_ref_idc, avr_slice_hdr_t *h);
+
+/* a NAL unit located in the file */
+typedef struct {
+  size_t offset;   /* file offset of the NAL header byte */
+  size_t size;     /* escaped size incl. header byte */
+} avr_nal_t;
+/* Enumerate the video NAL units of an MP4 (avcC) or Annex-B file in decode order.
+ * Returns count, *out malloc'd.  avcC parameter sets are returned first with offset into file. */
+int avr_demux(const uint8_t *file, size_t n, avr_nal_t **out);
+
+/* ------------------------------------------------------------------------------------------ */
+/* The hook surface the parser drives — AVCodecHooks (recode.cpp:137-228, signatures of the   */
+/* libavcodec-hooks fork).  CodingType identity follows EACH_PIP_CODING_TYPE usage.            */
+typedef enum {
+  PIP_UNKNOWN = 0,
+  PIP_UNREACHABLE,
+  PIP_SIGNIFICANCE_MAP,
+  PIP_SIGNIFICANCE_EOB,
+  PIP_SIGNIFICANCE_NZ,
+  PIP_RESIDUALS,
+} avr_coding_type;
+
+typedef struct {
+  void *opaque;
+  /* cabac hooks: return the bin; ctx_idx names FFmpeg's cabac_state[] slot */
+  int (*get)(void *opaque, uint8_t *state, int ctx_idx);
+  int (*get_bypass)(void *opaque);
+  int (*get_terminate)(void *opaque);
+  /* model hooks */
+  void (*frame_spec)(void *opaque, int frame_num, int mb_width, int mb_height);
+  void (*mb_xy)(void *opaque, int x, int y);
+  void (*begin_sub_mb)(void *opaque, int cat, int scan8index, int max_coeff, int is_dc, int chroma422);
+  void (*end_sub_mb)(void *opaque, int cat, int scan8index, int max_coeff, int is_dc, int chroma422);
+  void (*begin_coding_type)(void *opaque, avr_coding_type ct, int zigzag_index, int param0, int param1);
+  void (*end_coding_type)(void *opaque, avr_coding_type ct);
+} avr_hooks_t;
+
+/* Parse slice_data() of one slice, pulling every bin through hooks.  The parser owns the     */
+/* 1024 CABAC context bytes (FFmpeg's sl->cabac_state).  Returns 0 on success (end_of_slice   */
+/* reached at a legal MB), <0 on a syntax error / unsupported syntax / overrun.               */
+int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int picture_id);
+
+/* ------------------------------------------------------------------------------------------ */
+/* The predictor (recode.cpp:615-1059) and the two drivers                                   */
+enum { AVR_MODE_R = 0, AVR_MODE_P = 1 };
+
+typedef struct avr_model avr_model_t;
+avr_model_t *avr_model_new(void);
+void avr_model_free(avr_model_t *m);
+
+/* Whole-file drivers.  out is malloc'd.  Return 0 on success. */
+int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t *out_len);
+int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len);
+
+/* Per-slice statistics for tests and the CPU baseline */
+typedef struct {
+  size_t file_bytes, slices, coded_slices, skipped_slices, payload_bytes, recoded_bytes, bins;
+} avr_stats_t;
+extern avr_stats_t avr_last_stats;
+
+/* ------------------------------------------------------------------------------------------ */
+/* Slice-level API used by the tests to cross-check the GPU kernels slice by slice.          */
+/* Compress one CABAC slice payload with a FRESH model (P-mode semantics).                   */
+int avr_compress_slice_p(const avr_slice_hdr_t *h, const uint8_t *payload, size_t n, obuf_t *recoded,
+                         size_t *bins);
+/* Decompress one slice (P-mode): regenerate the CABAC bytes (before the last-byte patch).   */
+int avr_decompress_slice_p(const avr_slice_hdr_t *h, const uint8_t *recoded, size_t n, obuf_t *cabac);
+/* Regenerate CABAC bytes by decode+re-encode (no model): the parser/engine self-check.      */
+int avr_cabac_regenerate(const avr_slice_hdr_t *h, const uint8_t *payload, size_t n, obuf_t *cabac,
+                         size_t *bins, size_t *end_bitpos);
+
+/* Synthetic slice generator: walks slice_data with seeded random bin choices and CABAC-encodes */
+/* them (used to build goldens and the CPU-baseline corpus).                                   */
+int avr_generate_slice(const avr_slice_hdr_t *h, uint64_t seed, int target_mbs, obuf_t *payload);
+
+/* protobuf wire codec for recode.proto */
+typedef struct {
+  int64_t size;
+  int has_size, has_literal, has_skip, has_cabac, has_parity, has_last_byte;
+  int skip_coded, length_parity;
+  const uint8_t *literal;
+  size_t literal_len;
+  const uint8_t *cabac;
+  size_t cabac_len;
+  uint8_t last_byte;
+  int last_byte_len;
+} avr_pb_block_t;
+void avr_pb_put_block(obuf_t *o, const avr_pb_block_t *b);
+/* model mode recorded in Recoded.metadata.version (R-mode: absent, as the reference writes) */
+int avr_pb_mode(const uint8_t *in, size_t n);
+/* parses a Recoded message; returns block count, *blocks malloc'd (pointers into in) */
+int avr_pb_parse(const uint8_t *in, size_t n, avr_pb_block_t **blocks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

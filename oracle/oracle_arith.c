@@ -1,0 +1,272 @@
+/*
+ * Oracle: arithmetic coders.  TEST INFRASTRUCTURE ONLY (see avr_oracle.h).
+ *
+ * ac_enc_* / ac_dec_*  restate arithmetic_code.h:31-299 literally, including the unbounded
+ *                      "overflow" digit vector (arith:155-174, 200) so that the restatement can be
+ *                      compared against the header compiled as-is (oracle/_ref/ref_arith).
+ * cabac_enc_*          restates cabac_code.h:27-80.
+ * cabac_dec_*          restates the ITU-T H.264 9.3.1.2 / 9.3.3.2 decoding engine that the
+ *                      libavcodec-hooks fork exposes as ff_get_cabac* (recode.cpp:1176-1188).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "avr_oracle.h"
+
+void ob_init(obuf_t *b) { b->data = NULL; b->len = b->cap = 0; }
+void ob_free(obuf_t *b) { free(b->data); ob_init(b); }
+static void ob_reserve(obuf_t *b, size_t n) {
+  if (b->len + n <= b->cap) return;
+  size_t c = b->cap ? b->cap : 256;
+  while (c < b->len + n) c *= 2;
+  b->data = (uint8_t *)realloc(b->data, c);
+  b->cap = c;
+}
+void ob_put(obuf_t *b, uint8_t v) { ob_reserve(b, 1); b->data[b->len++] = v; }
+void ob_append(obuf_t *b, const uint8_t *p, size_t n) {
+  if (!n) return;
+  ob_reserve(b, n);
+  memcpy(b->data + b->len, p, n);
+  b->len += n;
+}
+
+/* ---------------------------------------------------------------- generic encoder (arith:89-203) */
+void ac_enc_init(ac_enc_t *e, obuf_t *out, int fixed_bits, int digit_bits, uint64_t min_range,
+                 uint64_t initial_range) {
+  e->fixed_one = 1ull << (fixed_bits - 1);                   /* arith:54-55 */
+  e->digit_bits = digit_bits;
+  e->out_bits = 8;
+  /* arith:60-61: MinRange > 0 ? MinRange : (fixed_one/digit_base)/16 */
+  e->min_range = min_range ? min_range : ((e->fixed_one >> digit_bits) / 16);
+  e->low = 0;
+  e->range = initial_range ? initial_range : e->fixed_one;  /* arith:96-98 */
+  e->overflow = NULL;
+  e->novf = e->capovf = 0;
+  e->bytes_emitted = 0;
+  e->out = out;
+}
+
+void ac_enc_free(ac_enc_t *e) { free(e->overflow); e->overflow = NULL; e->novf = e->capovf = 0; }
+
+/* emit_digit<Digit> (arith:178-184): big-endian split into OutputDigits; bills sizeof(digit) */
+static void emit_digit(ac_enc_t *e, uint32_t digit, int bits) {
+  for (int i = bits - 8; i >= 0; i -= 8) ob_put(e->out, (uint8_t)(digit >> i));
+  e->bytes_emitted += (size_t)(bits / 8);
+}
+
+/* renormalize_and_emit_digit<Digit> (arith:146-175) */
+static void renorm_emit(ac_enc_t *e, int bits) {
+  const uint64_t base = 1ull << bits;
+  const uint64_t msd = e->fixed_one / base;
+  const uint32_t dmask = (uint32_t)(base - 1);
+  const uint16_t cmask = (uint16_t)((1u << e->digit_bits) - 1);
+  if (e->low >= e->fixed_one) {  /* carry cascades from the lowest overflow digit upward */
+    for (long i = (long)e->novf - 1; i >= 0; i--) {
+      e->overflow[i] = (uint16_t)((e->overflow[i] + 1) & cmask);
+      if (e->overflow[i] != 0) break;
+    }
+    e->low -= e->fixed_one;
+  }
+  uint32_t digit = (uint32_t)(e->low / msd) & dmask;
+  uint32_t top = (uint32_t)((e->low + e->range - 1) / msd) & dmask;
+  if (digit != top) {
+    if (e->novf == e->capovf) {
+      e->capovf = e->capovf ? 2 * e->capovf : 16;
+      e->overflow = (uint16_t *)realloc(e->overflow, e->capovf * sizeof(uint16_t));
+    }
+    e->overflow[e->novf++] = (uint16_t)digit;
+  } else {
+    for (size_t i = 0; i < e->novf; i++) emit_digit(e, e->overflow[i], e->digit_bits);
+    e->novf = 0;
+    emit_digit(e, digit, bits);
+  }
+  e->low -= (uint64_t)digit * msd;
+  e->low *= base;
+  e->range *= base;
+}
+
+/* encoder::put (arith:106-126) */
+size_t ac_enc_put(ac_enc_t *e, int symbol, uint64_t range_of_1) {
+  uint64_t range_of_0 = e->range - range_of_1;
+  if (symbol != 0) {
+    e->low += range_of_0;
+    e->range = range_of_1;
+  } else {
+    e->range = range_of_0;
+  }
+  if (e->range < e->min_range) {
+    if (e->range == 0) abort(); /* "Encoder error: emitted a zero-probability symbol." */
+    size_t before = e->bytes_emitted;
+    while (e->range < e->fixed_one / (1ull << e->digit_bits)) renorm_emit(e, e->digit_bits);
+    return e->bytes_emitted - before;
+  }
+  return 0;
+}
+
+/* encoder::finish (arith:128-144) */
+void ac_enc_finish(ac_enc_t *e) {
+  if (e->range == 0) return; /* already finished (destructor's second call is a no-op) */
+  for (uint64_t stop_bit = e->fixed_one >> 1; stop_bit > 0; stop_bit >>= 1) {
+    uint64_t x = (e->low | stop_bit) & ~(stop_bit - 1);
+    if (stop_bit < e->range && e->low <= x && x < e->low + e->range) {
+      e->low = x;
+      break;
+    }
+  }
+  while (e->low != 0) {
+    e->range = 1;
+    renorm_emit(e, e->out_bits);
+  }
+  e->range = 0;
+}
+
+/* ---------------------------------------------------------------- generic decoder (arith:211-298) */
+static uint64_t consume_aligned(ac_dec_t *d) {
+  uint64_t digit = 0;
+  for (int i = 0; i < d->digit_bytes; i++) {
+    digit <<= 8;
+    if (d->in != d->end) digit |= *d->in++;  /* reads past the end return 0 */
+  }
+  return digit;
+}
+static uint64_t consume_digit(ac_dec_t *d) {
+  uint64_t in = consume_aligned(d);
+  uint64_t digit = ((d->next_digit * (d->digit_base / d->digit_alignment)) |
+                    (in / d->digit_alignment)) & (d->digit_base - 1);
+  d->next_digit = in;
+  return digit;
+}
+static void renorm_consume(ac_dec_t *d) {
+  uint64_t digit = consume_digit(d);
+  d->low = d->low * d->digit_base + digit;
+  d->range *= d->digit_base;
+}
+
+void ac_dec_init(ac_dec_t *d, const uint8_t *in, const uint8_t *end, int fixed_bits, int digit_bits,
+                 uint64_t min_range) {
+  d->fixed_one = 1ull << (fixed_bits - 1);
+  d->digit_base = 1ull << digit_bits;
+  d->digit_bytes = digit_bits / 8;
+  d->min_range = min_range ? min_range : ((d->fixed_one >> digit_bits) / 16);
+  /* digit_alignment = max/fixed_one + 1 (arith:252) */
+  uint64_t maxv = fixed_bits == 64 ? ~0ull : ((1ull << fixed_bits) - 1);
+  d->digit_alignment = maxv / d->fixed_one + 1;
+  d->in = in;
+  d->end = end;
+  d->next_digit = consume_aligned(d);
+  d->low = d->next_digit / d->digit_alignment;
+  d->range = d->digit_base / d->digit_alignment;
+  while (d->range < d->fixed_one) renorm_consume(d);
+}
+
+int ac_dec_get(ac_dec_t *d, uint64_t range_of_1) {
+  uint64_t range_of_0 = d->range - range_of_1;
+  int symbol = d->low >= range_of_0;
+  if (symbol) {
+    d->low -= range_of_0;
+    d->range = range_of_1;
+  } else {
+    d->range = range_of_0;
+  }
+  if (d->range < d->min_range) {
+    while (d->range < d->fixed_one / d->digit_base) renorm_consume(d);
+  }
+  return symbol;
+}
+
+/* recoded_code = arithmetic_code<uint64_t, uint8_t> (recode.cpp:315-316) */
+void rc_enc_init(ac_enc_t *e, obuf_t *out) { ac_enc_init(e, out, 64, 8, 0, 0); }
+void rc_dec_init(ac_dec_t *d, const uint8_t *in, size_t n) { ac_dec_init(d, in, in + n, 64, 8, 0); }
+
+/* ---------------------------------------------------------------- CABAC re-encoder (cabac_code.h) */
+static int ilog2_u64(uint64_t x) { /* cabac_code.h:70-79 */
+  int i = 0;
+  if (x >> 32) { x >>= 32; i += 32; }
+  if (x >> 16) { x >>= 16; i += 16; }
+  if (x >> 8) { x >>= 8; i += 8; }
+  if (x >> 4) { x >>= 4; i += 4; }
+  if (x >> 2) { x >>= 2; i += 2; }
+  if (x >> 1) { i += 1; }
+  return i;
+}
+
+void cabac_enc_init(cabac_enc_t *c, obuf_t *out) {
+  /* arithmetic_code<uint32_t, uint16_t, 0x200>, initial range (fixed_one/0x200)*0x1FE (cabac_code.h:30) */
+  ac_enc_init(&c->e, out, 32, 16, 0x200, ((1ull << 31) / 0x200) * 0x1FE);
+}
+void cabac_enc_free(cabac_enc_t *c) { ac_enc_free(&c->e); }
+
+size_t cabac_enc_put(cabac_enc_t *c, int symbol, uint8_t *state) { /* cabac_code.h:33-49 */
+  int lps = symbol != (*state & 1);
+  uint64_t range = c->e.range;
+  int normalize = ilog2_u64(range / 0x100);
+  int range_approx = (int)(range >> (normalize - 1));
+  uint64_t r1 = (uint64_t)avr_lps_range[(range_approx & 0x180) + *state] << normalize;
+  size_t ret = ac_enc_put(&c->e, lps, r1);
+  *state = lps ? avr_mlps_state[127 - *state] : avr_mlps_state[128 + *state];
+  return ret;
+}
+size_t cabac_enc_put_bypass(cabac_enc_t *c, int symbol) { /* cabac_code.h:52-54 */
+  return ac_enc_put(&c->e, symbol, c->e.range / 2);
+}
+size_t cabac_enc_put_terminate(cabac_enc_t *c, int symbol) { /* cabac_code.h:57-67 */
+  int normalize = ilog2_u64(c->e.range / 0x100);
+  size_t ret = ac_enc_put(&c->e, symbol, 2ull << normalize);
+  if (symbol) ac_enc_finish(&c->e);
+  return ret;
+}
+
+/* ---------------------------------------------------------------- CABAC decoding engine (9.3) */
+static inline uint32_t rd_bit(cabac_dec_t *d) {
+  uint32_t b = 0;
+  if (d->pos < d->nbits) b = (d->buf[d->pos >> 3] >> (7 - (d->pos & 7))) & 1;
+  else d->overrun++;
+  d->pos++;
+  return b;
+}
+void cabac_dec_init(cabac_dec_t *d, const uint8_t *buf, size_t n) { /* 9.3.1.2 */
+  d->buf = buf;
+  d->nbits = n * 8;
+  d->pos = 0;
+  d->overrun = 0;
+  d->range = 510;
+  d->offset = 0;
+  for (int i = 0; i < 9; i++) d->offset = (d->offset << 1) | rd_bit(d);
+}
+int cabac_dec_decision(cabac_dec_t *d, uint8_t *state) { /* 9.3.3.2.1 */
+  uint32_t s = *state;
+  uint32_t lps = avr_lps_range[((d->range >> 6) & 3) * 128 + s];
+  int bin;
+  d->range -= lps;
+  if (d->offset >= d->range) {
+    bin = !(s & 1);
+    d->offset -= d->range;
+    d->range = lps;
+    *state = avr_mlps_state[127 - s];
+  } else {
+    bin = s & 1;
+    *state = avr_mlps_state[128 + s];
+  }
+  while (d->range < 256) {
+    d->range <<= 1;
+    d->offset = (d->offset << 1) | rd_bit(d);
+  }
+  return bin;
+}
+int cabac_dec_bypass(cabac_dec_t *d) { /* 9.3.3.2.3 */
+  d->offset = (d->offset << 1) | rd_bit(d);
+  if (d->offset >= d->range) {
+    d->offset -= d->range;
+    return 1;
+  }
+  return 0;
+}
+int cabac_dec_terminate(cabac_dec_t *d) { /* 9.3.3.2.2.3 */
+  d->range -= 2;
+  if (d->offset >= d->range) return 1; /* no renormalisation; last bit read = rbsp_stop_one_bit */
+  while (d->range < 256) {
+    d->range <<= 1;
+    d->offset = (d->offset << 1) | rd_bit(d);
+  }
+  return 0;
+}

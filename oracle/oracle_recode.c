@@ -1,0 +1,694 @@
+/*
+ * Oracle: per-slice drivers, container and whole-file pipelines.  TEST INFRASTRUCTURE ONLY.
+ *
+ *   h264_symbol::execute              recode.cpp:1061-1100
+ *   compressor::cabac_decoder         recode.cpp:1134-1268
+ *   compressor::run / find_next_...   recode.cpp:1115-1132, 1275-1297
+ *   decompressor::cabac_decoder       recode.cpp:1411-1520
+ *   decompressor::run / read_packet / next_surrogate_marker / recognize_coded_block
+ *                                     recode.cpp:1338-1409, 1527-1573
+ *   recode.proto wire format          (proto2; field order as SerializeAsString writes it)
+ *
+ * The av_decoder / FFmpeg plumbing (recode.cpp:73-230) is replaced by a direct walk of the
+ * file's slice NAL units (oracle_bits.c) in decode order, calling the same hooks.
+ *
+ * Deviations:
+ *   - a slice is re-coded only if a CABAC re-encode + the decompressor's last-byte rule reproduces
+ *     the payload (checked before the model sees it); otherwise it becomes skip_coded, where the
+ *     reference would emit a block its own decompressor cannot restore;
+ *   - I_PCM / MBAFF / field slices become skip_coded (the reference throws on I_PCM);
+ *   - the memmem window is [prev_coded_block_end, end of file) (FFmpeg's AVIO read_offset).
+ */
+#define _GNU_SOURCE
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle_model.h"
+
+avr_stats_t avr_last_stats;
+static const int SURROGATE_MARKER_BYTES = 8; /* recode.cpp:27 */
+#define AVR_P_MODE_TAG "avrecode-amd:P"
+
+/* ===================================================================== protobuf wire codec */
+static void pb_varint(obuf_t *o, uint64_t v) {
+  while (v >= 0x80) { ob_put(o, (uint8_t)(v | 0x80)); v >>= 7; }
+  ob_put(o, (uint8_t)v);
+}
+static void pb_bytes(obuf_t *o, int field, const uint8_t *p, size_t n) {
+  pb_varint(o, (uint64_t)field << 3 | 2);
+  pb_varint(o, n);
+  ob_append(o, p, n);
+}
+void avr_pb_put_block(obuf_t *o, const avr_pb_block_t *b) {
+  obuf_t m;
+  ob_init(&m);
+  if (b->has_size) { pb_varint(&m, 1 << 3 | 0); pb_varint(&m, (uint64_t)b->size); }
+  if (b->has_literal) pb_bytes(&m, 2, b->literal, b->literal_len);
+  if (b->has_skip) { pb_varint(&m, 3 << 3 | 0); pb_varint(&m, (uint64_t)b->skip_coded); }
+  if (b->has_cabac) pb_bytes(&m, 4, b->cabac, b->cabac_len);
+  if (b->has_parity) { pb_varint(&m, 5 << 3 | 0); pb_varint(&m, (uint64_t)b->length_parity); }
+  if (b->has_last_byte) pb_bytes(&m, 6, &b->last_byte, (size_t)b->last_byte_len);
+  pb_bytes(o, 2, m.data, m.len);
+  ob_free(&m);
+}
+
+static int pb_rd_varint(const uint8_t **p, const uint8_t *e, uint64_t *v) {
+  *v = 0;
+  for (int s = 0; s < 64; s += 7) {
+    if (*p >= e) return -1;
+    uint8_t c = *(*p)++;
+    *v |= (uint64_t)(c & 0x7f) << s;
+    if (!(c & 0x80)) return 0;
+  }
+  return -1;
+}
+static int pb_skip(const uint8_t **p, const uint8_t *e, int wt) {
+  uint64_t v;
+  switch (wt) {
+    case 0: return pb_rd_varint(p, e, &v);
+    case 1: if (e - *p < 8) return -1; *p += 8; return 0;
+    case 2: if (pb_rd_varint(p, e, &v) || (uint64_t)(e - *p) < v) return -1; *p += v; return 0;
+    case 5: if (e - *p < 4) return -1; *p += 4; return 0;
+    default: return -1;
+  }
+}
+static int pb_parse_block(const uint8_t *p, const uint8_t *e, avr_pb_block_t *b) {
+  memset(b, 0, sizeof(*b));
+  while (p < e) {
+    uint64_t tag, v;
+    if (pb_rd_varint(&p, e, &tag)) return -1;
+    int field = (int)(tag >> 3), wt = (int)(tag & 7);
+    if (wt == 0 && (field == 1 || field == 3 || field == 5)) {
+      if (pb_rd_varint(&p, e, &v)) return -1;
+      if (field == 1) { b->has_size = 1; b->size = (int64_t)v; }
+      if (field == 3) { b->has_skip = 1; b->skip_coded = v != 0; }
+      if (field == 5) { b->has_parity = 1; b->length_parity = v != 0; }
+    } else if (wt == 2 && (field == 2 || field == 4 || field == 6)) {
+      if (pb_rd_varint(&p, e, &v) || (uint64_t)(e - p) < v) return -1;
+      if (field == 2) { b->has_literal = 1; b->literal = p; b->literal_len = v; }
+      if (field == 4) { b->has_cabac = 1; b->cabac = p; b->cabac_len = v; }
+      if (field == 6) { b->has_last_byte = 1; b->last_byte_len = (int)v; b->last_byte = v ? p[0] : 0; }
+      p += v;
+    } else if (pb_skip(&p, e, wt)) {
+      return -1;
+    }
+  }
+  return 0;
+}
+/* Recoded.metadata.version == AVR_P_MODE_TAG -> P-mode, anything else R-mode */
+int avr_pb_mode(const uint8_t *in, size_t n) {
+  const uint8_t *p = in, *e = in + n;
+  int mode = AVR_MODE_R;
+  while (p < e) {
+    uint64_t tag, len;
+    if (pb_rd_varint(&p, e, &tag)) return mode;
+    if ((tag & 7) != 2) { if (pb_skip(&p, e, (int)(tag & 7))) return mode; continue; }
+    if (pb_rd_varint(&p, e, &len) || (uint64_t)(e - p) < len) return mode;
+    if ((tag >> 3) == 1) {
+      const uint8_t *q = p, *qe = p + len;
+      while (q < qe) {
+        uint64_t t2, l2;
+        if (pb_rd_varint(&q, qe, &t2)) break;
+        if ((t2 & 7) != 2) { if (pb_skip(&q, qe, (int)(t2 & 7))) break; continue; }
+        if (pb_rd_varint(&q, qe, &l2) || (uint64_t)(qe - q) < l2) break;
+        if ((t2 >> 3) == 1) mode = (l2 == strlen(AVR_P_MODE_TAG) && !memcmp(q, AVR_P_MODE_TAG, l2)) ? AVR_MODE_P : AVR_MODE_R;
+        q += l2;
+      }
+    }
+    p += len;
+  }
+  return mode;
+}
+
+int avr_pb_parse(const uint8_t *in, size_t n, avr_pb_block_t **blocks) {
+  const uint8_t *p = in, *e = in + n;
+  int cnt = 0, cap = 0;
+  avr_pb_block_t *v = NULL;
+  while (p < e) {
+    uint64_t tag, len;
+    if (pb_rd_varint(&p, e, &tag)) goto fail;
+    if ((tag >> 3) == 2 && (tag & 7) == 2) {
+      if (pb_rd_varint(&p, e, &len) || (uint64_t)(e - p) < len) goto fail;
+      if (cnt == cap) { cap = cap ? 2 * cap : 64; v = (avr_pb_block_t *)realloc(v, (size_t)cap * sizeof(*v)); }
+      if (pb_parse_block(p, p + len, &v[cnt])) goto fail;
+      cnt++;
+      p += len;
+    } else if (pb_skip(&p, e, (int)(tag & 7))) {
+      goto fail;
+    }
+  }
+  *blocks = v;
+  return cnt;
+fail:
+  free(v);
+  *blocks = NULL;
+  return -1;
+}
+
+/* ============================================================ shared model-hook plumbing */
+static void h_frame_spec(void *o, int fn, int w, int h);
+static void h_mb_xy(void *o, int x, int y);
+static void h_begin_sub_mb(void *o, int cat, int idx, int max, int is_dc, int c422);
+static void h_end_sub_mb(void *o, int cat, int idx, int max, int is_dc, int c422);
+
+/* every driver starts with the model pointer so the model hooks can be shared */
+typedef struct { avr_model_t *model; } drv_base_t;
+static void h_frame_spec(void *o, int fn, int w, int h) {
+  avr_model_t *m = ((drv_base_t *)o)->model;
+  if (m) model_update_frame_spec(m, fn, w, h);
+}
+static void h_mb_xy(void *o, int x, int y) {
+  avr_model_t *m = ((drv_base_t *)o)->model;
+  if (m) { m->mb_x = x; m->mb_y = y; }
+}
+static void h_begin_sub_mb(void *o, int cat, int idx, int max, int is_dc, int c422) {
+  avr_model_t *m = ((drv_base_t *)o)->model;
+  if (!m) return;
+  m->sub_mb_cat = cat;
+  m->scan8_index = idx;
+  m->sub_mb_size = max;
+  m->sub_mb_is_dc = is_dc;
+  m->sub_mb_chroma422 = c422;
+}
+static void h_end_sub_mb(void *o, int cat, int idx, int max, int is_dc, int c422) {
+  avr_model_t *m = ((drv_base_t *)o)->model;
+  if (!m) return;
+  if (m->sub_mb_cat != cat || m->scan8_index != idx || m->sub_mb_size != max || m->sub_mb_is_dc != is_dc ||
+      m->sub_mb_chroma422 != c422)
+    abort(); /* asserts at recode.cpp:185-189 */
+  m->sub_mb_cat = -1;
+  m->scan8_index = -1;
+  m->sub_mb_size = -1;
+  m->sub_mb_is_dc = 0;
+  m->sub_mb_chroma422 = 0;
+}
+
+/* ===================================================== compressor::cabac_decoder (1134-1268) */
+typedef struct {
+  avr_model_t *model;
+  cabac_dec_t dec;
+  obuf_t enc_out;
+  ac_enc_t enc;
+  int queueing;
+  int *bsym, *bctx, nbuf, capbuf;
+  int finished;
+  size_t bins;
+} cdrv_t;
+
+static void c_execute(cdrv_t *c, int symbol, int ctx) { /* h264_symbol::execute (1068-1096) */
+  avr_model_t *m = c->model;
+  if (m->coding_type != PIP_SIGNIFICANCE_EOB) {
+    size_t billable = ac_enc_put(&c->enc, symbol, model_p1(m, c->enc.range, model_get_key(m, ctx)));
+    m->bill[m->coding_type] += billable;
+  }
+  model_update_state(m, symbol, ctx);
+  if (ctx == K_TERMINATE && symbol) {
+    ac_enc_finish(&c->enc);
+    c->finished = 1;
+  }
+}
+static void c_execute_symbol(cdrv_t *c, int symbol, int ctx) { /* 1160-1173 */
+  c->bins++;
+  if (c->queueing == PIP_SIGNIFICANCE_MAP || c->queueing == PIP_SIGNIFICANCE_EOB || c->nbuf) {
+    if (c->nbuf == c->capbuf) {
+      c->capbuf = c->capbuf ? 2 * c->capbuf : 256;
+      c->bsym = (int *)realloc(c->bsym, (size_t)c->capbuf * sizeof(int));
+      c->bctx = (int *)realloc(c->bctx, (size_t)c->capbuf * sizeof(int));
+    }
+    c->bsym[c->nbuf] = symbol;
+    c->bctx[c->nbuf++] = ctx;
+    model_update_tracking(c->model, symbol);
+  } else {
+    c_execute(c, symbol, ctx);
+  }
+}
+static int c_get(void *o, uint8_t *state, int ctx) {
+  cdrv_t *c = (cdrv_t *)o;
+  int s = cabac_dec_decision(&c->dec, state);
+  c_execute_symbol(c, s, ctx);
+  return s;
+}
+static int c_get_bypass(void *o) {
+  cdrv_t *c = (cdrv_t *)o;
+  int s = cabac_dec_bypass(&c->dec);
+  c_execute_symbol(c, s, K_BYPASS);
+  return s;
+}
+static int c_get_terminate(void *o) {
+  cdrv_t *c = (cdrv_t *)o;
+  int s = cabac_dec_terminate(&c->dec) != 0;
+  c_execute_symbol(c, s, K_TERMINATE);
+  return s;
+}
+static void c_put_nz(void *ctx, avr_model_t *m, model_key_t key, int *symbol) { /* 1213-1221 */
+  cdrv_t *c = (cdrv_t *)ctx;
+  size_t billable = ac_enc_put(&c->enc, *symbol, model_p1(m, c->enc.range, key));
+  model_update_key(m, *symbol, key);
+  m->bill[m->coding_type] += billable;
+}
+static void c_begin_coding_type(void *o, avr_coding_type ct, int zz, int p0, int p1) {
+  cdrv_t *c = (cdrv_t *)o;
+  int begin_queue = model_begin_coding_type(c->model, ct);
+  if (begin_queue && (ct == PIP_SIGNIFICANCE_MAP || ct == PIP_SIGNIFICANCE_EOB)) {
+    if (c->queueing != PIP_UNKNOWN || c->nbuf) abort(); /* 1233-1235 */
+    c->queueing = ct;
+  }
+}
+static void c_end_coding_type(void *o, avr_coding_type ct) {
+  cdrv_t *c = (cdrv_t *)o;
+  model_end_coding_type(c->model, ct);
+  if (ct == PIP_SIGNIFICANCE_MAP || ct == PIP_SIGNIFICANCE_EOB) {
+    c->queueing = PIP_UNKNOWN;
+    model_finished_queueing(c->model, ct, c_put_nz, c);
+    model_reset_sig_tracking(c->model); /* pop_queueing_symbols (1244-1255) */
+    for (int i = 0; i < c->nbuf; i++) c_execute(c, c->bsym[i], c->bctx[i]);
+    c->nbuf = 0;
+    c->model->coding_type = PIP_UNKNOWN;
+  }
+}
+
+/* ==================================================== decompressor::cabac_decoder (1411-1520) */
+typedef struct {
+  avr_model_t *model;
+  ac_dec_t dec;
+  cabac_enc_t cenc;
+  obuf_t cabac_out;
+  int finished;
+} ddrv_t;
+
+static int d_get(void *o, uint8_t *state, int ctx) {
+  ddrv_t *d = (ddrv_t *)o;
+  avr_model_t *m = d->model;
+  int s;
+  if (m->coding_type == PIP_SIGNIFICANCE_EOB) {
+    model_key_t k = model_get_key(m, ctx);
+    s = (int)((k >> 24) & 0xffffff); /* std::get<1>(key) */
+  } else {
+    s = ac_dec_get(&d->dec, model_p1(m, d->dec.range, model_get_key(m, ctx)));
+  }
+  m->cabac_bill[m->coding_type] += cabac_enc_put(&d->cenc, s, state);
+  model_update_state(m, s, ctx);
+  return s;
+}
+static int d_get_bypass(void *o) {
+  ddrv_t *d = (ddrv_t *)o;
+  int s = ac_dec_get(&d->dec, model_p1(d->model, d->dec.range, model_get_key(d->model, K_BYPASS)));
+  model_update_state(d->model, s, K_BYPASS);
+  d->model->cabac_bill[d->model->coding_type] += cabac_enc_put_bypass(&d->cenc, s);
+  return s;
+}
+static int d_get_terminate(void *o) {
+  ddrv_t *d = (ddrv_t *)o;
+  int s = ac_dec_get(&d->dec, model_p1(d->model, d->dec.range, model_get_key(d->model, K_TERMINATE)));
+  model_update_state(d->model, s, K_TERMINATE);
+  d->model->cabac_bill[d->model->coding_type] += cabac_enc_put_terminate(&d->cenc, s);
+  if (s) {
+    if (d->cabac_out.len && d->cabac_out.data[d->cabac_out.len - 1] == 0x80) d->cabac_out.len--; /* 1503-1505 */
+    d->finished = 1;
+  }
+  return s;
+}
+static void d_get_nz(void *ctx, avr_model_t *m, model_key_t key, int *symbol) { /* 1481-1486 */
+  ddrv_t *d = (ddrv_t *)ctx;
+  *symbol = ac_dec_get(&d->dec, model_p1(m, d->dec.range, key));
+  model_update_key(m, *symbol, key);
+}
+static void d_begin_coding_type(void *o, avr_coding_type ct, int zz, int p0, int p1) {
+  ddrv_t *d = (ddrv_t *)o;
+  int begin_queue = model_begin_coding_type(d->model, ct);
+  if (begin_queue && ct) model_finished_queueing(d->model, ct, d_get_nz, d);
+}
+static void d_end_coding_type(void *o, avr_coding_type ct) {
+  ddrv_t *d = (ddrv_t *)o;
+  model_end_coding_type(d->model, ct);
+}
+
+/* ======================================= regenerate (decode + CABAC re-encode, no model) */
+typedef struct {
+  avr_model_t *model; /* NULL: model hooks are no-ops */
+  cabac_dec_t dec;
+  cabac_enc_t cenc;
+  obuf_t out;
+  size_t bins;
+  int finished;
+} rdrv_t;
+static int r_get(void *o, uint8_t *state, int ctx) {
+  rdrv_t *r = (rdrv_t *)o;
+  uint8_t before = *state;
+  int s = cabac_dec_decision(&r->dec, state);
+  uint8_t st = before;
+  cabac_enc_put(&r->cenc, s, &st);
+  r->bins++;
+  return s;
+}
+static int r_get_bypass(void *o) {
+  rdrv_t *r = (rdrv_t *)o;
+  int s = cabac_dec_bypass(&r->dec);
+  cabac_enc_put_bypass(&r->cenc, s);
+  r->bins++;
+  return s;
+}
+static int r_get_terminate(void *o) {
+  rdrv_t *r = (rdrv_t *)o;
+  int s = cabac_dec_terminate(&r->dec) != 0;
+  cabac_enc_put_terminate(&r->cenc, s);
+  r->bins++;
+  if (s) r->finished = 1;
+  return s;
+}
+static void nop_bct(void *o, avr_coding_type ct, int zz, int p0, int p1) {}
+static void nop_ect(void *o, avr_coding_type ct) {}
+
+/* the decompressor's finish + last-byte patch applied to regenerated bytes (1345-1356, 1501-1508) */
+static void apply_patch(obuf_t *out, size_t size, const uint8_t *payload) {
+  if (out->len && out->data[out->len - 1] == 0x80) out->len--;
+  if (size > 1) {
+    int parity = (int)(size & 1);
+    if (parity != (int)(out->len & 1)) ob_put(out, payload[size - 1]);
+    else if (out->len) out->data[out->len - 1] = payload[size - 1];
+  }
+}
+
+int avr_cabac_regenerate(const avr_slice_hdr_t *h, const uint8_t *rbsp_from_cabac, size_t n, obuf_t *cabac,
+                         size_t *bins, size_t *end_bitpos) {
+  rdrv_t r;
+  memset(&r, 0, sizeof(r));
+  cabac_dec_init(&r.dec, rbsp_from_cabac, n);
+  ob_init(&r.out);
+  cabac_enc_init(&r.cenc, &r.out);
+  avr_hooks_t hk = {&r, r_get, r_get_bypass, r_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
+                    h_end_sub_mb, nop_bct, nop_ect};
+  int ret = avr_walk_slice(h, &hk, 0);
+  cabac_enc_free(&r.cenc);
+  if (bins) *bins = r.bins;
+  if (end_bitpos) *end_bitpos = r.dec.pos;
+  if (ret == 0 && (!r.finished || r.dec.overrun)) ret = -20;
+  *cabac = r.out;
+  return ret;
+}
+
+/* ======================================================================= slice helpers */
+typedef struct {
+  avr_slice_hdr_t h;
+  uint8_t *rbsp;      /* unescaped NAL payload after the header byte */
+  size_t rbsp_len;
+  size_t size;        /* FFmpeg payload size (init_decoder's size) */
+  const uint8_t *payload;
+  int picture_id;
+} slice_t;
+
+typedef struct {
+  avr_param_sets_t ps;
+  int x264_build;
+  int have_prev, picture_id;
+  avr_slice_hdr_t prev;
+} stream_state_t;
+
+/* parse one NAL; returns 1 and fills *s for a CABAC slice that FFmpeg would hand to init_decoder */
+static int nal_to_slice(stream_state_t *st, const uint8_t *nal, size_t n, slice_t *s) {
+  if (n < 2) return 0;
+  int type = nal[0] & 0x1f, ref_idc = (nal[0] >> 5) & 3;
+  if (type != 1 && type != 5 && type != 6 && type != 7 && type != 8) return 0;
+  uint8_t *rbsp = (uint8_t *)malloc(n);
+  size_t rl = avr_nal_unescape(nal + 1, n - 1, rbsp);
+  if (type == 6) {
+    int b = avr_parse_sei_x264_build(rbsp, rl);
+    if (b > 0) st->x264_build = b;
+    free(rbsp);
+    return 0;
+  }
+  if (type == 7) { avr_parse_sps(&st->ps, rbsp, rl); free(rbsp); return 0; }
+  if (type == 8) { avr_parse_pps(&st->ps, rbsp, rl); free(rbsp); return 0; }
+  memset(s, 0, sizeof(*s));
+  if (avr_parse_slice_header(&st->ps, rbsp, rl, type, ref_idc, &s->h) != 0 ||
+      !st->ps.pps[s->h.pps_id].entropy_coding_mode) {
+    free(rbsp);
+    return 0;
+  }
+  s->h.x264_build = st->x264_build;
+  const avr_slice_hdr_t *p = &st->prev;
+  int new_pic = !st->have_prev || s->h.first_mb == 0 || s->h.first_mb <= p->first_mb ||
+                s->h.frame_num != p->frame_num || s->h.pps_id != p->pps_id || s->h.poc_lsb != p->poc_lsb ||
+                (s->h.nal_unit_type == 5) != (p->nal_unit_type == 5) || s->h.idr_pic_id != p->idr_pic_id ||
+                (s->h.nal_ref_idc == 0) != (p->nal_ref_idc == 0);
+  if (new_pic) st->picture_id++;
+  st->prev = s->h;
+  st->have_prev = 1;
+  s->picture_id = st->picture_id;
+  s->rbsp = rbsp;
+  s->rbsp_len = rl;
+  size_t bits = avr_rbsp_bit_length(rbsp, rl);
+  size_t end = (bits + 7) / 8;
+  s->size = end > s->h.cabac_start ? end - s->h.cabac_start : 0;
+  s->payload = rbsp + s->h.cabac_start;
+  return 1;
+}
+
+/* Pre-check: the slice parses and a CABAC re-encode + last-byte rule restores the payload. */
+static int slice_recodable(const slice_t *s) {
+  if (!s->h.supported || s->size < (size_t)SURROGATE_MARKER_BYTES) return 0;
+  obuf_t regen;
+  int r = avr_cabac_regenerate(&s->h, s->payload, s->rbsp_len - s->h.cabac_start, &regen, NULL, NULL);
+  int ok = 0;
+  if (r == 0) {
+    apply_patch(&regen, s->size, s->payload);
+    ok = regen.len == s->size && memcmp(regen.data, s->payload, s->size) == 0;
+  }
+  ob_free(&regen);
+  return ok;
+}
+
+static int compress_slice_with_model(avr_model_t *m, const slice_t *s, obuf_t *recoded, size_t *bins) {
+  cdrv_t c;
+  memset(&c, 0, sizeof(c));
+  c.model = m;
+  cabac_dec_init(&c.dec, s->payload, s->rbsp_len - s->h.cabac_start);
+  ob_init(&c.enc_out);
+  rc_enc_init(&c.enc, &c.enc_out);
+  c.queueing = PIP_UNKNOWN;
+  avr_hooks_t hk = {&c, c_get, c_get_bypass, c_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
+                    h_end_sub_mb, c_begin_coding_type, c_end_coding_type};
+  int ret = avr_walk_slice(&s->h, &hk, s->picture_id);
+  ac_enc_free(&c.enc);
+  free(c.bsym);
+  free(c.bctx);
+  if (ret == 0 && !c.finished) ret = -21;
+  *recoded = c.enc_out;
+  if (bins) *bins = c.bins;
+  return ret;
+}
+
+static int decompress_slice_with_model(avr_model_t *m, const avr_slice_hdr_t *h, int picture_id,
+                                       const uint8_t *rc, size_t rn, obuf_t *cabac) {
+  ddrv_t d;
+  memset(&d, 0, sizeof(d));
+  d.model = m;
+  m->decompress_side = 1;
+  rc_dec_init(&d.dec, rc, rn);
+  ob_init(&d.cabac_out);
+  cabac_enc_init(&d.cenc, &d.cabac_out);
+  avr_hooks_t hk = {&d, d_get, d_get_bypass, d_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
+                    h_end_sub_mb, d_begin_coding_type, d_end_coding_type};
+  int ret = avr_walk_slice(h, &hk, picture_id);
+  cabac_enc_free(&d.cenc);
+  if (ret == 0 && !d.finished) ret = -22;
+  *cabac = d.cabac_out;
+  return ret;
+}
+
+int avr_compress_slice_p(const avr_slice_hdr_t *h, const uint8_t *payload, size_t n, obuf_t *recoded, size_t *bins) {
+  slice_t s;
+  memset(&s, 0, sizeof(s));
+  s.h = *h;
+  s.payload = payload;
+  s.rbsp_len = n + h->cabac_start;
+  avr_model_t *m = avr_model_new();
+  int r = compress_slice_with_model(m, &s, recoded, bins);
+  avr_model_free(m);
+  return r;
+}
+int avr_decompress_slice_p(const avr_slice_hdr_t *h, const uint8_t *rc, size_t n, obuf_t *cabac) {
+  avr_model_t *m = avr_model_new();
+  int r = decompress_slice_with_model(m, h, 0, rc, n, cabac);
+  avr_model_free(m);
+  return r;
+}
+
+/* ========================================================================== compress */
+int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t *out_len) {
+  avr_nal_t *nals;
+  int nn = avr_demux(file, n, &nals);
+  if (nn < 0) return -1;
+  stream_state_t *st = (stream_state_t *)calloc(1, sizeof(stream_state_t));
+  st->x264_build = -1;
+  avr_model_t *model = mode == AVR_MODE_R ? avr_model_new() : NULL;
+  obuf_t o;
+  ob_init(&o);
+  if (mode == AVR_MODE_P) {
+    /* Recoded.Metadata.version (recode.proto:3) tags the parallel model; R-mode writes none,
+     * exactly like the reference (which never sets metadata). */
+    obuf_t md;
+    ob_init(&md);
+    pb_bytes(&md, 1, (const uint8_t *)AVR_P_MODE_TAG, strlen(AVR_P_MODE_TAG));
+    pb_bytes(&o, 1, md.data, md.len);
+    ob_free(&md);
+  }
+  size_t prev_end = 0;
+  memset(&avr_last_stats, 0, sizeof(avr_last_stats));
+  avr_last_stats.file_bytes = n;
+  for (int i = 0; i < nn; i++) {
+    slice_t s;
+    if (!nal_to_slice(st, file + nals[i].offset, nals[i].size, &s)) continue;
+    avr_last_stats.slices++;
+    /* find_next_coded_block_and_emit_literal (1275-1297) */
+    const uint8_t *found = s.size ? (const uint8_t *)memmem(file + prev_end, n - prev_end, s.payload, s.size) : NULL;
+    int coded = found && s.size >= (size_t)SURROGATE_MARKER_BYTES && slice_recodable(&s);
+    if (coded) {
+      size_t gap = (size_t)(found - (file + prev_end));
+      avr_pb_block_t lit = {0};
+      lit.has_literal = 1;
+      lit.literal = file + prev_end;
+      lit.literal_len = gap;
+      avr_pb_put_block(&o, &lit);
+      prev_end += gap + s.size;
+      avr_model_t *m = mode == AVR_MODE_R ? model : avr_model_new();
+      obuf_t rc;
+      size_t bins = 0;
+      int r = compress_slice_with_model(m, &s, &rc, &bins);
+      if (mode != AVR_MODE_R) avr_model_free(m);
+      if (r != 0) abort(); /* pre-check passed, so the walk must succeed */
+      avr_pb_block_t b = {0};
+      b.has_size = 1;
+      b.size = (int64_t)s.size;
+      b.has_parity = 1;
+      b.length_parity = (int)(s.size & 1);
+      if (s.size > 1) { b.has_last_byte = 1; b.last_byte = s.payload[s.size - 1]; b.last_byte_len = 1; }
+      b.has_cabac = 1;
+      b.cabac = rc.data;
+      b.cabac_len = rc.len;
+      avr_pb_put_block(&o, &b);
+      avr_last_stats.coded_slices++;
+      avr_last_stats.payload_bytes += s.size;
+      avr_last_stats.recoded_bytes += rc.len;
+      avr_last_stats.bins += bins;
+      ob_free(&rc);
+    } else {
+      avr_pb_block_t b = {0};
+      b.has_skip = 1;
+      b.skip_coded = 1;
+      b.has_size = 1;
+      b.size = (int64_t)s.size;
+      avr_pb_put_block(&o, &b);
+      avr_last_stats.skipped_slices++;
+      /* model hooks still run for skipped slices (codec-level hooks, recode.cpp:212-228) */
+      if (model) model_update_frame_spec(model, s.picture_id, s.h.mb_width, s.h.mb_height);
+    }
+    free(s.rbsp);
+  }
+  avr_pb_block_t lit = {0};
+  lit.has_literal = 1;
+  lit.literal = file + prev_end;
+  lit.literal_len = n - prev_end;
+  avr_pb_put_block(&o, &lit);
+  avr_model_free(model);
+  free(st);
+  free(nals);
+  *out = o.data;
+  *out_len = o.len;
+  return 0;
+}
+
+/* ======================================================================== decompress */
+static void surrogate_marker(uint64_t n, uint8_t m[8]) { /* next_surrogate_marker (1527-1535) */
+  for (int i = 0; i < SURROGATE_MARKER_BYTES; i++) {
+    m[i] = (uint8_t)(n % 255 + 1);
+    n /= 255;
+  }
+}
+
+int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) {
+  avr_pb_block_t *blocks;
+  int nb = avr_pb_parse(in, n, &blocks);
+  if (nb < 0) return -1;
+  /* read_packet (1359-1409): literals + surrogate blocks form the stream FFmpeg sees */
+  obuf_t stream;
+  ob_init(&stream);
+  size_t *pos = (size_t *)calloc((size_t)nb + 1, sizeof(size_t));
+  uint64_t seq = 1;
+  int ret = 0;
+  for (int i = 0; i < nb; i++) {
+    avr_pb_block_t *b = &blocks[i];
+    if (b->has_literal + b->has_cabac + b->has_skip != 1) { ret = -2; goto done; }
+    pos[i] = stream.len;
+    if (b->has_literal) {
+      ob_append(&stream, b->literal, b->literal_len);
+    } else if (b->has_cabac) {
+      if (!b->has_size || b->size < SURROGATE_MARKER_BYTES) { ret = -3; goto done; }
+      uint8_t mk[8];
+      surrogate_marker(seq++, mk);
+      ob_append(&stream, mk, 8);
+      for (int64_t k = 8; k < b->size; k++) ob_put(&stream, 'X');
+    } else if (!b->skip_coded) {
+      ret = -4;
+      goto done;
+    }
+  }
+  /* walk the rebuilt stream; each CABAC slice claims the next coded block (recognize_coded_block) */
+  avr_nal_t *nals;
+  int nn = avr_demux(stream.data, stream.len, &nals);
+  if (nn < 0) { ret = -5; goto done; }
+  stream_state_t *st = (stream_state_t *)calloc(1, sizeof(stream_state_t));
+  st->x264_build = -1;
+  avr_model_t *model = avr_model_new();
+  int mode_r = avr_pb_mode(in, n) == AVR_MODE_R;
+  int next_coded = 0;
+  obuf_t *regen = (obuf_t *)calloc((size_t)nb, sizeof(obuf_t));
+  for (int i = 0; i < nn && ret == 0; i++) {
+    slice_t s;
+    if (!nal_to_slice(st, stream.data + nals[i].offset, nals[i].size, &s)) continue;
+    while (next_coded < nb && !blocks[next_coded].has_cabac && !blocks[next_coded].has_skip) next_coded++;
+    if (next_coded >= nb) { ret = -6; free(s.rbsp); break; }
+    avr_pb_block_t *b = &blocks[next_coded];
+    if ((size_t)b->size != s.size) { ret = -7; free(s.rbsp); break; }
+    if (b->has_cabac) {
+      avr_model_t *m = model;
+      avr_model_t *fresh = NULL;
+      if (!mode_r) m = fresh = avr_model_new();
+      obuf_t cab;
+      int r = decompress_slice_with_model(m, &s.h, s.picture_id, b->cabac, b->cabac_len, &cab);
+      if (fresh) avr_model_free(fresh);
+      if (r != 0) { ret = -8; ob_free(&cab); free(s.rbsp); break; }
+      if (b->has_parity && b->has_last_byte && b->last_byte_len) {
+        size_t sz = cab.len;
+        if (b->length_parity != (int)(sz & 1)) ob_put(&cab, b->last_byte);
+        else if (sz) cab.data[sz - 1] = b->last_byte;
+      }
+      regen[next_coded] = cab;
+    } else {
+      model_update_frame_spec(model, s.picture_id, s.h.mb_width, s.h.mb_height);
+    }
+    next_coded++;
+    free(s.rbsp);
+  }
+  obuf_t o;
+  ob_init(&o);
+  for (int i = 0; i < nb && ret == 0; i++) {
+    if (blocks[i].has_literal) ob_append(&o, blocks[i].literal, blocks[i].literal_len);
+    else if (blocks[i].has_cabac) {
+      if (!regen[i].data && blocks[i].size) { ret = -9; break; } /* "Not all blocks were decoded." */
+      ob_append(&o, regen[i].data, regen[i].len);
+    }
+  }
+  for (int i = 0; i < nb; i++) ob_free(&regen[i]);
+  free(regen);
+  avr_model_free(model);
+  free(st);
+  free(nals);
+  if (ret == 0) { *out = o.data; *out_len = o.len; }
+  else ob_free(&o);
+done:
+  free(pos);
+  ob_free(&stream);
+  free(blocks);
+  return ret;
+}
