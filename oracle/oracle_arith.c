@@ -270,3 +270,66 @@ int cabac_dec_terminate(cabac_dec_t *d) { /* 9.3.3.2.2.3 */
   }
   return 0;
 }
+
+/* ---------------------------------------------------------------- op scripts (tests) */
+/* Runs the same op scripts as oracle/ref_arith_driver.cpp.  ops = quads (op, a, b, c):
+ *   's' sym pos neg (recoded), 'd' sym state (cabac), 'b' sym, 't' sym, 'f' finish.
+ * kind 0 = recoded coder, 1 = CABAC coder.  Returns bytes written (or -1 if cap too small). */
+long avr_script_run(int kind, const int32_t *ops, size_t nops, uint8_t *out, size_t cap) {
+  obuf_t o;
+  ob_init(&o);
+  ac_enc_t rc;
+  cabac_enc_t cb;
+  if (kind == 0) rc_enc_init(&rc, &o);
+  else cabac_enc_init(&cb, &o);
+  for (size_t i = 0; i < nops; i++) {
+    const int32_t *q = ops + 4 * i;
+    switch (q[0]) {
+      case 's': ac_enc_put(&rc, q[1], rc_p1(rc.range, q[2], q[3])); break;
+      case 'd': { uint8_t st = (uint8_t)q[2]; cabac_enc_put(&cb, q[1], &st); break; }
+      case 'b': cabac_enc_put_bypass(&cb, q[1]); break;
+      case 't': cabac_enc_put_terminate(&cb, q[1]); break;
+      case 'f': if (kind == 0) ac_enc_finish(&rc); else ac_enc_finish(&cb.e); break;
+      default: break;
+    }
+  }
+  if (kind == 0) { ac_enc_finish(&rc); ac_enc_free(&rc); }
+  else { ac_enc_finish(&cb.e); cabac_enc_free(&cb); }
+  long n = (long)o.len;
+  if (o.len > cap) n = -1;
+  else memcpy(out, o.data, o.len);
+  ob_free(&o);
+  return n;
+}
+
+/* decode a recoded stream with the given (pos, neg) sequence; returns #symbols matching */
+long avr_script_decode_recoded(const uint8_t *in, size_t n, const int32_t *ops, size_t nops) {
+  ac_dec_t d;
+  rc_dec_init(&d, in, n);
+  long ok = 0;
+  for (size_t i = 0; i < nops; i++) {
+    const int32_t *q = ops + 4 * i;
+    if (q[0] != 's') continue;
+    if (ac_dec_get(&d, rc_p1(d.range, q[2], q[3])) != q[1]) return ok;
+    ok++;
+  }
+  return ok;
+}
+
+/* decode a CABAC stream produced from 'd'/'b'/'t' ops with the spec engine; returns #ops matching */
+long avr_script_decode_cabac(const uint8_t *in, size_t n, const int32_t *ops, size_t nops) {
+  cabac_dec_t d;
+  cabac_dec_init(&d, in, n);
+  long ok = 0;
+  for (size_t i = 0; i < nops; i++) {
+    const int32_t *q = ops + 4 * i;
+    int s;
+    if (q[0] == 'd') { uint8_t st = (uint8_t)q[2]; s = cabac_dec_decision(&d, &st); }
+    else if (q[0] == 'b') s = cabac_dec_bypass(&d);
+    else if (q[0] == 't') s = cabac_dec_terminate(&d) != 0;
+    else continue;
+    if (s != q[1]) return ok;
+    ok++;
+  }
+  return ok;
+}

@@ -1,0 +1,77 @@
+"""Test-side access to the oracle (oracle/, CPU restatement of the reference path).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module.
+"""
+import ctypes
+import os
+import subprocess
+import tempfile
+from functools import lru_cache
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+ORACLE = ROOT / "oracle"
+
+
+def build_oracle():
+    lib, cli = ORACLE / "liboracle.so", ORACLE / "recode_oracle"
+    if not lib.exists() or not cli.exists():
+        subprocess.run(["make", "-s", "-C", str(ORACLE), "all"], check=True)
+    return lib, cli
+
+
+@lru_cache(None)
+def lib():
+    path, _ = build_oracle()
+    L = ctypes.CDLL(str(path))
+    L.avr_script_run.restype = ctypes.c_long
+    L.avr_script_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    L.avr_script_decode_recoded.restype = ctypes.c_long
+    L.avr_script_decode_recoded.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    L.avr_script_decode_cabac.restype = ctypes.c_long
+    L.avr_script_decode_cabac.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    return L
+
+
+def _ops_array(ops):
+    flat = []
+    for op in ops:
+        flat += [ord(op[0]), int(op[1]), int(op[2]), int(op[3])]
+    return (ctypes.c_int32 * max(1, len(flat)))(*flat)
+
+
+def script_encode(kind, ops):
+    """kind: 'recoded' or 'cabac'; ops: list of (op, a, b, c).  Returns bytes."""
+    arr = _ops_array(ops)
+    cap = 64 + 4 * len(ops)
+    buf = ctypes.create_string_buffer(cap)
+    n = lib().avr_script_run(0 if kind == "recoded" else 1, arr, len(ops), buf, cap)
+    assert n >= 0
+    return buf.raw[:n]
+
+
+def script_decode_ok(kind, data, ops):
+    arr = _ops_array(ops)
+    fn = lib().avr_script_decode_recoded if kind == "recoded" else lib().avr_script_decode_cabac
+    return fn(data, len(data), arr, len(ops))
+
+
+@lru_cache(None)
+def lps_table():
+    """FFmpeg-layout rangeTabLPS (512 bytes) as the oracle builds it."""
+    L = lib()
+    return list((ctypes.c_uint8 * 512).in_dll(L, "avr_lps_range"))
+
+
+def oracle_cli(cmd, path, mode="R", out=None):
+    """Run recode_oracle; returns stdout bytes (or the output file's bytes)."""
+    _, cli = build_oracle()
+    with tempfile.TemporaryDirectory() as td:
+        o = Path(td) / "out.bin"
+        args = [str(cli), cmd] + (["-p"] if mode == "P" else []) + [str(path), str(o)]
+        r = subprocess.run(args, capture_output=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"recode_oracle {cmd} failed: {r.stderr.decode()}")
+        if cmd == "roundtrip":
+            return r.stdout
+        return o.read_bytes()
