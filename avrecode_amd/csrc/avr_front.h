@@ -1,0 +1,87 @@
+// Host front end of the recode path: what recode.cpp obtains from FFmpeg's demuxer and H.264
+// headers parser (av_decoder, recode.cpp:73-135), the block segmentation
+// (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297) and the recode.proto container.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace avr {
+
+struct Sps {
+  bool valid = false;
+  int profile_idc = 0, chroma_format_idc = 1, separate_colour_plane = 0;
+  int log2_max_frame_num = 4, poc_type = 0, log2_max_poc_lsb = 4, delta_pic_order_always_zero = 0;
+  int frame_mbs_only = 1, mb_aff = 0, direct_8x8_inference = 0, mb_width = 0, mb_height = 0;
+};
+struct Pps {
+  bool valid = false;
+  int sps_id = 0, entropy_coding_mode = 0, bottom_field_pic_order_present = 0, num_slice_groups = 1;
+  int num_ref_idx_default[2] = {1, 1}, weighted_pred = 0, weighted_bipred_idc = 0, pic_init_qp = 26;
+  int deblocking_filter_control_present = 0, redundant_pic_cnt_present = 0, transform_8x8_mode = 0;
+};
+
+struct SliceHeader {
+  int nal_unit_type = 0, nal_ref_idc = 0, first_mb = 0, slice_type = 0, pps_id = 0, frame_num = 0;
+  int field_pic = 0, mbaff = 0, idr_pic_id = 0, poc_lsb = 0, num_ref_idx[2] = {0, 0}, cabac_init_idc = -1;
+  int slice_qp = 26, chroma_array_type = 1, transform_8x8_mode = 0, direct_8x8_inference = 0;
+  int mb_width = 0, mb_height = 0, x264_build = -1, entropy_coding_mode = 0;
+  size_t cabac_start = 0;   // byte offset of slice_data() in the RBSP
+  bool supported = false;
+};
+
+// A CABAC slice as FFmpeg would hand it to init_decoder (recode.cpp:143).
+struct SliceInfo {
+  SliceHeader h;
+  int picture_id = 0;
+  size_t nal_offset = 0, nal_size = 0;   // escaped NAL in the file
+  std::vector<uint8_t> rbsp;             // unescaped NAL payload after the header byte
+  size_t size = 0;                       // init_decoder size
+  size_t read_limit = 0;                 // bytes a decoder may read from the payload start
+  const uint8_t* payload() const { return rbsp.data() + h.cabac_start; }
+};
+
+struct NalRef {
+  size_t offset, size;
+};
+
+// MP4 (avcC) or Annex-B; returns false on a malformed container.
+bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals);
+
+// Stateful walk over a NAL sequence (parameter sets, x264 SEI, picture boundaries).
+class StreamParser {
+ public:
+  // Returns true and fills *s when the NAL is a CABAC slice FFmpeg would decode.
+  bool next(const uint8_t* nal, size_t n, SliceInfo* s);
+
+ private:
+  Sps sps_[32];
+  Pps pps_[256];
+  int x264_build_ = -1;
+  bool have_prev_ = false;
+  SliceHeader prev_;
+  int picture_id_ = 0;
+};
+
+// recode.proto
+struct PbBlock {
+  bool has_size = false, has_literal = false, has_skip = false, has_cabac = false, has_parity = false,
+       has_last_byte = false;
+  int64_t size = 0;
+  bool skip_coded = false, length_parity = false;
+  const uint8_t* literal = nullptr;
+  size_t literal_len = 0;
+  const uint8_t* cabac = nullptr;
+  size_t cabac_len = 0;
+  std::string last_byte;
+};
+void pb_put_block(std::vector<uint8_t>* o, const PbBlock& b);
+void pb_put_metadata_version(std::vector<uint8_t>* o, const std::string& version);
+bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version);
+
+extern const char* const kParallelModelTag;   // Recoded.Metadata.version for the parallel model
+constexpr int kSurrogateMarkerBytes = 8;      // recode.cpp:27
+void surrogate_marker(uint64_t seq, uint8_t out[8]);
+
+}  // namespace avr

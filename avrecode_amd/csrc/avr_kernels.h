@@ -1,0 +1,24 @@
+// Host-visible entry points of avr_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/avrecode.h"
+
+namespace avr {
+
+struct EngineTables;
+
+// dense SIG + NZ estimator entries per model instance (u16 each), see avr_kernels.hip
+constexpr int kEstGlobal = 294016;
+
+size_t shared_bytes(int max_mb_width);
+// mode: 0 compress, 1 decompress, 2 generate.  sequential = reference model (single wavefront).
+hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
+                         int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
+                         uint8_t* frames, int* frame_meta, hipStream_t stream);
+hipError_t launch_pack(const avr_slice_desc* descs, const avr_slice_result* res, int n, const uint8_t* out,
+                       uint8_t* packed, uint64_t* offsets, hipStream_t stream);
+
+}  // namespace avr

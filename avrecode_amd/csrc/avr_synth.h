@@ -1,0 +1,13 @@
+// Synthetic H.264 CABAC streams for benchmarks: the device generator (avr_kernels.hip, generate
+// mode) produces slice_data(); this writes SPS/PPS and slice headers around it (Annex-B).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "../../include/avrecode.h"
+
+namespace avr {
+void synth_write_parameter_sets(std::vector<uint8_t>* out, const avr_synth_params& p);
+void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int index, const uint8_t* payload,
+                       size_t payload_len);
+}  // namespace avr

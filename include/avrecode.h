@@ -1,0 +1,130 @@
+/*
+ * avrecode-amd: MI355X-native implementation of avrecode's CABAC decode -> predict ->
+ * arithmetic re-encode path (ddkang/avrecode, reference mounted at /root/reference).
+ *
+ * C ABI: extern "C", plain pointers and sizes, integer status codes, no exceptions across the
+ * boundary, caller-owned buffers unless stated, one avr_ctx per host thread (not thread-safe).
+ *
+ * Reference interfaces each group replaces (file:line in /root/reference):
+ *   avr_compress_file    compressor(...).run()           recode.cpp:1102-1125, 1275-1297
+ *   avr_decompress_file  decompressor(...).run()         recode.cpp:1312-1357, 1359-1409, 1527-1573
+ *   avr_roundtrip_file   roundtrip(input, out)           recode.cpp:1594-1624
+ *   avr_compress_slices  compressor::cabac_decoder x N    recode.cpp:1134-1268 (+ h264_model 615-1059,
+ *                        (one CABAC slice per wavefront)  h264_symbol::execute 1061-1100,
+ *                                                         arithmetic_code.h encoder 89-203)
+ *   avr_decompress_slices decompressor::cabac_decoder x N recode.cpp:1411-1520 (+ cabac_code.h 27-80,
+ *                                                         arithmetic_code.h decoder 211-298)
+ * The per-bin libavcodec-hooks callback surface (AVCodecHooks, recode.cpp:137-228) is realised
+ * inside the device kernels: the kernel owns the CABAC parse that drives those callbacks.
+ */
+#ifndef AVRECODE_AMD_H
+#define AVRECODE_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVRECODE_ABI_VERSION 1
+
+typedef enum {
+  AVR_OK = 0,
+  AVR_ERR_INVALID_ARGUMENT = -1,
+  AVR_ERR_DEVICE = -2,          /* HIP error; see avr_last_error */
+  AVR_ERR_FORMAT = -3,          /* malformed input file / container */
+  AVR_ERR_OUT_OF_MEMORY = -4,
+  AVR_ERR_ROUNDTRIP = -5,       /* decompress(compress(x)) != x */
+  AVR_ERR_UNSUPPORTED = -6,
+} avr_status;
+
+/* Model modes.  REFERENCE = recode.cpp's h264_model exactly (estimators persist across slices,
+ * previous-frame and cross-slice contexts); output bytes equal the reference compressor's.
+ * Sequential over slices (one wavefront for the whole file).
+ * PARALLEL = the same model applied to every slice from a fresh state; slices are independent,
+ * one wavefront per slice, shardable across GPUs.  Tagged in Recoded.Metadata.version. */
+typedef enum { AVR_MODEL_REFERENCE = 0, AVR_MODEL_PARALLEL = 1 } avr_model;
+
+typedef struct avr_ctx avr_ctx;
+
+/* device = HIP device ordinal.  Fails with AVR_ERR_DEVICE when no usable GPU is present: the
+ * library has no CPU implementation of the hot path. */
+int avr_create(int device, avr_ctx** out);
+void avr_destroy(avr_ctx* ctx);
+const char* avr_last_error(const avr_ctx* ctx);
+/* free a buffer returned by the library */
+void avr_free(void* p);
+
+/* ------------------------------------------------------------------ whole files (host memory) */
+/* in: an MP4 (avcC) or Annex-B H.264 file.  *out: serialized Recoded protobuf (recode.proto). */
+int avr_compress_file(avr_ctx* ctx, const uint8_t* in, size_t n, int model, uint8_t** out, size_t* out_len);
+/* in: a Recoded protobuf.  *out: the original file bytes. */
+int avr_decompress_file(avr_ctx* ctx, const uint8_t* in, size_t n, uint8_t** out, size_t* out_len);
+
+typedef struct {
+  uint64_t file_bytes, slices, coded_slices, skipped_slices, payload_bytes, recoded_bytes, bins;
+  double compress_s, decompress_s;  /* wall time of the two halves (host + device) */
+} avr_file_stats;
+/* compress, decompress, compare (recode.cpp:1594-1624).  Returns AVR_ERR_ROUNDTRIP on mismatch. */
+int avr_roundtrip_file(avr_ctx* ctx, const uint8_t* in, size_t n, int model, uint8_t** compressed,
+                       size_t* compressed_len, avr_file_stats* stats);
+
+/* ------------------------------------------------------- slice batches (device-resident data) */
+/* One CABAC slice: the (buf, size) FFmpeg hands to AVCodecHooks.cabac.init_decoder
+ * (recode.cpp:143), plus the slice-header fields the slice_data() parse needs. */
+typedef struct {
+  uint64_t payload_offset;   /* byte offset of the CABAC payload in the input buffer */
+  uint32_t payload_size;     /* init_decoder's size */
+  uint32_t read_limit;       /* bytes readable from payload_offset (>= payload_size) */
+  uint64_t out_offset;       /* where this slice's output goes in the output buffer */
+  uint32_t out_capacity;     /* bytes reserved there */
+  int32_t slice_type;        /* 0 P, 1 B, 2 I */
+  int32_t slice_qp, cabac_init_idc, first_mb, mb_width, mb_height;
+  int32_t num_ref_idx_l0, num_ref_idx_l1;
+  int32_t chroma_array_type, transform_8x8_mode, direct_8x8_inference, x264_build;
+  int32_t picture_id;        /* decode-order picture counter (frame_spec, recode.cpp:824-843) */
+  int32_t coded;             /* 0: skip_coded slice (reference mode only calls frame_spec) */
+} avr_slice_desc;
+
+typedef struct {
+  uint32_t out_len;          /* bytes written at out_offset */
+  int32_t status;            /* 0 ok, <0 parse/overflow error (slice must be stored skip_coded) */
+  uint32_t bins;             /* CABAC bins processed */
+  uint32_t mbs;              /* macroblocks parsed */
+} avr_slice_result;
+
+/* All pointers are device pointers; stream is a hipStream_t (NULL = default stream).
+ * Compress: payload bytes -> re-coded bytes.  For each slice the kernel also checks that a
+ * CABAC re-encode plus the decompressor's last-byte rule (recode.cpp:1345-1356, 1503-1505)
+ * restores the payload, and reports status < 0 otherwise. */
+/* max_mb_width / max_mb_height bound every slice's picture size (LDS ring and frame sizing). */
+int avr_compress_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, int n, int max_mb_width, int max_mb_height,
+                        const uint8_t* d_in, uint8_t* d_out, avr_slice_result* d_res, int model, void* stream);
+/* Decompress: re-coded bytes (at payload_offset/payload_size = recoded stream) -> regenerated
+ * CABAC bytes at out_offset (before the last-byte patch; trailing 0x80 already dropped). */
+int avr_decompress_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, int n, int max_mb_width, int max_mb_height,
+                          const uint8_t* d_in, uint8_t* d_out, avr_slice_result* d_res, int model, void* stream);
+/* Pack variable-length per-slice outputs contiguously: d_packed[k] gets slice k's bytes at
+ * d_offsets[k] (exclusive prefix sum of out_len, computed on the device). */
+int avr_pack_outputs(avr_ctx* ctx, const avr_slice_desc* d_desc, const avr_slice_result* d_res, int n,
+                     const uint8_t* d_out, uint8_t* d_packed, uint64_t* d_offsets, void* stream);
+
+/* --------------------------------------------------------------- synthetic H.264 (benchmarks) */
+typedef struct {
+  int32_t mb_width, mb_height;   /* e.g. 120 x 68 for 1080p */
+  int32_t slice_type;            /* 0 P, 1 B, 2 I */
+  int32_t slice_qp;
+  int32_t chroma_format_idc;     /* 1 (4:2:0) .. 3 */
+  int32_t transform_8x8_mode;
+  int32_t num_ref_idx_l0, num_ref_idx_l1;
+  uint64_t seed;
+} avr_synth_params;
+/* Generate n independent single-slice pictures on the device and return them as one Annex-B
+ * stream (SPS/PPS + n slice NAL units) in host memory. */
+int avr_synthesize_stream(avr_ctx* ctx, const avr_synth_params* params, int n, uint8_t** out, size_t* out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
