@@ -1,0 +1,305 @@
+"""avrecode-amd: MI355X-native CABAC recode path (ddkang/avrecode's decode -> predict -> re-encode).
+
+Python view of the C ABI in include/avrecode.h (libavrecode.so, built in-tree by
+``make -C avrecode_amd``).  The product is the native library and the ``recode`` CLI next to it;
+this module is the binding tests, bench.py and the sharded driver use.  There is no Python or CPU
+implementation of the hot path: without the library, or without a GPU, every call raises.
+
+Reference interfaces mirrored here (file:line in ddkang/avrecode):
+  compress / decompress / roundtrip   recode.cpp:1102-1125, 1312-1357, 1594-1624 (+ CLI 1626-1660)
+  parse_stream                        av_decoder::decode_video -> init_decoder(buf, size), recode.cpp:73-143
+  Context.compress_slices / ...       compressor::cabac_decoder / decompressor::cabac_decoder per
+                                      slice, recode.cpp:1134-1268, 1411-1520
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+__all__ = [
+    "AvrError", "Context", "MODEL_REFERENCE", "MODEL_PARALLEL", "SLICE_DESC", "SLICE_RESULT",
+    "SynthParams", "lib", "parse_stream", "assemble_container", "library_path", "EXPORTED_SYMBOLS",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+library_path = os.path.join(_HERE, "libavrecode.so")
+
+MODEL_REFERENCE = 0
+MODEL_PARALLEL = 1
+
+AVR_OK = 0
+_STATUS = {
+    -1: "invalid argument", -2: "device error", -3: "format error", -4: "out of memory",
+    -5: "roundtrip mismatch", -6: "unsupported",
+}
+
+# every function include/avrecode.h declares
+EXPORTED_SYMBOLS = (
+    "avr_create", "avr_destroy", "avr_last_error", "avr_free", "avr_compress_file", "avr_decompress_file",
+    "avr_roundtrip_file", "avr_compress_slices", "avr_decompress_slices", "avr_pack_outputs",
+    "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream", "avr_assemble_container", "avr_synthesize_stream",
+)
+
+# avr_slice_desc / avr_slice_result (include/avrecode.h), C layout
+SLICE_DESC = np.dtype([
+    ("payload_offset", "<u8"), ("payload_size", "<u4"), ("read_limit", "<u4"),
+    ("out_offset", "<u8"), ("out_capacity", "<u4"),
+    ("slice_type", "<i4"), ("slice_qp", "<i4"), ("cabac_init_idc", "<i4"), ("first_mb", "<i4"),
+    ("mb_width", "<i4"), ("mb_height", "<i4"), ("num_ref_idx_l0", "<i4"), ("num_ref_idx_l1", "<i4"),
+    ("chroma_array_type", "<i4"), ("transform_8x8_mode", "<i4"), ("direct_8x8_inference", "<i4"),
+    ("x264_build", "<i4"), ("picture_id", "<i4"), ("coded", "<i4"),
+], align=True)
+SLICE_RESULT = np.dtype([("out_len", "<u4"), ("status", "<i4"), ("bins", "<u4"), ("mbs", "<u4")], align=True)
+assert SLICE_DESC.itemsize == 88 and SLICE_RESULT.itemsize == 16
+
+
+class AvrError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"avrecode: {_STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class _FileStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("file_bytes", "slices", "coded_slices", "skipped_slices", "payload_bytes", "recoded_bytes", "bins")] + \
+               [("compress_s", ctypes.c_double), ("decompress_s", ctypes.c_double)]
+
+
+class _SynthParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("mb_width", "mb_height", "slice_type", "slice_qp", "chroma_format_idc", "transform_8x8_mode",
+                 "num_ref_idx_l0", "num_ref_idx_l1")] + [("seed", ctypes.c_uint64)]
+
+
+@dataclass
+class SynthParams:
+    """Synthetic slice parameters (avr_synth_params); defaults = one 1080p 4:2:0 High I picture."""
+    mb_width: int = 120
+    mb_height: int = 68
+    slice_type: int = 2
+    slice_qp: int = 26
+    chroma_format_idc: int = 1
+    transform_8x8_mode: int = 1
+    num_ref_idx_l0: int = 1
+    num_ref_idx_l1: int = 1
+    seed: int = 0
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libavrecode.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(library_path):
+        raise ImportError(f"{library_path} is missing: build it with `make -C {_HERE}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(library_path)
+    vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    psz = ctypes.POINTER(ctypes.c_size_t)
+    pi = ctypes.POINTER(ctypes.c_int)
+    L.avr_create.argtypes = [i32, pp]
+    L.avr_destroy.argtypes = [vp]
+    L.avr_destroy.restype = None
+    L.avr_last_error.argtypes = [vp]
+    L.avr_last_error.restype = ctypes.c_char_p
+    L.avr_free.argtypes = [vp]
+    L.avr_free.restype = None
+    L.avr_compress_file.argtypes = [vp, vp, sz, i32, pp, psz]
+    L.avr_decompress_file.argtypes = [vp, vp, sz, pp, psz]
+    L.avr_roundtrip_file.argtypes = [vp, vp, sz, i32, pp, psz, ctypes.POINTER(_FileStats)]
+    for f in (L.avr_compress_slices, L.avr_decompress_slices):
+        f.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, i32, vp]
+    L.avr_roundtrip_slices.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, i32, vp]
+    L.avr_derive_decompress_descs.argtypes = [vp, vp, vp, i32, vp, vp]
+    L.avr_verify_slices.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
+    L.avr_pack_outputs.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
+    L.avr_parse_stream.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
+    L.avr_assemble_container.argtypes = [vp, sz, i32, vp, vp, vp, vp, pp, psz]
+    L.avr_synthesize_stream.argtypes = [vp, ctypes.POINTER(_SynthParams), i32, pp, psz]
+    for name in EXPORTED_SYMBOLS:   # fails here, not at first use, when the build is stale
+        getattr(L, name)
+    _lib = L
+    return L
+
+
+def _buf(data) -> tuple[ctypes.c_void_p, int, object]:
+    """(pointer, length, keepalive) for bytes / bytearray / numpy uint8."""
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data, dtype=np.uint8)
+        return ctypes.c_void_p(a.ctypes.data), a.nbytes, a
+    b = bytes(data)
+    cb = ctypes.create_string_buffer(b, len(b)) if b else ctypes.create_string_buffer(1)
+    return ctypes.cast(cb, ctypes.c_void_p), len(b), cb
+
+
+def _take(p: ctypes.c_void_p, n: int) -> bytes:
+    L = lib()
+    try:
+        return ctypes.string_at(p.value, n) if n else b""
+    finally:
+        L.avr_free(p)
+
+
+@dataclass
+class ParsedStream:
+    """Per-slice descriptors + payload arena (what init_decoder receives, recode.cpp:143)."""
+    descs: np.ndarray        # SLICE_DESC[n]
+    arena: np.ndarray        # uint8 payloads (16-byte aligned, zero padded)
+    work_len: int            # bytes of compress output space the descs' out_offset/out_capacity index
+    max_mb_width: int
+    max_mb_height: int
+
+    @property
+    def payload_bytes(self) -> int:
+        return int(self.descs["payload_size"].sum())
+
+
+def parse_stream(data) -> ParsedStream:
+    """Host-side slice extraction (avr_parse_stream).  Needs no GPU."""
+    L = lib()
+    p, n, keep = _buf(data)
+    descs, arena = ctypes.c_void_p(), ctypes.c_void_p()
+    ns, mw, mh = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    alen, wlen = ctypes.c_size_t(), ctypes.c_size_t()
+    r = L.avr_parse_stream(p, n, ctypes.byref(descs), ctypes.byref(ns), ctypes.byref(arena), ctypes.byref(alen),
+                           ctypes.byref(wlen), ctypes.byref(mw), ctypes.byref(mh))
+    del keep
+    if r != AVR_OK:
+        raise AvrError(r, "avr_parse_stream failed")
+    d = np.frombuffer(_take(descs, ns.value * SLICE_DESC.itemsize), dtype=SLICE_DESC).copy()
+    a = np.frombuffer(_take(arena, alen.value), dtype=np.uint8).copy()
+    return ParsedStream(d, a, int(wlen.value), int(mw.value), int(mh.value))
+
+
+def assemble_container(data, status: np.ndarray, recoded: bytes, offsets: np.ndarray, lens: np.ndarray) -> bytes:
+    """PARALLEL-model Recoded container from per-slice outputs (avr_assemble_container).  Host only."""
+    L = lib()
+    p, n, keep = _buf(data)
+    st = np.ascontiguousarray(status, dtype=np.int32)
+    of = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint32)
+    rp, _, keep2 = _buf(recoded)
+    out, olen = ctypes.c_void_p(), ctypes.c_size_t()
+    r = L.avr_assemble_container(p, n, len(st), st.ctypes.data, rp, of.ctypes.data, ln.ctypes.data,
+                                 ctypes.byref(out), ctypes.byref(olen))
+    if r != AVR_OK:
+        raise AvrError(r, "avr_assemble_container failed")
+    return _take(out, olen.value)
+
+
+class Context:
+    """One device context (avr_ctx).  Raises AvrError(AVR_ERR_DEVICE) when no GPU is usable."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = ctypes.c_void_p()
+        r = L.avr_create(int(device), ctypes.byref(h))
+        if r != AVR_OK:
+            raise AvrError(r, f"avr_create(device={device}) failed (no usable GPU? the hot path has no CPU path)")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().avr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, r: int, what: str):
+        if r != AVR_OK:
+            raise AvrError(r, f"{what}: {lib().avr_last_error(self._h).decode(errors='replace')}")
+
+    # ------------------------------------------------------------------ whole files
+    def compress(self, data, model: int = MODEL_REFERENCE) -> bytes:
+        p, n, keep = _buf(data)
+        out, olen = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(lib().avr_compress_file(self._h, p, n, model, ctypes.byref(out), ctypes.byref(olen)),
+                    "compress")
+        return _take(out, olen.value)
+
+    def decompress(self, data) -> bytes:
+        p, n, keep = _buf(data)
+        out, olen = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(lib().avr_decompress_file(self._h, p, n, ctypes.byref(out), ctypes.byref(olen)), "decompress")
+        return _take(out, olen.value)
+
+    def roundtrip(self, data, model: int = MODEL_REFERENCE) -> tuple[bytes, dict]:
+        p, n, keep = _buf(data)
+        out, olen = ctypes.c_void_p(), ctypes.c_size_t()
+        st = _FileStats()
+        self._check(lib().avr_roundtrip_file(self._h, p, n, model, ctypes.byref(out), ctypes.byref(olen),
+                                             ctypes.byref(st)), "roundtrip")
+        stats = {f: getattr(st, f) for f, _ in _FileStats._fields_}
+        return _take(out, olen.value), stats
+
+    # ------------------------------------------------------- device-resident slice batches
+    # All tensor arguments are torch tensors on this context's device (uint8 buffers, and uint8
+    # views of descriptor/result arrays); `stream` is a torch.cuda.Stream or None (= its current).
+    @staticmethod
+    def _ptr(t) -> ctypes.c_void_p:
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p()
+
+    @staticmethod
+    def _stream(stream):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def compress_slices(self, d_desc, n, max_w, max_h, d_in, d_out, d_res, model=MODEL_PARALLEL, stream=None):
+        self._check(lib().avr_compress_slices(self._h, self._ptr(d_desc), n, max_w, max_h, self._ptr(d_in),
+                                              self._ptr(d_out), self._ptr(d_res), model, self._stream(stream)),
+                    "compress_slices")
+
+    def decompress_slices(self, d_desc, n, max_w, max_h, d_in, d_out, d_res, model=MODEL_PARALLEL, stream=None):
+        self._check(lib().avr_decompress_slices(self._h, self._ptr(d_desc), n, max_w, max_h, self._ptr(d_in),
+                                                self._ptr(d_out), self._ptr(d_res), model, self._stream(stream)),
+                    "decompress_slices")
+
+    def roundtrip_slices(self, d_desc, n, max_w, max_h, d_in, d_work, d_regen, d_dec_desc, d_res_c, d_res_d,
+                         d_verdict, model=MODEL_PARALLEL, stream=None):
+        P = self._ptr
+        self._check(lib().avr_roundtrip_slices(self._h, P(d_desc), n, max_w, max_h, P(d_in), P(d_work), P(d_regen),
+                                               P(d_dec_desc), P(d_res_c), P(d_res_d), P(d_verdict), model,
+                                               self._stream(stream)), "roundtrip_slices")
+
+    def derive_decompress_descs(self, d_desc, d_res_c, n, d_dec_desc, stream=None):
+        P = self._ptr
+        self._check(lib().avr_derive_decompress_descs(self._h, P(d_desc), P(d_res_c), n, P(d_dec_desc),
+                                                      self._stream(stream)), "derive_decompress_descs")
+
+    def verify_slices(self, d_desc, d_res_c, d_res_d, n, d_in, d_regen, d_verdict, stream=None):
+        P = self._ptr
+        self._check(lib().avr_verify_slices(self._h, P(d_desc), P(d_res_c), P(d_res_d), n, P(d_in), P(d_regen),
+                                            P(d_verdict), self._stream(stream)), "verify_slices")
+
+    def pack_outputs(self, d_desc, d_res, n, d_out, d_packed, d_offsets, stream=None):
+        P = self._ptr
+        self._check(lib().avr_pack_outputs(self._h, P(d_desc), P(d_res), n, P(d_out), P(d_packed), P(d_offsets),
+                                           self._stream(stream)), "pack_outputs")
+
+    # ------------------------------------------------------------------ synthetic input
+    def synthesize(self, params: SynthParams, n: int) -> bytes:
+        sp = _SynthParams(params.mb_width, params.mb_height, params.slice_type, params.slice_qp,
+                          params.chroma_format_idc, params.transform_8x8_mode, params.num_ref_idx_l0,
+                          params.num_ref_idx_l1, params.seed)
+        out, olen = ctypes.c_void_p(), ctypes.c_size_t()
+        self._check(lib().avr_synthesize_stream(self._h, ctypes.byref(sp), int(n), ctypes.byref(out),
+                                                ctypes.byref(olen)), "synthesize")
+        return _take(out, olen.value)

@@ -253,6 +253,70 @@ int parse_file(avr_ctx* c, const uint8_t* in, size_t n, ParsedFile* pf) {
 
 bool recodable_candidate(const avr::SliceInfo& s) { return s.h.supported && s.size >= (size_t)avr::kSurrogateMarkerBytes; }
 
+// find_next_coded_block_and_emit_literal (recode.cpp:1275-1297): slice i becomes a cabac block when
+// it is recodable (ok[i]), at least a surrogate marker long, and its payload occurs verbatim after
+// the previous coded block.  Returns the payload's position in the file per slice (null = skip).
+std::vector<const uint8_t*> segment(const uint8_t* in, size_t n, const ParsedFile& pf, const std::vector<char>& ok) {
+  std::vector<const uint8_t*> found(pf.slices.size(), nullptr);
+  size_t prev_end = 0;
+  for (size_t i = 0; i < pf.slices.size(); i++) {
+    const avr::SliceInfo& s = pf.slices[i];
+    if (!ok[i] || s.size < (size_t)avr::kSurrogateMarkerBytes) continue;
+    const uint8_t* f = (const uint8_t*)memmem(in + prev_end, n - prev_end, s.payload(), s.size);
+    if (f) {
+      found[i] = f;
+      prev_end = (size_t)(f - in) + s.size;
+    }
+  }
+  return found;
+}
+
+// compressor::run's block stream (recode.cpp:1115-1125, 1275-1297) as a Recoded protobuf.
+int emit_container(const uint8_t* in, size_t n, const ParsedFile& pf, const std::vector<const uint8_t*>& found,
+                   const std::vector<std::pair<const uint8_t*, size_t>>& recoded, bool parallel, uint8_t** out,
+                   size_t* out_len) {
+  std::vector<uint8_t> o;
+  o.reserve(n + n / 8 + 1024);
+  if (parallel) avr::pb_put_metadata_version(&o, avr::kParallelModelTag);
+  size_t prev_end = 0;
+  for (size_t i = 0; i < pf.slices.size(); i++) {
+    const avr::SliceInfo& s = pf.slices[i];
+    avr::PbBlock b;
+    if (found[i]) {
+      avr::PbBlock lit;
+      lit.has_literal = true;
+      lit.literal = in + prev_end;
+      lit.literal_len = (size_t)(found[i] - (in + prev_end));
+      avr::pb_put_block(&o, lit);
+      prev_end = (size_t)(found[i] - in) + s.size;
+      b.has_size = true;
+      b.size = (int64_t)s.size;
+      b.has_parity = true;
+      b.length_parity = s.size & 1;
+      if (s.size > 1) b.has_last_byte = true, b.last_byte.assign(1, (char)s.payload()[s.size - 1]);
+      b.has_cabac = true;
+      b.cabac = recoded[i].first;
+      b.cabac_len = recoded[i].second;
+    } else {
+      b.has_skip = true;
+      b.skip_coded = true;
+      b.has_size = true;
+      b.size = (int64_t)s.size;
+    }
+    avr::pb_put_block(&o, b);
+  }
+  avr::PbBlock lit;
+  lit.has_literal = true;
+  lit.literal = in + prev_end;
+  lit.literal_len = n - prev_end;
+  avr::pb_put_block(&o, lit);
+  *out = (uint8_t*)malloc(o.size() ? o.size() : 1);
+  if (!*out) return AVR_ERR_OUT_OF_MEMORY;
+  memcpy(*out, o.data(), o.size());
+  *out_len = o.size();
+  return AVR_OK;
+}
+
 }  // namespace
 
 // ================================================================================ C ABI
@@ -318,19 +382,7 @@ int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_
   std::vector<char> ok(pf.slices.size(), 0);
   for (size_t i = 0; i < pf.slices.size(); i++) ok[i] = cand_of[i] >= 0 && res[cand_of[i]].status == 0;
   // 2) segmentation (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297)
-  std::vector<const uint8_t*> found(pf.slices.size(), nullptr);
-  {
-    size_t prev_end = 0;
-    for (size_t i = 0; i < pf.slices.size(); i++) {
-      const avr::SliceInfo& s = pf.slices[i];
-      const uint8_t* f =
-          s.size ? (const uint8_t*)memmem(in + prev_end, n - prev_end, s.payload(), s.size) : nullptr;
-      if (f && s.size >= (size_t)avr::kSurrogateMarkerBytes && ok[i]) {
-        found[i] = f;
-        prev_end = (size_t)(f - in) + s.size;
-      }
-    }
-  }
+  std::vector<const uint8_t*> found = segment(in, n, pf, ok);
   // 3) reference model: re-run the coded slices through the sequential kernel in file order;
   //    a slice that fails there is demoted to skip_coded and the pass repeated.
   std::vector<std::vector<uint8_t>> recoded(pf.slices.size());
@@ -368,14 +420,8 @@ int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_
       }
       if (!again) break;
       // a demoted slice changes the literal gaps of later ones: redo the segmentation
-      size_t prev_end = 0;
-      for (size_t i = 0; i < pf.slices.size(); i++) {
-        if (!found[i]) continue;
-        const avr::SliceInfo& s = pf.slices[i];
-        const uint8_t* f = (const uint8_t*)memmem(in + prev_end, n - prev_end, s.payload(), s.size);
-        found[i] = f;
-        if (f) prev_end = (size_t)(f - in) + s.size;
-      }
+      for (size_t i = 0; i < pf.slices.size(); i++) ok[i] = ok[i] && found[i] != nullptr;
+      found = segment(in, n, pf, ok);
       if (attempt == 7) return fail(c, AVR_ERR_DEVICE, "reference-model pass did not converge");
     }
   } else {
@@ -387,46 +433,28 @@ int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_
       }
   }
   // 4) container (compressor::run, recode.cpp:1115-1125)
-  std::vector<uint8_t> o;
-  o.reserve(n + n / 8 + 1024);
-  if (model == AVR_MODEL_PARALLEL) avr::pb_put_metadata_version(&o, avr::kParallelModelTag);
-  size_t prev_end = 0;
+  std::vector<std::pair<const uint8_t*, size_t>> blobs(pf.slices.size(), {nullptr, 0});
+  for (size_t i = 0; i < pf.slices.size(); i++) blobs[i] = {recoded[i].data(), recoded[i].size()};
+  return emit_container(in, n, pf, found, blobs, model == AVR_MODEL_PARALLEL, out, out_len);
+}
+
+int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
+                           const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len) {
+  if (!file || !out || !out_len || n_slices < 0 || (n_slices && (!status || !offsets || !lens)))
+    return AVR_ERR_INVALID_ARGUMENT;
+  ParsedFile pf;
+  if (int r = parse_file(nullptr, file, n, &pf)) return r;
+  if ((size_t)n_slices != pf.slices.size()) return AVR_ERR_INVALID_ARGUMENT;
+  std::vector<char> ok(pf.slices.size(), 0);
+  std::vector<std::pair<const uint8_t*, size_t>> blobs(pf.slices.size(), {nullptr, 0});
   for (size_t i = 0; i < pf.slices.size(); i++) {
-    const avr::SliceInfo& s = pf.slices[i];
-    avr::PbBlock b;
-    if (found[i]) {
-      avr::PbBlock lit;
-      lit.has_literal = true;
-      lit.literal = in + prev_end;
-      lit.literal_len = (size_t)(found[i] - (in + prev_end));
-      avr::pb_put_block(&o, lit);
-      prev_end = (size_t)(found[i] - in) + s.size;
-      b.has_size = true;
-      b.size = (int64_t)s.size;
-      b.has_parity = true;
-      b.length_parity = s.size & 1;
-      if (s.size > 1) b.has_last_byte = true, b.last_byte.assign(1, (char)s.payload()[s.size - 1]);
-      b.has_cabac = true;
-      b.cabac = recoded[i].data();
-      b.cabac_len = recoded[i].size();
-    } else {
-      b.has_skip = true;
-      b.skip_coded = true;
-      b.has_size = true;
-      b.size = (int64_t)s.size;
+    ok[i] = recodable_candidate(pf.slices[i]) && status[i] == 0;
+    if (ok[i]) {
+      if (!recoded) return AVR_ERR_INVALID_ARGUMENT;
+      blobs[i] = {recoded + offsets[i], lens[i]};
     }
-    avr::pb_put_block(&o, b);
   }
-  avr::PbBlock lit;
-  lit.has_literal = true;
-  lit.literal = in + prev_end;
-  lit.literal_len = n - prev_end;
-  avr::pb_put_block(&o, lit);
-  *out = (uint8_t*)malloc(o.size() ? o.size() : 1);
-  if (!*out) return AVR_ERR_OUT_OF_MEMORY;
-  memcpy(*out, o.data(), o.size());
-  *out_len = o.size();
-  return AVR_OK;
+  return emit_container(file, n, pf, segment(file, n, pf, ok), blobs, true, out, out_len);
 }
 
 int avr_decompress_file(avr_ctx* c, const uint8_t* in, size_t n, uint8_t** out, size_t* out_len) {
@@ -602,6 +630,81 @@ int avr_compress_slices(avr_ctx* c, const avr_slice_desc* d_desc, int n, int max
 int avr_decompress_slices(avr_ctx* c, const avr_slice_desc* d_desc, int n, int max_mb_width, int max_mb_height,
                           const uint8_t* d_in, uint8_t* d_out, avr_slice_result* d_res, int model, void* stream) {
   return batch(c, 1, d_desc, n, max_mb_width, max_mb_height, d_in, d_out, d_res, model, stream);
+}
+
+int avr_roundtrip_slices(avr_ctx* c, const avr_slice_desc* d_desc, int n, int max_w, int max_h, const uint8_t* d_in,
+                         uint8_t* d_work, uint8_t* d_regen, avr_slice_desc* d_dec_desc, avr_slice_result* d_res_c,
+                         avr_slice_result* d_res_d, int32_t* d_verdict, int model, void* stream) {
+  if (!c || n < 0 || (n && (!d_regen || !d_dec_desc || !d_res_d || !d_verdict))) return AVR_ERR_INVALID_ARGUMENT;
+  if (int r = batch(c, 0, d_desc, n, max_w, max_h, d_in, d_work, d_res_c, model, stream)) return r;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(c, avr::launch_derive_decompress(d_desc, d_res_c, n, d_dec_desc, s));
+  if (int r = batch(c, 1, d_dec_desc, n, max_w, max_h, d_work, d_regen, d_res_d, model, stream)) return r;
+  HIP_TRY(c, avr::launch_verify(d_desc, d_res_c, d_res_d, n, d_in, d_regen, d_verdict, s));
+  return AVR_OK;
+}
+
+int avr_derive_decompress_descs(avr_ctx* c, const avr_slice_desc* d_desc, const avr_slice_result* d_res_c, int n,
+                                avr_slice_desc* d_dec_desc, void* stream) {
+  if (!c || n < 0 || (n && (!d_desc || !d_res_c || !d_dec_desc))) return AVR_ERR_INVALID_ARGUMENT;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, avr::launch_derive_decompress(d_desc, d_res_c, n, d_dec_desc, (hipStream_t)stream));
+  return AVR_OK;
+}
+
+int avr_verify_slices(avr_ctx* c, const avr_slice_desc* d_desc, const avr_slice_result* d_res_c,
+                      const avr_slice_result* d_res_d, int n, const uint8_t* d_in, const uint8_t* d_regen,
+                      int32_t* d_verdict, void* stream) {
+  if (!c || n < 0 || (n && (!d_desc || !d_res_c || !d_res_d || !d_in || !d_regen || !d_verdict)))
+    return AVR_ERR_INVALID_ARGUMENT;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, avr::launch_verify(d_desc, d_res_c, d_res_d, n, d_in, d_regen, d_verdict, (hipStream_t)stream));
+  return AVR_OK;
+}
+
+int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
+                     size_t* arena_len, size_t* work_len, int* max_w, int* max_h) {
+  if (!file || !descs || !n_slices || !arena || !arena_len || !work_len || !max_w || !max_h)
+    return AVR_ERR_INVALID_ARGUMENT;
+  *descs = nullptr;
+  *arena = nullptr;
+  ParsedFile pf;
+  if (int r = parse_file(nullptr, file, n, &pf)) return r;
+  Plan plan;
+  uint64_t work = 0;
+  int mh = 1;
+  for (const avr::SliceInfo& s : pf.slices) {
+    avr_slice_desc d = desc_from_header(s);
+    append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
+    d.payload_size = (uint32_t)s.size;
+    d.read_limit = (uint32_t)s.read_limit;
+    d.coded = recodable_candidate(s);
+    d.out_offset = work;
+    d.out_capacity = (uint32_t)(s.size * 2 + 256);
+    work += ((uint64_t)d.out_capacity + 15) & ~15ull;
+    plan.max_w = std::max(plan.max_w, d.mb_width);
+    mh = std::max(mh, d.mb_height);
+    plan.descs.push_back(d);
+  }
+  plan.arena.resize(plan.arena.size() + 16, 0);
+  const size_t dn = sizeof(avr_slice_desc) * plan.descs.size();
+  *descs = (avr_slice_desc*)malloc(dn ? dn : 1);
+  *arena = (uint8_t*)malloc(plan.arena.size());
+  if (!*descs || !*arena) {
+    free(*descs);
+    free(*arena);
+    *descs = nullptr;
+    *arena = nullptr;
+    return AVR_ERR_OUT_OF_MEMORY;
+  }
+  if (dn) memcpy(*descs, plan.descs.data(), dn);
+  memcpy(*arena, plan.arena.data(), plan.arena.size());
+  *n_slices = (int)plan.descs.size();
+  *arena_len = plan.arena.size();
+  *work_len = work;
+  *max_w = plan.max_w;
+  *max_h = mh;
+  return AVR_OK;
 }
 
 int avr_pack_outputs(avr_ctx* c, const avr_slice_desc* d_desc, const avr_slice_result* d_res, int n,

@@ -441,9 +441,9 @@ bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals) {
   nals->clear();
   const bool mp4 = n >= 8 && (rd32(file + 4) == fourcc("ftyp") || rd32(file + 4) == fourcc("moov") ||
                               rd32(file + 4) == fourcc("mdat") || rd32(file + 4) == fourcc("free"));
-  if (mp4) return demux_mp4(file, n, nals);
+  if (mp4) return demux_mp4(file, n, nals) && !nals->empty();
   demux_annexb(file, n, nals);
-  return true;
+  return !nals->empty();   // nothing H.264 in it: av_decoder::run throws (recode.cpp:92-93)
 }
 
 bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s) {

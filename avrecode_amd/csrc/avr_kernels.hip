@@ -1078,6 +1078,62 @@ __global__ void pack_kernel(const avr_slice_desc* descs, const avr_slice_result*
   for (uint32_t i = threadIdx.x; i < len; i += blockDim.x) dst[i] = src[i];
 }
 
+// ------------------------------------------------------------------------------- roundtrip chain
+// Decompress descriptors from the compress results, on the device (no host round trip): the
+// recoded stream of slice k is read where compress wrote it, the regenerated CABAC bytes go to
+// the payload's own offset in a buffer laid out like the input arena.
+__global__ void derive_decompress_descs_kernel(const avr_slice_desc* d, const avr_slice_result* rc, int n,
+                                               avr_slice_desc* dd) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  avr_slice_desc x = d[k];
+  const bool coded = x.coded && rc[k].status == 0;
+  x.payload_offset = d[k].out_offset;
+  x.payload_size = coded ? rc[k].out_len : 0;
+  x.read_limit = x.payload_size;
+  x.out_offset = d[k].payload_offset;
+  x.out_capacity = d[k].payload_size + 16;  // the input arena reserves >= size + 16 per payload
+  x.coded = coded;
+  dd[k] = x;
+}
+
+// Last-byte rule (decompressor::run, recode.cpp:1345-1356) + compare: with parity(size) != parity(L)
+// the stored last byte is appended, otherwise it overwrites the last regenerated byte; either way
+// the result equals the payload iff L is size-1 or size and the first size-1 bytes agree.
+// One workgroup per slice, 16-byte loads where both sides are aligned.
+__global__ __launch_bounds__(256) void verify_kernel(const avr_slice_desc* d, const avr_slice_result* rc,
+                                                     const avr_slice_result* rd, int n, const uint8_t* in,
+                                                     const uint8_t* regen, int32_t* verdict) {
+  const int k = blockIdx.x;
+  if (k >= n) return;
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  if (!d[k].coded || rc[k].status != 0) {
+    if (threadIdx.x == 0) verdict[k] = 2;
+    return;
+  }
+  const uint32_t size = d[k].payload_size, len = rd[k].out_len;
+  if (rd[k].status != 0 || !(len == size || len + 1 == size) || size == 0) {
+    if (threadIdx.x == 0) verdict[k] = 0;
+    return;
+  }
+  const uint8_t* a = in + d[k].payload_offset;
+  const uint8_t* b = regen + d[k].payload_offset;
+  const uint32_t m = size - 1, m16 = m / 16;
+  int local = 0;
+  const uint4* a4 = (const uint4*)a;
+  const uint4* b4 = (const uint4*)b;
+  for (uint32_t i = threadIdx.x; i < m16; i += blockDim.x) {
+    uint4 x = a4[i], y = b4[i];
+    local |= (x.x != y.x) | (x.y != y.y) | (x.z != y.z) | (x.w != y.w);
+  }
+  for (uint32_t i = m16 * 16 + threadIdx.x; i < m; i += blockDim.x) local |= a[i] != b[i];
+  if (local) atomicOr(&bad, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) verdict[k] = bad ? 0 : 1;
+}
+
 // ------------------------------------------------------------------------------- launchers
 size_t shared_bytes(int max_mb_width) { return sizeof(Shared) + (size_t)max_mb_width * sizeof(EdgeRec); }
 
@@ -1105,6 +1161,20 @@ hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const
       hipLaunchKernelGGL(slices_parallel_kernel<MODE_GENERATE>, dim3(n), dim3(64), lds, stream, T, descs, n, in, out, res,
                          est);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_derive_decompress(const avr_slice_desc* descs, const avr_slice_result* rc, int n,
+                                    avr_slice_desc* dd, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(derive_decompress_descs_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, descs, rc, n, dd);
+  return hipGetLastError();
+}
+
+hipError_t launch_verify(const avr_slice_desc* descs, const avr_slice_result* rc, const avr_slice_result* rd, int n,
+                         const uint8_t* in, const uint8_t* regen, int32_t* verdict, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(verify_kernel, dim3(n), dim3(256), 0, stream, descs, rc, rd, n, in, regen, verdict);
   return hipGetLastError();
 }
 

@@ -1,0 +1,223 @@
+"""Headline benchmark: input H.264 MB/s (compress + roundtrip), bit-exact, PARALLEL model.
+
+Workload (BASELINE.json configs[2]): a synthetic batch of 1024 independent
+1080p (120x68 MB) 4:2:0 High-profile CABAC I-slices, QP 22/26/30 by i%3, 8x8 transform on, made by
+the device generator (avr_synthesize_stream) before timing.  One step = one roundtrip of the whole
+batch, resident in HBM: compress every slice (CABAC decode -> model -> re-encode), derive the
+decompress descriptors, decompress every slice (model decode -> CABAC re-encode) and verify the
+regenerated payloads + last-byte patch against the input (recode.cpp:1594-1624 per slice).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+Weak scaling: every rank roundtrips its own 1024-slice batch (different seeds); slices are
+independent in the parallel model, so there is no collective in the timed region.  value = bytes of
+input H.264 processed by all ranks / max-over-ranks wall time.
+
+roofline: the dominant slice kernel (compress or decompress, whichever is longer), algorithmic
+bytes per launch = S + C (compress reads the S payload bytes and writes C re-coded bytes;
+decompress the reverse) over its average launch time from HIP events on the launch stream.
+traffic: HBM bytes per launch of that kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+(profiles/<round>_pmc.json, written by scripts/pmc_traffic.py), or null.
+cpu_baseline: the oracle (CPU restatement of the reference algorithm, oracle/) compress +
+decompress of the first slices of the same batch on one host core, ~10-20 s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+QPS = (22, 26, 30)
+METRIC = "input H.264 MB/s (compress+roundtrip) at 1/2/4/8 GPUs; bit-exact pass"
+WORKLOAD = "synthetic batch of independent 1080p CABAC I-slices (BASELINE configs[2])"
+
+
+def synth_params(qp, seed, args):
+    import avrecode_amd as avr
+    return avr.SynthParams(mb_width=args.mb_width, mb_height=args.mb_height, slice_type=2, slice_qp=qp,
+                           chroma_format_idc=1, transform_8x8_mode=1, seed=seed)
+
+
+def make_input(ctx, n, rank, args):
+    """Annex-B stream of n slices: three parameter-set groups (QP 22/26/30), i%3 -> QP."""
+    parts = []
+    for j, qp in enumerate(QPS):
+        k = (n - j + 2) // 3
+        if k:
+            parts.append(ctx.synthesize(synth_params(qp, args.seed + 1000003 * rank + j, args), k))
+    return b"".join(parts)
+
+
+def cpu_baseline(ctx, args, n_bytes_hint):
+    """Oracle P-mode compress+decompress of the first slices of the same batch, one core."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _oracle
+    _oracle.build_oracle()
+    t_budget = args.cpu_seconds
+    # time one slice per QP group first, then size the sample to the budget
+    total_bytes, total_t, slices = 0, 0.0, 0
+    k = 1
+    while True:
+        sample = b"".join(ctx.synthesize(synth_params(qp, args.seed + j, args), k) for j, qp in enumerate(QPS))
+        t0 = time.perf_counter()
+        _, recs = _oracle.slices_p(sample, check_recodable=False)
+        dt = time.perf_counter() - t0
+        assert all(r["status_c"] == 0 and r["status_d"] == 0 for r in recs)
+        total_bytes, total_t, slices = len(sample), dt, len(recs)
+        if dt >= t_budget * 0.5 or k >= 64:
+            break
+        k = max(k + 1, min(64, int(k * t_budget / max(dt, 1e-3))))
+    return {"value": total_bytes / total_t / 1e6, "unit": "MB/s", "cores": 1, "kind": "port",
+            "sample": f"first {slices} slices of the batch ({k} per QP group, {total_bytes} input bytes), oracle "
+                      f"fresh-model compress+decompress, {total_t:.1f} s"}
+
+
+def load_traffic(args, kernel):
+    p = ROOT / "profiles" / f"{args.round}_pmc.json"
+    if not p.exists():
+        return None
+    try:
+        j = json.loads(p.read_text())
+        if j.get("slices") != args.slices or j.get("mb") != [args.mb_width, args.mb_height]:
+            return None
+        return j["kernels"][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--slices", type=int, default=1024)
+    ap.add_argument("--mb-width", type=int, default=120)
+    ap.add_argument("--mb-height", type=int, default=68)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--round", default="r01")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import avrecode_amd as avr
+    from avrecode_amd.batch import DeviceBatch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    ctx = avr.Context(local)
+    data = make_input(ctx, args.slices, rank, args)
+    ps = avr.parse_stream(data)
+    assert len(ps.descs) == args.slices
+    batch = DeviceBatch(ctx, ps)
+    stream = torch.cuda.Stream(dev)
+    mk = lambda: [torch.cuda.Event(enable_timing=True) for _ in range(4)]  # noqa: E731
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            batch.roundtrip_timed(mk(), avr.MODEL_PARALLEL, stream)
+        stream.synchronize()
+        verdict = batch.verdicts()
+        bit_exact = bool((verdict == 1).all())
+        res_c = batch.results("c")
+        S = int(ps.descs["payload_size"].sum())
+        C = int(res_c["out_len"][verdict == 1].sum())
+        bins = int(res_c["bins"].sum())
+
+        evs = [mk() for _ in range(args.steps)]
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            batch.roundtrip_timed(evs[k], avr.MODEL_PARALLEL, stream)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+    # the timed steps recomputed the same outputs: re-check them
+    bit_exact = bit_exact and bool((batch.verdicts() == 1).all())
+    t_comp = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps / 1e3
+    t_dec = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps / 1e3
+
+    tot = torch.tensor([elapsed, len(data), 0.0 if bit_exact else 1.0], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = tot[0:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tot[1:3].clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, total_bytes, bad = float(mx[0]), float(sm[0]), float(sm[1])
+    else:
+        total_bytes, bad = float(len(data)), float(tot[2])
+
+    if rank == 0:
+        ms = elapsed / args.steps * 1e3
+        dominant, t_dom = ("compress", t_comp) if t_comp >= t_dec else ("decompress", t_dec)
+        kernel_name = "slices_parallel_kernel<0>" if dominant == "compress" else "slices_parallel_kernel<1>"
+        achieved = (S + C) / t_dom / 1e9
+        line = {
+            "metric": METRIC,
+            "value": total_bytes * args.steps / elapsed / 1e6,
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (device generator, seeded)",
+            "bit_exact": bit_exact and bad == 0,
+            "config": {
+                "workload": WORKLOAD,
+                "slices_per_gpu": args.slices,
+                "mb": [args.mb_width, args.mb_height],
+                "qp": list(QPS),
+                "model": "parallel (fresh model per slice)",
+                "input_bytes_per_gpu": len(data),
+                "payload_bytes_S": S,
+                "recoded_bytes_C": C,
+                "bins": bins,
+                "compress_ms": t_comp * 1e3,
+                "decompress_ms": t_dec * 1e3,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": kernel_name,
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_traffic(args, kernel_name),
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(ctx, args, len(data))
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

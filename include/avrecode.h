@@ -110,6 +110,45 @@ int avr_decompress_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, int n, int
 int avr_pack_outputs(avr_ctx* ctx, const avr_slice_desc* d_desc, const avr_slice_result* d_res, int n,
                      const uint8_t* d_out, uint8_t* d_packed, uint64_t* d_offsets, void* stream);
 
+/* Device-resident roundtrip of a slice batch: recode.cpp:1594-1624 applied per slice, without the
+ * container.  Compress d_in -> d_work (at each desc's out_offset), derive the decompress
+ * descriptors on the device (d_dec_desc, n entries of scratch), decompress d_work -> d_regen
+ * (slice k at d_desc[k].payload_offset, i.e. d_regen has d_in's layout), then apply the last-byte
+ * rule (recode.cpp:1345-1356) and compare with the payload.  d_verdict[k]: 1 bit-exact,
+ * 0 mismatch, 2 not coded (compress status != 0: the container stores it skip_coded).
+ * Everything is enqueued on `stream`; nothing is synchronised. */
+int avr_roundtrip_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, int n, int max_mb_width, int max_mb_height,
+                         const uint8_t* d_in, uint8_t* d_work, uint8_t* d_regen, avr_slice_desc* d_dec_desc,
+                         avr_slice_result* d_res_c, avr_slice_result* d_res_d, int32_t* d_verdict, int model,
+                         void* stream);
+
+/* The two device steps avr_roundtrip_slices runs between its compress and decompress launches,
+ * for callers that time or overlap the halves themselves (same semantics as above). */
+int avr_derive_decompress_descs(avr_ctx* ctx, const avr_slice_desc* d_desc, const avr_slice_result* d_res_c, int n,
+                                avr_slice_desc* d_dec_desc, void* stream);
+int avr_verify_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, const avr_slice_result* d_res_c,
+                      const avr_slice_result* d_res_d, int n, const uint8_t* d_in, const uint8_t* d_regen,
+                      int32_t* d_verdict, void* stream);
+
+/* ------------------------------------------------------------ host-side slice extraction */
+/* What FFmpeg hands AVCodecHooks.cabac.init_decoder for every CABAC slice of a file
+ * (av_decoder::decode_video, recode.cpp:73-135): demux (MP4/avcC or Annex-B), unescape, parse
+ * SPS/PPS/SEI/slice headers.  Host only, no device needed.  Returns malloc'd arrays (free with
+ * avr_free): *descs (n entries; payload_offset/read_limit index *arena, out_offset/out_capacity
+ * index a work buffer of *work_len bytes sized for compress output) and *arena (payloads, each
+ * 16-byte aligned, followed by >= 16 zero bytes).  desc.coded = 0 for slices the recoder does not
+ * take (unsupported syntax, or shorter than a surrogate marker, recode.cpp:1285). */
+int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
+                     size_t* arena_len, size_t* work_len, int* max_mb_width, int* max_mb_height);
+
+/* Rank 0 of a sharded PARALLEL-model compress: build the Recoded container from per-slice outputs
+ * gathered from every rank (compressor::run + find_next_coded_block_and_emit_literal,
+ * recode.cpp:1115-1132, 1275-1297).  Host only.  Slice k (avr_parse_stream order) is coded when it
+ * is a candidate and status[k] == 0; its re-coded bytes are recoded[offsets[k] .. + lens[k]).
+ * The result is byte-identical to avr_compress_file(..., AVR_MODEL_PARALLEL). */
+int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
+                           const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len);
+
 /* --------------------------------------------------------------- synthetic H.264 (benchmarks) */
 typedef struct {
   int32_t mb_width, mb_height;   /* e.g. 120 x 68 for 1080p */

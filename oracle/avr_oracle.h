@@ -237,9 +237,10 @@ int avr_decompress_slice_p(const avr_slice_hdr_t *h, const uint8_t *recoded, siz
 int avr_cabac_regenerate(const avr_slice_hdr_t *h, const uint8_t *payload, size_t n, obuf_t *cabac,
                          size_t *bins, size_t *end_bitpos);
 
-/* Synthetic slice generator: walks slice_data with seeded random bin choices and CABAC-encodes */
-/* them (used to build goldens and the CPU-baseline corpus).                                   */
-int avr_generate_slice(const avr_slice_hdr_t *h, uint64_t seed, int target_mbs, obuf_t *payload);
+/* Per-slice fresh-model compress -> decompress records for CABAC slices [lo, hi) of a file      */
+/* (layout in oracle_recode.c).  Returns the file's CABAC slice count, or -1.                   */
+long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int check_recodable, uint8_t **out,
+                         size_t *out_len);
 
 /* protobuf wire codec for recode.proto */
 typedef struct {

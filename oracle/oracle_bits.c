@@ -536,7 +536,7 @@ int avr_demux(const uint8_t *file, size_t n, avr_nal_t **out) {
   int is_mp4 = n >= 8 && (rd32(file + 4) == FOURCC('f', 't', 'y', 'p') || rd32(file + 4) == FOURCC('m', 'o', 'o', 'v') ||
                           rd32(file + 4) == FOURCC('m', 'd', 'a', 't') || rd32(file + 4) == FOURCC('f', 'r', 'e', 'e'));
   int r = is_mp4 ? demux_mp4(file, n, &nv) : demux_annexb(file, n, &nv);
-  if (r) {
+  if (r || nv.n == 0) { /* no H.264 in it: the reference's avformat_open_input fails */
     free(nv.v);
     *out = NULL;
     return -1;

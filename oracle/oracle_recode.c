@@ -507,11 +507,74 @@ int avr_compress_slice_p(const avr_slice_hdr_t *h, const uint8_t *payload, size_
   avr_model_free(m);
   return r;
 }
+static int decompress_slice_with_model_fresh(const slice_t *s, const uint8_t *rc, size_t n, obuf_t *cabac) {
+  avr_model_t *m = avr_model_new();
+  int r = decompress_slice_with_model(m, &s->h, s->picture_id, rc, n, cabac);
+  avr_model_free(m);
+  return r;
+}
 int avr_decompress_slice_p(const avr_slice_hdr_t *h, const uint8_t *rc, size_t n, obuf_t *cabac) {
   avr_model_t *m = avr_model_new();
   int r = decompress_slice_with_model(m, h, 0, rc, n, cabac);
   avr_model_free(m);
   return r;
+}
+
+/* Per-slice P-mode cross-check (tests, bench cpu_baseline): for CABAC slices [lo, hi) of a file,
+ * in the order avr_parse_stream enumerates them, record
+ *   i32 recodable  (slice_recodable: parse + regenerate + last-byte rule restores the payload)
+ *   i32 status_c, u32 bins, u32 len_c, recoded bytes      (fresh-model compress)
+ *   i32 status_d, u32 len_d, regenerated bytes            (fresh-model decompress of the above)
+ * into *out.  check_recodable = 0 skips the regeneration pre-check (timing the bare algorithm).
+ * Returns the number of slices seen in the whole file, or -1. */
+static void put_u32(obuf_t *o, uint32_t v) {
+  for (int k = 0; k < 4; k++) ob_put(o, (uint8_t)(v >> (8 * k)));
+}
+long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int check_recodable, uint8_t **out,
+                         size_t *out_len) {
+  avr_nal_t *nals;
+  int nn = avr_demux(file, n, &nals);
+  if (nn < 0) return -1;
+  stream_state_t *st = (stream_state_t *)calloc(1, sizeof(stream_state_t));
+  st->x264_build = -1;
+  obuf_t o;
+  ob_init(&o);
+  long idx = 0;
+  for (int i = 0; i < nn; i++) {
+    slice_t s;
+    if (!nal_to_slice(st, file + nals[i].offset, nals[i].size, &s)) continue;
+    if (idx >= lo && idx < hi) {
+      put_u32(&o, (uint32_t)(check_recodable ? slice_recodable(&s) : -1));
+      obuf_t rc, cab;
+      size_t bins = 0;
+      int rcs = -30;
+      if (s.h.supported) {
+        avr_model_t *m = avr_model_new();
+        rcs = compress_slice_with_model(m, &s, &rc, &bins);
+        avr_model_free(m);
+      } else {
+        ob_init(&rc);
+      }
+      put_u32(&o, (uint32_t)rcs);
+      put_u32(&o, (uint32_t)bins);
+      put_u32(&o, (uint32_t)rc.len);
+      ob_append(&o, rc.data, rc.len);
+      int rds = rcs == 0 ? decompress_slice_with_model_fresh(&s, rc.data, rc.len, &cab) : -31;
+      if (rcs != 0) ob_init(&cab);
+      put_u32(&o, (uint32_t)rds);
+      put_u32(&o, (uint32_t)cab.len);
+      ob_append(&o, cab.data, cab.len);
+      ob_free(&rc);
+      ob_free(&cab);
+    }
+    idx++;
+    free(s.rbsp);
+  }
+  free(st);
+  free(nals);
+  *out = o.data;
+  *out_len = o.len;
+  return idx;
 }
 
 /* ========================================================================== compress */

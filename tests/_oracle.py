@@ -75,3 +75,46 @@ def oracle_cli(cmd, path, mode="R", out=None):
         if cmd == "roundtrip":
             return r.stdout
         return o.read_bytes()
+
+
+def slices_p(data: bytes, lo: int = 0, hi: int = 1 << 62, check_recodable: bool = True):
+    """Per-slice fresh-model (P-mode) compress -> decompress through the oracle.
+
+    Returns (total_slices, records); each record is a dict with recodable, status_c, bins, recoded,
+    status_d, regen (avr_oracle_slices_p, oracle/oracle_recode.c)."""
+    import struct
+    L = lib()
+    f = L.avr_oracle_slices_p
+    f.restype = ctypes.c_long
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_long, ctypes.c_long, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+    out, olen = ctypes.c_void_p(), ctypes.c_size_t()
+    total = f(data, len(data), lo, hi, 1 if check_recodable else 0, ctypes.byref(out), ctypes.byref(olen))
+    if total < 0:
+        raise RuntimeError("avr_oracle_slices_p: demux failed")
+    raw = ctypes.string_at(out.value, olen.value) if olen.value else b""
+    ctypes.CDLL(None).free(ctypes.c_void_p(out.value))
+    recs, p = [], 0
+    while p < len(raw):
+        rec, sc, bins, lc = struct.unpack_from("<iiII", raw, p)
+        p += 16
+        rc = raw[p:p + lc]
+        p += lc
+        sd, ld = struct.unpack_from("<iI", raw, p)
+        p += 8
+        rg = raw[p:p + ld]
+        p += ld
+        recs.append(dict(recodable=rec, status_c=sc, bins=bins, recoded=rc, status_d=sd, regen=rg))
+    return total, recs
+
+
+def patch_restores(regen: bytes, payload: bytes) -> bool:
+    """decompressor::run's last-byte rule (recode.cpp:1345-1356) applied to regen equals payload."""
+    size = len(payload)
+    if size < 1:
+        return False
+    if (len(regen) & 1) != (size & 1):
+        fixed = regen + payload[-1:]
+    else:
+        fixed = regen[:-1] + payload[-1:] if regen else b""
+    return fixed == payload
