@@ -82,13 +82,13 @@ int fail(avr_ctx* c, int code, const std::string& msg) {
 void build_tables(avr::EngineTables* t) {
   memset(t, 0, sizeof(*t));
   for (int q = 0; q < 4; q++)
-    for (int i = 0; i < 64; i++) t->lps[q * 128 + 2 * i] = t->lps[q * 128 + 2 * i + 1] = avr::kRangeTabLPS[i][q];
+    for (int i = 0; i < 64; i++) t->hot.lps[q * 128 + 2 * i] = t->hot.lps[q * 128 + 2 * i + 1] = avr::kRangeTabLPS[i][q];
   for (int i = 0; i < 64; i++) {
     int mps = i < 62 ? i + 1 : i;
-    t->mlps[128 + 2 * i] = (uint8_t)(2 * mps);
-    t->mlps[128 + 2 * i + 1] = (uint8_t)(2 * mps + 1);
-    t->mlps[127 - 2 * i] = (uint8_t)(i == 0 ? 1 : 2 * avr::kTransIdxLPS[i]);
-    t->mlps[127 - (2 * i + 1)] = (uint8_t)(i == 0 ? 0 : 2 * avr::kTransIdxLPS[i] + 1);
+    t->hot.mlps[128 + 2 * i] = (uint8_t)(2 * mps);
+    t->hot.mlps[128 + 2 * i + 1] = (uint8_t)(2 * mps + 1);
+    t->hot.mlps[127 - 2 * i] = (uint8_t)(i == 0 ? 1 : 2 * avr::kTransIdxLPS[i]);
+    t->hot.mlps[127 - (2 * i + 1)] = (uint8_t)(i == 0 ? 0 : 2 * avr::kTransIdxLPS[i] + 1);
   }
   for (int tbl = 0; tbl < 4; tbl++)
     for (int c = 0; c < 1024; c++) {
@@ -101,9 +101,9 @@ void build_tables(avr::EngineTables* t) {
     int l = 0;
     while ((1u << l) < d) l++;
     unsigned __int128 num = (unsigned __int128)1 << (63 + l);
-    t->div_m[d] = (uint64_t)((num + d - 1) / d);
-    t->div_s[d] = (uint8_t)(l - 1);
-    t->div_top[d] = (1ull << 63) / d;
+    t->hot.div_m[d] = (uint64_t)((num + d - 1) / d);
+    t->hot.div_s[d] = (uint8_t)(l - 1);
+    t->hot.div_top[d] = (1ull << 63) / d;
   }
   // reverse_scan_8 neighbours (recode.cpp:279-312, 444-447)
   static const uint8_t scan8[48] = {
@@ -126,9 +126,9 @@ void build_tables(avr::EngineTables* t) {
     bool cr;
     int s = scan8[n];
     int l = cell_block(s >> 3, (s & 7) - 1, &cr);
-    t->nb_left[n] = (uint8_t)(l | (cr ? 128 : 0));
+    t->hot.nb_left[n] = (uint8_t)(l | (cr ? 128 : 0));
     int u = cell_block((s >> 3) - 1, s & 7, &cr);
-    t->nb_up[n] = (uint8_t)(u | (cr ? 128 : 0));
+    t->hot.nb_up[n] = (uint8_t)(u | (cr ? 128 : 0));
   }
   const double alpha = std::pow(0.01875 / 0.5, 1.0 / 63.0);
   for (int s = 0; s < 64; s++) t->gen_plps[s] = (uint16_t)std::lround(65536.0 * 0.5 * std::pow(alpha, s));
@@ -138,8 +138,8 @@ bool check_reciprocals(const avr::EngineTables& t) {
   uint64_t x = 0x9E3779B97F4A7C15ull;
   for (uint32_t d = 2; d < 128; d++) {
     auto q = [&](uint64_t v) -> uint64_t {
-      if (v >> 63) return t.div_top[d];
-      return (uint64_t)(((unsigned __int128)v * t.div_m[d]) >> 64) >> t.div_s[d];
+      if (v >> 63) return t.hot.div_top[d];
+      return (uint64_t)(((unsigned __int128)v * t.hot.div_m[d]) >> 64) >> t.hot.div_s[d];
     };
     const uint64_t edge[] = {0, 1, d - 1, d, d + 1, (1ull << 63) - 1, 1ull << 63, (1ull << 62) + 12345};
     for (uint64_t v : edge)

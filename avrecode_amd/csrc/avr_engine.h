@@ -20,15 +20,21 @@ namespace avr {
 
 constexpr int kStage = 1024;  // bytes per LDS staging window
 
-struct EngineTables {
+// Tables read on every bin: copied into each workgroup's LDS at kernel start.
+struct HotTables {
+  uint64_t div_m[128];    // ceil(2^(63+l)/d), l = ceil(log2 d)
+  uint64_t div_top[128];  // floor(2^63 / d)
   uint8_t lps[512];       // [q*128 + state]
   uint8_t mlps[256];      // [128+s] after MPS, [127-s] after LPS
-  int8_t mn[4][1024][2];  // init (m,n): [0] I, [1..3] cabac_init_idc 0..2
-  uint64_t div_m[128];    // ceil(2^(63+l)/d), l = ceil(log2 d)
   uint8_t div_s[128];     // l - 1
-  uint64_t div_top[128];  // floor(2^63 / d)
   uint8_t nb_left[48];    // get_neighbor_sub_mb: block left of n (| 128 if in the left macroblock)
   uint8_t nb_up[48];      //                      block above n (| 128 if in the upper macroblock)
+};
+static_assert(sizeof(HotTables) % 16 == 0, "HotTables is copied in 16-byte units");
+
+struct EngineTables {
+  HotTables hot;
+  int8_t mn[4][1024][2];  // init (m,n): [0] I, [1..3] cabac_init_idc 0..2
   uint16_t gen_plps[64];  // generator: p_LPS(pStateIdx) * 65536
 };
 
@@ -114,7 +120,7 @@ __device__ __forceinline__ void cd_init(CabacDecoder& d, InStream& in) {  // 9.3
 // bits consumed by the spec decoder so far (9 + renormalisation shifts)
 __device__ __forceinline__ uint32_t cd_bitpos(const CabacDecoder& d) { return 8u * d.next - (uint32_t)d.avail; }
 
-__device__ __forceinline__ int cd_decision(CabacDecoder& d, InStream& in, uint8_t* state, const EngineTables* T) {
+__device__ __forceinline__ int cd_decision(CabacDecoder& d, InStream& in, uint8_t* state, const HotTables* T) {
   uint32_t s = *state;
   uint32_t lps = T->lps[((d.range >> 6) & 3) * 128 + s];
   d.range -= lps;
@@ -208,7 +214,7 @@ __device__ __forceinline__ void ce_renorm(CabacEncoder& e, OutStream& o) {
   if (e.queue >= 0) ce_putbyte(e, o);
 }
 __device__ __forceinline__ void ce_decision(CabacEncoder& e, OutStream& o, int bin, uint8_t* state,
-                                            const EngineTables* T) {
+                                            const HotTables* T) {
   uint32_t s = *state;
   uint32_t lps = T->lps[((e.range >> 6) & 3) * 128 + s];
   e.range -= lps;
@@ -247,12 +253,12 @@ __device__ __forceinline__ void ce_terminate(CabacEncoder& e, OutStream& o, int 
 }
 
 // ----------------------------------------------------------------- recoded coder (u64 / u8)
-__device__ __forceinline__ uint64_t rc_div(uint64_t range, uint32_t d, const EngineTables* T) {
+__device__ __forceinline__ uint64_t rc_div(uint64_t range, uint32_t d, const HotTables* T) {
   if (range >> 63) return T->div_top[d];
   return __umul64hi(range, T->div_m[d]) >> T->div_s[d];
 }
 // p1 = (range/(pos+neg))*pos  (recode.cpp:819); est = (pos-1) | (neg-1) << 8
-__device__ __forceinline__ uint64_t rc_p1(uint64_t range, uint32_t est, const EngineTables* T) {
+__device__ __forceinline__ uint64_t rc_p1(uint64_t range, uint32_t est, const HotTables* T) {
   uint32_t pos = (est & 0xff) + 1, neg = (est >> 8) + 1;
   return rc_div(range, pos + neg, T) * pos;
 }

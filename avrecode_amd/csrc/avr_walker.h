@@ -1,0 +1,1086 @@
+// The per-slice walker shared by the slice kernels (included by the avr_k_*.hip translation
+// units only; each instantiates one kernel so the kernels compile in parallel).
+//
+// One wavefront (64 lanes) owns one CABAC slice and runs the whole hot path for it:
+//   compress:    CABAC decode (fork ff_get_cabac*) -> H.264 slice_data() parse (the fork's
+//                caller of the hooks) -> h264_model keys/estimators (recode.cpp:615-1059)
+//                -> recoded arithmetic encode (arithmetic_code.h, recode.cpp:1061-1100, 1134-1268)
+//   decompress:  recoded decode -> parse -> model -> CABAC re-encode (recode.cpp:1411-1520,
+//                cabac_code.h)
+//   generate:    seeded bins -> parse -> CABAC encode (synthetic benchmark slices)
+// The serial part runs redundantly on all lanes (wave-uniform values); the lanes cooperate on
+// staging the byte streams through LDS and on clearing the model tables.  Everything is inlined
+// into the kernel (no calls, no private arrays) so the walker state lives in registers: a
+// non-inlined member call would put the whole Walker in scratch memory.
+//
+// Model modes: RM = true reproduces recode.cpp exactly (estimators and frame metadata persist
+// across slices; one wavefront walks all slices in file order).  RM = false applies the same
+// model to each slice from a fresh state (independent slices, one wavefront per slice).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "../../include/avrecode.h"
+#include "avr_engine.h"
+#include "avr_kernels.h"
+
+#define AVR_FI __device__ __forceinline__
+
+namespace avr {
+
+enum { MODE_COMPRESS = 0, MODE_DECOMPRESS = 1, MODE_GENERATE = 2 };
+enum { F_DEC = 1, F_SKIP = 2, F_INTRA = 4, F_I16 = 8, F_D16 = 16, F_T8 = 32, F_CPRED = 64 };
+enum { SE_OTHER = 0, SE_REF, SE_QPDELTA, SE_MVD_SUFFIX, SE_LEVEL_SUFFIX, SE_EOS, SE_PCM };
+
+static __constant__ uint8_t c_scan8[51] = {
+  4 + 1 * 8,  5 + 1 * 8,  4 + 2 * 8,  5 + 2 * 8,  6 + 1 * 8,  7 + 1 * 8,  6 + 2 * 8,  7 + 2 * 8,
+  4 + 3 * 8,  5 + 3 * 8,  4 + 4 * 8,  5 + 4 * 8,  6 + 3 * 8,  7 + 3 * 8,  6 + 4 * 8,  7 + 4 * 8,
+  4 + 6 * 8,  5 + 6 * 8,  4 + 7 * 8,  5 + 7 * 8,  6 + 6 * 8,  7 + 6 * 8,  6 + 7 * 8,  7 + 7 * 8,
+  4 + 8 * 8,  5 + 8 * 8,  4 + 9 * 8,  5 + 9 * 8,  6 + 8 * 8,  7 + 8 * 8,  6 + 9 * 8,  7 + 9 * 8,
+  4 + 11 * 8, 5 + 11 * 8, 4 + 12 * 8, 5 + 12 * 8, 6 + 11 * 8, 7 + 11 * 8, 6 + 12 * 8, 7 + 12 * 8,
+  4 + 13 * 8, 5 + 13 * 8, 4 + 14 * 8, 5 + 14 * 8, 6 + 13 * 8, 7 + 13 * 8, 6 + 14 * 8, 7 + 14 * 8,
+  0 + 0 * 8,  0 + 5 * 8,  0 + 10 * 8,
+};
+static __constant__ int16_t c_cbf_base[14] = {85, 89, 93, 97, 101, 1012, 460, 464, 468, 1016, 472, 476, 480, 1020};
+static __constant__ int16_t c_sig_base[14] = {105, 120, 134, 149, 152, 402, 484, 499, 513, 660, 528, 543, 557, 718};
+static __constant__ int16_t c_last_base[14] = {166, 181, 195, 210, 213, 417, 572, 587, 601, 690, 616, 631, 645, 748};
+static __constant__ int16_t c_abs_base[14] = {227, 237, 247, 257, 266, 426, 952, 962, 972, 708, 982, 992, 1002, 766};
+static __constant__ uint8_t c_sig8x8[63] = {
+  0, 1, 2, 3, 4, 5, 5, 4, 4, 3, 3, 4, 4, 4, 5, 5, 4, 4, 4, 4, 3, 3, 6, 7, 7, 7, 8, 9, 10, 9, 8, 7,
+  7, 6, 11, 12, 13, 11, 6, 7, 8, 9, 14, 10, 9, 8, 6, 11, 12, 13, 11, 6, 9, 14, 10, 9, 11, 12, 13, 11, 14, 10, 12};
+static __constant__ uint8_t c_last8x8[63] = {
+  0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
+  3, 3, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7, 8, 8, 8};
+static __constant__ uint8_t c_b_pairs[9][2] = {{1, 1}, {2, 2}, {1, 2}, {2, 1}, {1, 3}, {2, 3}, {3, 1}, {3, 2}, {3, 3}};
+// dense SIG estimator base per ctxBlockCat: 4096 per 4x4-class cat, 61440 for 8x8 cats (5, 9, 13)
+static __constant__ int32_t c_sig_est_base[14] = {0, 4096, 8192, 12288, 16384, 20480, 81920, 86016, 90112,
+                                           94208, 155648, 159744, 163840, 167936};
+constexpr int kSigEst = 229376;
+constexpr int kNzEst = 63 * 2 * 3 * 3 * 57;
+constexpr int kEstDefault = 1026;
+static_assert(kEstGlobal >= kSigEst + kNzEst, "estimator table size");
+
+struct MbRec {
+  uint8_t flags, is8x8;
+  uint16_t cbp;         // FFmpeg cbp_table layout: luma b0-3, chroma b4-5, chroma DC b6-7, luma DC b8-10
+  uint8_t nnz[3][16];   // coefficient count per 4x4, raster per plane
+  uint8_t mvd[2][16][2];
+  int8_t ref[2][4];
+  uint8_t direct8[4];
+  uint8_t mnnz[52];     // model BlockMeta.num_nonzeros[51]
+};
+struct EdgeRec {        // bottom edge of the macroblock above
+  uint8_t flags, pad;
+  uint16_t cbp;
+  uint8_t nnz[3][4];
+  uint8_t mvd[2][4][2];
+  int8_t ref[2][2];
+  uint8_t direct8[2];
+  uint8_t mnnz[52];
+  uint8_t pad2[2];
+};
+static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
+
+// LDS layout (per workgroup = one wavefront); the ring is sized by mb_width at launch.
+struct Shared {
+  HotTables tab;          // copy of EngineTables::hot (per-bin lookups stay in LDS)
+  uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
+  uint8_t state[1024];
+  uint16_t est[kEstDefault + 2];
+  uint8_t in_stage[kStage];
+  uint8_t out_stage[kStage];
+  MbRec cur, left;
+  uint16_t gen_p[1024];   // generator: P(bin = 1) in 1/65536 per context
+};
+
+template <int MODE, bool RM>
+struct Walker {
+  const HotTables* T;     // LDS copy
+  const EngineTables* G;  // global (init-only tables)
+  const avr_slice_desc* d;
+  Shared* sh;
+  EdgeRec* ring;
+  uint16_t* est_g;        // SIG + NZ estimators (global)
+  uint8_t* frames;        // RM: 2 frames of W*H*52 model bytes
+  int cur_frame;
+  // engines
+  InStream in;
+  OutStream out;
+  CabacDecoder cd;
+  CabacEncoder ce;
+  RecodedEncoder re;
+  RecodedDecoder rd;
+  uint64_t rng;
+  // slice state
+  int W, H, mb_x, mb_y, slice_type, is_b, cat_, t8mode;
+  int left_ok, top_ok, last_dqp_nz;
+  int err, finished;
+  uint32_t bins;
+  int target_mbs, mbs_done, last_mb;
+
+  // ------------------------------------------------------------------ bins through the model
+  AVR_FI int bin(int se, int k, int ctx) {
+    bins++;
+    if (MODE == MODE_COMPRESS) {
+      int b = cd_decision(cd, in, &sh->state[ctx], T);
+      uint32_t e = sh->est[ctx];
+      re_put(re, out, b, rc_p1(re.range, e, T));
+      sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
+      return b;
+    } else if (MODE == MODE_DECOMPRESS) {
+      uint32_t e = sh->est[ctx];
+      int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
+      ce_decision(ce, out, b, &sh->state[ctx], T);
+      return b;
+    } else {
+      int b = gen_bin(se, k, ctx);
+      ce_decision(ce, out, b, &sh->state[ctx], T);
+      return b;
+    }
+  }
+  AVR_FI int bypass(int se, int k) {
+    bins++;
+    if (MODE == MODE_COMPRESS) {
+      int b = cd_bypass(cd, in);
+      uint32_t e = sh->est[1024];
+      re_put(re, out, b, rc_p1(re.range, e, T));
+      sh->est[1024] = (uint16_t)est_update(e, b, 0x60);
+      return b;
+    } else if (MODE == MODE_DECOMPRESS) {
+      uint32_t e = sh->est[1024];
+      int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      sh->est[1024] = (uint16_t)est_update(e, b, 0x60);
+      ce_bypass(ce, out, b);
+      return b;
+    } else {
+      int b = gen_bypass(se, k);
+      ce_bypass(ce, out, b);
+      return b;
+    }
+  }
+  AVR_FI int terminate(int se) {
+    bins++;
+    int b;
+    if (MODE == MODE_COMPRESS) {
+      b = cd_terminate(cd, in);
+      uint32_t e = sh->est[1025];
+      re_put(re, out, b, rc_p1(re.range, e, T));
+      sh->est[1025] = (uint16_t)est_update(e, b, 0x60);
+      if (b) re_finish(re, out);
+    } else if (MODE == MODE_DECOMPRESS) {
+      uint32_t e = sh->est[1025];
+      b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      sh->est[1025] = (uint16_t)est_update(e, b, 0x60);
+      ce_terminate(ce, out, b);
+    } else {
+      b = se == SE_EOS ? (mbs_done >= target_mbs || last_mb) : 0;
+      ce_terminate(ce, out, b);
+    }
+    if (b && se == SE_EOS) finished = 1;
+    return b;
+  }
+
+  // ------------------------------------------------------------------ synthetic bin policy
+  AVR_FI uint32_t rnd() {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return (uint32_t)(rng >> 16) & 0xffff;
+  }
+  AVR_FI int gen_bin(int se, int k, int ctx) {
+    if (se == SE_REF && k >= avr_limit) return 0;
+    if (se == SE_QPDELTA && k >= 2) return 0;
+    return rnd() < sh->gen_p[ctx];
+  }
+  AVR_FI int gen_bypass(int se, int k) {
+    if ((se == SE_MVD_SUFFIX || se == SE_LEVEL_SUFFIX) && k >= 5 && k < 100) return 0;
+    return rnd() & 1;
+  }
+  int avr_limit;
+
+  // ------------------------------------------------------------------ neighbours (parser)
+  AVR_FI const EdgeRec& top() const { return ring[mb_x]; }
+  AVR_FI uint16_t nb_cbp_left() const {
+    return left_ok ? sh->left.cbp : ((sh->cur.flags & F_INTRA) ? 0x7CF : 0x00F);
+  }
+  AVR_FI uint16_t nb_cbp_top() const {
+    return top_ok ? ring[mb_x].cbp : ((sh->cur.flags & F_INTRA) ? 0x7CF : 0x00F);
+  }
+  // FFmpeg 4:4:4 8x8 coded_block_flag quirk for x264 < r151 (see oracle_walker.c)
+  AVR_FI int nnz_override(uint8_t nbflags, int* v) const {
+    if (cat_ != 3 || !(sh->cur.flags & F_T8) || (nbflags & F_T8)) return 0;
+    *v = (uint32_t)d->x264_build < 151u ? ((sh->cur.flags & F_INTRA) ? 64 : 0) : 0;
+    return 1;
+  }
+  AVR_FI int nnz_left(int p, int pw, int x4, int y4) const {
+    if (x4 > 0) return sh->cur.nnz[p][y4 * 4 + x4 - 1];
+    if (!left_ok) return (sh->cur.flags & F_INTRA) ? 64 : 0;
+    int v;
+    if (nnz_override(sh->left.flags, &v)) return v;
+    return sh->left.nnz[p][y4 * 4 + pw - 1];
+  }
+  AVR_FI int nnz_top(int p, int x4, int y4) const {
+    if (y4 > 0) return sh->cur.nnz[p][(y4 - 1) * 4 + x4];
+    if (!top_ok) return (sh->cur.flags & F_INTRA) ? 64 : 0;
+    int v;
+    if (nnz_override(ring[mb_x].flags, &v)) return v;
+    return ring[mb_x].nnz[p][x4];
+  }
+
+  // ------------------------------------------------------------------ model neighbours
+  // model num_nonzeros of a neighbouring macroblock (get_neighbor_sub_mb, recode.cpp:419-471)
+  AVR_FI int mnnz_left(int idx) const {
+    if (RM) return frames[(size_t)cur_frame * W * H * 52 + ((size_t)mb_y * W + mb_x - 1) * 52 + idx];
+    return left_ok ? sh->left.mnnz[idx] : 0;
+  }
+  AVR_FI int mnnz_top(int idx) const {
+    if (RM) return frames[(size_t)cur_frame * W * H * 52 + ((size_t)(mb_y - 1) * W + mb_x) * 52 + idx];
+    return top_ok ? ring[mb_x].mnnz[idx] : 0;
+  }
+  AVR_FI int mnnz_prev(int idx) const {
+    if (RM) return frames[(size_t)(1 - cur_frame) * W * H * 52 + ((size_t)mb_y * W + mb_x) * 52 + idx];
+    return 0;
+  }
+
+  // finished_queueing (recode.cpp:845-930): the 2/4/6 nnz bits, LSB first
+  AVR_FI int nz_bits(int cat, int n, int max, int is_dc, int c422, int count) {
+    const int bits = max > 16 ? 6 : max > 4 ? 4 : 2;
+    int has_left, has_above, lv = 0, av = 0;
+    if (n >= 48) {
+      has_left = mb_x > 0;
+      has_above = mb_y > 0;
+      if (has_left) lv = mnnz_left(n);
+      if (has_above) av = mnnz_top(n);
+    } else {
+      uint8_t L = T->nb_left[n], U = T->nb_up[n];
+      int li = L & 63, ui = U & 63;
+      if (max >= 32) { li &= ~3; ui &= ~3; }
+      has_left = !(L & 128) || mb_x > 0;
+      has_above = !(U & 128) || mb_y > 0;
+      if (has_left) lv = (L & 128) ? mnnz_left(li) : sh->cur.mnnz[li];
+      if (has_above) av = (U & 128) ? mnnz_top(ui) : sh->cur.mnnz[ui];
+    }
+    const int pv = mnnz_prev(n);
+    const int t = ((sh->cur.is8x8 | (max > 32)) ? 1 : 0) + 2 * is_dc + c422 + 4 * cat;
+    int so_far = 0;
+    for (int i = 0; i < bits; i++) {
+      const int cur_bit = 1 << i;
+      const int lb = has_left ? (lv >= cur_bit) : 2;
+      const int ab = av ? (av >= cur_bit) : 2;
+      const int pb = pv >= cur_bit;
+      const int idx = kSigEst + (((((cur_bit - 1 + so_far) * 2 + pb) * 3 + lb) * 3 + ab) * 57 + t);
+      uint32_t e = est_g[idx];
+      int b;
+      if (MODE == MODE_COMPRESS) {
+        b = (count >> i) & 1;
+        re_put(re, out, b, rc_p1(re.range, e, T));
+      } else {
+        b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      }
+      est_g[idx] = (uint16_t)est_update(e, b, 0x60);
+      if (b) so_far |= cur_bit;
+    }
+    return so_far;
+  }
+
+  AVR_FI int sig_est_index(int cat, int max, int is_dc, int c422, int zz, int nnz_m, int obs) const {
+    if (max == 64) return c_sig_est_base[cat] + (c_sig8x8[zz] * 64 + nnz_m) * 64 + obs;
+    int zo = (is_dc && c422) ? (zz < 2 ? 0 : zz < 4 ? 1 : 2) : zz;
+    return c_sig_est_base[cat] + (zo * 16 + nnz_m) * 16 + obs;
+  }
+
+  // significance map of one residual block; returns the coefficient count
+  AVR_FI int sig_map(int cat, int n, int max, int is_dc, int c422) {
+    const int numc8x8 = cat_ == 2 ? 2 : 1;
+    const int sb = c_sig_base[cat], lb = c_last_base[cat];
+    const int bits = max > 16 ? 6 : max > 4 ? 4 : 2;
+    const int mask = (1 << bits) - 1;
+    int cnt = 0;
+    if (MODE == MODE_COMPRESS) {
+      uint64_t sigmask = 0;
+      int pos, end = max - 2;
+      for (pos = 0; pos < max - 1; pos++) {
+        int sc, lc;
+        if (max == 64) { sc = c_sig8x8[pos]; lc = c_last8x8[pos]; }
+        else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
+        else sc = lc = pos;
+        bins++;
+        if (cd_decision(cd, in, &sh->state[sb + sc], T)) {
+          sigmask |= 1ull << pos;
+          cnt++;
+          bins++;
+          if (cd_decision(cd, in, &sh->state[lb + lc], T)) { end = pos; break; }
+        }
+      }
+      if (pos == max - 1) cnt++;
+      // model: nnz first (recode.cpp:1208-1221), then the buffered map (1244-1255)
+      nz_bits(cat, n, max, is_dc, c422, cnt);
+      const int nnz_m = cnt & mask;
+      int obs = 0;
+      for (int zz = 0; zz <= end; zz++) {
+        int b = (int)((sigmask >> zz) & 1);
+        int idx = sig_est_index(cat, max, is_dc, c422, zz, nnz_m, obs);
+        uint32_t e = est_g[idx];
+        re_put(re, out, b, rc_p1(re.range, e, T));
+        est_g[idx] = (uint16_t)est_update(e, b, 0x50);
+        obs += b;
+      }
+    } else if (MODE == MODE_DECOMPRESS) {
+      const int nnz_m = nz_bits(cat, n, max, is_dc, c422, 0);   // recode.cpp:1476-1486
+      int pos;
+      for (pos = 0; pos < max - 1; pos++) {
+        int sc, lc;
+        if (max == 64) { sc = c_sig8x8[pos]; lc = c_last8x8[pos]; }
+        else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
+        else sc = lc = pos;
+        int idx = sig_est_index(cat, max, is_dc, c422, pos, nnz_m, cnt);
+        uint32_t e = est_g[idx];
+        int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+        est_g[idx] = (uint16_t)est_update(e, b, 0x50);
+        bins++;
+        ce_decision(ce, out, b, &sh->state[sb + sc], T);
+        if (b) {
+          cnt++;
+          int last = nnz_m == cnt;   // derived EOB (recode.cpp:1437-1438)
+          bins++;
+          ce_decision(ce, out, last, &sh->state[lb + lc], T);
+          if (last) break;
+        }
+      }
+      if (pos == max - 1) cnt++;
+    } else {
+      int pos;
+      for (pos = 0; pos < max - 1; pos++) {
+        int sc, lc;
+        if (max == 64) { sc = c_sig8x8[pos]; lc = c_last8x8[pos]; }
+        else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
+        else sc = lc = pos;
+        if (bin(SE_OTHER, 0, sb + sc)) {
+          cnt++;
+          if (bin(SE_OTHER, 0, lb + lc)) break;
+        }
+      }
+      if (pos == max - 1) cnt++;
+    }
+    return cnt;
+  }
+
+  // residual_block_cabac() of one block; p/x4/y4 locate it in the walker's nnz grid
+  AVR_FI void residual_block(int cat, int n, int max, int is_dc, int c422, int p, int pw, int x4, int y4) {
+    if (err) return;
+    MbRec& cur = sh->cur;
+    int coded = 1;
+    if (max != 64 || cat_ == 3) {
+      int nza, nzb;
+      if (is_dc) {
+        int bit = cat == 3 ? (0x40 << (n - 49)) : (0x100 << (n - 48));
+        nza = (nb_cbp_left() & bit) != 0;
+        nzb = (nb_cbp_top() & bit) != 0;
+      } else {
+        nza = nnz_left(p, pw, x4, y4) > 0;
+        nzb = nnz_top(p, x4, y4) > 0;
+      }
+      coded = bin(SE_OTHER, 0, c_cbf_base[cat] + nza + 2 * nzb);
+    }
+    int cnt = 0;
+    if (coded) {
+      cnt = sig_map(cat, n, max, is_dc, c422);
+      // coeff_abs_level_minus1 + sign, reverse scan order
+      const int ab = c_abs_base[cat];
+      int gt1 = 0, eq1 = 0;
+      for (int i = cnt - 1; i >= 0 && !err; i--) {
+        int absl;
+        if (!bin(SE_OTHER, 0, ab + (gt1 ? 0 : min(4, 1 + eq1)))) {
+          absl = 1;
+        } else {
+          const int c1 = ab + 5 + min(4 - (cat == 3), gt1);
+          absl = 2;
+          while (absl < 15 && bin(SE_OTHER, 0, c1)) absl++;
+          if (absl >= 15) {
+            int k = 0;
+            while (bypass(SE_LEVEL_SUFFIX, k)) {
+              if (++k > 30) { err = -5; break; }
+            }
+            int v = 1;
+            while (k-- > 0) v += v + bypass(SE_LEVEL_SUFFIX, 100);
+            absl = 14 + v;
+          }
+        }
+        bypass(SE_OTHER, 0);
+        if (absl == 1) eq1++;
+        else gt1++;
+      }
+      cur.mnnz[n] = (uint8_t)cnt;             // end_coding_type recount (recode.cpp:935-947)
+      if (max > 32) cur.is8x8 = 1;
+    }
+    if (is_dc) {
+      if (cnt) cur.cbp |= (uint16_t)(cat == 3 ? (0x40 << (n - 49)) : (0x100 << (n - 48)));
+    } else if (max == 64) {
+      cur.nnz[p][y4 * 4 + x4] = cur.nnz[p][y4 * 4 + x4 + 1] = (uint8_t)cnt;
+      cur.nnz[p][y4 * 4 + 4 + x4] = cur.nnz[p][y4 * 4 + 4 + x4 + 1] = (uint8_t)cnt;
+    } else {
+      cur.nnz[p][y4 * 4 + x4] = (uint8_t)cnt;
+    }
+  }
+
+  AVR_FI void blk_pos(int n, int* x4, int* y4) const {
+    int s = c_scan8[n];
+    int row = s >> 3;
+    *x4 = (s & 7) - 4;
+    *y4 = row <= 4 ? row - 1 : row <= 9 ? row - 6 : row - 11;
+  }
+
+  // The macroblock's residual blocks in bitstream order (residual(), 7.3.5.3) are listed in LDS
+  // first and then coded through ONE inlined residual_block site, so the per-bin code exists
+  // once in the kernel instead of once per block kind.
+  AVR_FI int push_block(int nb, int cat, int n, int max, int is_dc, int c422, int p, int pw, int x4, int y4) {
+    sh->blk[nb] = (uint32_t)cat | (uint32_t)n << 4 | (uint32_t)max << 10 | (uint32_t)is_dc << 17 |
+                  (uint32_t)c422 << 18 | (uint32_t)p << 19 | (uint32_t)pw << 21 | (uint32_t)x4 << 24 |
+                  (uint32_t)y4 << 26;
+    return nb + 1;
+  }
+  AVR_FI int list_luma(int nb, int p, int i16, int cbp) {
+    const int cat_dc = p == 0 ? 0 : p == 1 ? 6 : 10;
+    const int cat_ac = cat_dc + 1, cat_4 = cat_dc + 2, cat_8 = p == 0 ? 5 : p == 1 ? 9 : 13;
+    int x4, y4;
+    if (i16) {
+      nb = push_block(nb, cat_dc, 48 + p, 16, 1, 0, p, 4, 0, 0);
+      if (cbp & 15)
+        for (int i = 0; i < 16; i++) {
+          blk_pos(16 * p + i, &x4, &y4);
+          nb = push_block(nb, cat_ac, 16 * p + i, 15, 0, 0, p, 4, x4, y4);
+        }
+      return nb;
+    }
+    for (int i8 = 0; i8 < 4; i8++) {
+      if (!(cbp & (1 << i8))) continue;
+      if (sh->cur.flags & F_T8) {
+        blk_pos(16 * p + 4 * i8, &x4, &y4);
+        nb = push_block(nb, cat_8, 16 * p + 4 * i8, 64, 0, 0, p, 4, x4, y4);
+      } else {
+        for (int i4 = 0; i4 < 4; i4++) {
+          int n = 16 * p + 4 * i8 + i4;
+          blk_pos(n, &x4, &y4);
+          nb = push_block(nb, cat_4, n, 16, 0, 0, p, 4, x4, y4);
+        }
+      }
+    }
+    return nb;
+  }
+
+  AVR_FI void residual(int i16, int cbp) {
+    int nb = list_luma(0, 0, i16, cbp);
+    if (cat_ == 3) {
+      nb = list_luma(nb, 1, i16, cbp);
+      nb = list_luma(nb, 2, i16, cbp);
+    } else if (cat_ == 1 || cat_ == 2) {
+      const int c422 = cat_ == 2;
+      if (cbp & 0x30)
+        for (int c = 0; c < 2; c++) nb = push_block(nb, 3, 49 + c, c422 ? 8 : 4, 1, c422, 1 + c, 2, 0, 0);
+      if (cbp & 0x20)
+        for (int c = 0; c < 2; c++)
+          for (int i8 = 0; i8 < (c422 ? 2 : 1); i8++)
+            for (int i = 0; i < 4; i++) {
+              int n = 16 + 16 * c + 8 * i8 + i, x4, y4;
+              blk_pos(n, &x4, &y4);
+              nb = push_block(nb, 4, n, 15, 0, 0, 1 + c, 2, x4, y4);
+            }
+    }
+    for (int j = 0; j < nb && !err; j++) {
+      const uint32_t b = sh->blk[j];
+      residual_block(b & 15, (b >> 4) & 63, (b >> 10) & 127, (b >> 17) & 1, (b >> 18) & 1, (b >> 19) & 3,
+                     (b >> 21) & 7, (b >> 24) & 3, (b >> 26) & 3);
+    }
+  }
+
+  // ------------------------------------------------------------------ prediction syntax
+  AVR_FI int ref_gt0(int list, int x4, int y4, int use_left) const {
+    uint8_t fl, dir;
+    int r;
+    if (use_left) {
+      if (x4 > 0) {
+        int b8 = (y4 >> 1) * 2 + ((x4 - 1) >> 1);
+        fl = sh->cur.flags | F_DEC; dir = sh->cur.direct8[b8]; r = sh->cur.ref[list][b8];
+      } else {
+        if (!left_ok) return 0;
+        int b8 = (y4 >> 1) * 2 + 1;
+        fl = sh->left.flags; dir = sh->left.direct8[b8]; r = sh->left.ref[list][b8];
+      }
+    } else {
+      if (y4 > 0) {
+        int b8 = ((y4 - 1) >> 1) * 2 + (x4 >> 1);
+        fl = sh->cur.flags | F_DEC; dir = sh->cur.direct8[b8]; r = sh->cur.ref[list][b8];
+      } else {
+        if (!top_ok) return 0;
+        fl = ring[mb_x].flags; dir = ring[mb_x].direct8[x4 >> 1]; r = ring[mb_x].ref[list][x4 >> 1];
+      }
+    }
+    (void)fl;
+    if (is_b && dir) return 0;
+    return r > 0;
+  }
+  AVR_FI int decode_ref(int list, int x4, int y4) {
+    int ctx = ref_gt0(list, x4, y4, 1) + 2 * ref_gt0(list, x4, y4, 0);
+    int ref = 0;
+    avr_limit = (list ? d->num_ref_idx_l1 : d->num_ref_idx_l0) - 1;
+    while (bin(SE_REF, ref, 54 + ctx)) {
+      ref++;
+      ctx = (ctx >> 2) + 4;
+      if (ref >= 32) { err = -3; return 0; }
+    }
+    return ref;
+  }
+  AVR_FI int mvd_nb(int list, int comp, int x4, int y4, int use_left) const {
+    if (use_left) {
+      if (x4 > 0) return sh->cur.mvd[list][y4 * 4 + x4 - 1][comp];
+      return left_ok ? sh->left.mvd[list][y4 * 4 + 3][comp] : 0;
+    }
+    if (y4 > 0) return sh->cur.mvd[list][(y4 - 1) * 4 + x4][comp];
+    return top_ok ? ring[mb_x].mvd[list][x4][comp] : 0;
+  }
+  AVR_FI int decode_mvd(int list, int comp, int x4, int y4) {
+    const int base = comp ? 47 : 40;
+    const int amvd = mvd_nb(list, comp, x4, y4, 1) + mvd_nb(list, comp, x4, y4, 0);
+    const int inc = amvd < 3 ? 0 : amvd <= 32 ? 1 : 2;
+    if (!bin(SE_OTHER, 0, base + inc)) return 0;
+    int mvd = 1, ctx = base + 3;
+    while (mvd < 9 && bin(SE_OTHER, 0, ctx)) {
+      if (mvd < 4) ctx++;
+      mvd++;
+    }
+    if (mvd >= 9) {
+      int k = 3;
+      while (bypass(SE_MVD_SUFFIX, k - 3)) {
+        mvd += 1 << k;
+        if (++k > 24) { err = -4; return 0; }
+      }
+      while (k--) mvd += bypass(SE_MVD_SUFFIX, 100) << k;
+    }
+    bypass(SE_OTHER, 0);
+    return mvd < 70 ? mvd : 70;
+  }
+  AVR_FI void mvd_part(int list, int px, int py, int pw, int ph) {
+    int mx = decode_mvd(list, 0, px, py);
+    int my = decode_mvd(list, 1, px, py);
+    for (int y = py; y < py + ph; y++)
+      for (int x = px; x < px + pw; x++) {
+        sh->cur.mvd[list][y * 4 + x][0] = (uint8_t)mx;
+        sh->cur.mvd[list][y * 4 + x][1] = (uint8_t)my;
+      }
+  }
+
+  AVR_FI int intra_mb_type(int base, int intra_slice, int* i16_cbp) {
+    // returns 0 = I_NxN, 1 = I_16x16, 2 = I_PCM
+    int ctx = 0;
+    if (intra_slice) {
+      if (left_ok && (sh->left.flags & F_I16)) ctx++;
+      if (top_ok && (ring[mb_x].flags & F_I16)) ctx++;
+      if (!bin(SE_OTHER, 0, base + ctx)) return 0;
+      base += 2;
+    } else {
+      if (!bin(SE_OTHER, 0, base)) return 0;
+    }
+    if (terminate(SE_PCM)) return 2;
+    int luma = bin(SE_OTHER, 0, base + 1) ? 15 : 0;
+    int chroma = 0;
+    if (bin(SE_OTHER, 0, base + 2)) chroma = 1 + bin(SE_OTHER, 0, base + 2 + intra_slice);
+    bin(SE_OTHER, 0, base + 3 + intra_slice);
+    bin(SE_OTHER, 0, base + 3 + 2 * intra_slice);
+    *i16_cbp = luma | (chroma << 4);
+    return 1;
+  }
+
+  // ------------------------------------------------------------------ one macroblock
+  AVR_FI void decode_mb() {
+    MbRec& cur = sh->cur;
+    const int nlists = is_b ? 2 : 1;
+    if (slice_type != 2) {
+      int ctx = (left_ok && !(sh->left.flags & F_SKIP)) + (top_ok && !(ring[mb_x].flags & F_SKIP));
+      if (bin(SE_OTHER, 0, (is_b ? 24 : 11) + ctx)) {
+        cur.flags |= F_SKIP;
+        if (is_b) {
+          cur.flags |= F_D16;
+          cur.direct8[0] = cur.direct8[1] = cur.direct8[2] = cur.direct8[3] = 1;
+        } else {
+          cur.ref[0][0] = cur.ref[0][1] = cur.ref[0][2] = cur.ref[0][3] = 0;
+        }
+        last_dqp_nz = 0;
+        return;
+      }
+    }
+    // mb_type
+    int intra = 0, kind = 0, i16_cbp = 0, nparts = 0, vertical = 0, pred0 = 0, pred1 = 0, direct16 = 0;
+    if (slice_type == 2) {
+      intra = 1;
+      kind = intra_mb_type(3, 1, &i16_cbp);
+    } else if (slice_type == 0) {
+      if (!bin(SE_OTHER, 0, 14)) {
+        int mt;
+        if (!bin(SE_OTHER, 0, 15)) mt = 3 * bin(SE_OTHER, 0, 16);
+        else mt = 2 - bin(SE_OTHER, 0, 17);
+        if (mt == 0) { nparts = 1; pred0 = 1; }
+        else if (mt == 1) { nparts = 2; pred0 = pred1 = 1; }
+        else if (mt == 2) { nparts = 2; vertical = 1; pred0 = pred1 = 1; }
+        else nparts = 4;
+      } else {
+        intra = 1;
+        kind = intra_mb_type(17, 0, &i16_cbp);
+      }
+    } else {
+      int ctx = (left_ok && !(sh->left.flags & F_D16)) + (top_ok && !(ring[mb_x].flags & F_D16));
+      if (!bin(SE_OTHER, 0, 27 + ctx)) {
+        direct16 = 1;
+        nparts = 4;
+      } else if (!bin(SE_OTHER, 0, 27 + 3)) {
+        nparts = 1;
+        pred0 = 1 + bin(SE_OTHER, 0, 27 + 5);
+      } else {
+        int bits = bin(SE_OTHER, 0, 27 + 4) << 3;
+        bits |= bin(SE_OTHER, 0, 27 + 5) << 2;
+        bits |= bin(SE_OTHER, 0, 27 + 5) << 1;
+        bits |= bin(SE_OTHER, 0, 27 + 5);
+        int mt = -1;
+        if (bits < 8) mt = bits + 3;
+        else if (bits == 13) { intra = 1; kind = intra_mb_type(32, 0, &i16_cbp); }
+        else if (bits == 14) mt = 11;
+        else if (bits == 15) mt = 22;
+        else mt = ((bits << 1) | bin(SE_OTHER, 0, 27 + 5)) - 4;
+        if (!intra) {
+          if (mt == 3) { nparts = 1; pred0 = 3; }
+          else if (mt == 22) nparts = 4;
+          else {
+            int k = mt - 4;
+            nparts = 2;
+            vertical = k & 1;
+            pred0 = c_b_pairs[k >> 1][0];
+            pred1 = c_b_pairs[k >> 1][1];
+          }
+        }
+      }
+    }
+    if (err) return;
+    if (intra && kind == 2) { err = -2; return; }  // I_PCM (skip_bytes hook, recode.cpp:161-163)
+    int no_sub_lt8x8 = 1;
+    int t8 = 0;
+    if (intra) {
+      cur.flags |= F_INTRA;
+      if (kind == 1) cur.flags |= F_I16;
+      if (kind == 0) {
+        if (t8mode) {
+          t8 = bin(SE_OTHER, 0, 399 + (left_ok && (sh->left.flags & F_T8)) + (top_ok && (ring[mb_x].flags & F_T8)));
+          if (t8) cur.flags |= F_T8;
+        }
+        const int nmodes = t8 ? 4 : 16;
+        for (int i = 0; i < nmodes; i++)
+          if (!bin(SE_OTHER, 0, 68)) {
+            bin(SE_OTHER, 0, 69);
+            bin(SE_OTHER, 0, 69);
+            bin(SE_OTHER, 0, 69);
+          }
+      }
+      if (cat_ == 1 || cat_ == 2) {
+        int ctx = (left_ok && (sh->left.flags & F_INTRA) && (sh->left.flags & F_CPRED)) +
+                  (top_ok && (ring[mb_x].flags & F_INTRA) && (ring[mb_x].flags & F_CPRED));
+        if (bin(SE_OTHER, 0, 64 + ctx)) {
+          cur.flags |= F_CPRED;
+          if (bin(SE_OTHER, 0, 67)) bin(SE_OTHER, 0, 67);
+        }
+      }
+    } else if (nparts == 4) {
+      if (direct16) {
+        cur.flags |= F_D16;
+        cur.direct8[0] = cur.direct8[1] = cur.direct8[2] = cur.direct8[3] = 1;
+        if (!d->direct_8x8_inference) no_sub_lt8x8 = 0;
+      } else {
+        uint32_t sub = 0;  // per 8x8: parts b0-2, vertical b3, pred b4-5 (no private arrays)
+        for (int i = 0; i < 4; i++) {
+          int t, sp, sv, spr;
+          if (!is_b) {
+            if (bin(SE_OTHER, 0, 21)) t = 0;
+            else if (!bin(SE_OTHER, 0, 22)) t = 1;
+            else if (bin(SE_OTHER, 0, 23)) t = 2;
+            else t = 3;
+            sp = t == 0 ? 1 : t == 3 ? 4 : 2;
+            sv = t == 2;
+            spr = 1;
+          } else {
+            if (!bin(SE_OTHER, 0, 36)) t = 0;
+            else if (!bin(SE_OTHER, 0, 37)) t = 1 + bin(SE_OTHER, 0, 39);
+            else {
+              t = 3;
+              if (bin(SE_OTHER, 0, 38)) {
+                if (bin(SE_OTHER, 0, 39)) t = 11 + bin(SE_OTHER, 0, 39);
+                else {
+                  t += 4;
+                  t += 2 * bin(SE_OTHER, 0, 39);
+                  t += bin(SE_OTHER, 0, 39);
+                }
+              } else {
+                t += 2 * bin(SE_OTHER, 0, 39);
+                t += bin(SE_OTHER, 0, 39);
+              }
+            }
+            if (t == 0) { sp = 0; sv = 0; spr = 0; }
+            else if (t <= 3) { sp = 1; sv = 0; spr = t; }
+            else if (t <= 9) { int k = t - 4; sp = 2; sv = k & 1; spr = (k >> 1) + 1; }
+            else { sp = 4; sv = 0; spr = t - 9; }
+          }
+          sub |= (uint32_t)(sp | sv << 3 | spr << 4) << (8 * i);
+          if (sp == 0) {
+            cur.direct8[i] = 1;
+            if (!d->direct_8x8_inference) no_sub_lt8x8 = 0;
+          } else if (sp > 1) {
+            no_sub_lt8x8 = 0;
+          }
+        }
+        for (int list = 0; list < nlists; list++)
+          for (int i = 0; i < 4; i++) {
+            const int sp = (sub >> (8 * i)) & 7, spr = (sub >> (8 * i + 4)) & 3;
+            if (!sp || !(spr & (1 << list))) continue;
+            int nref = list ? d->num_ref_idx_l1 : d->num_ref_idx_l0;
+            cur.ref[list][i] = (int8_t)(nref > 1 ? decode_ref(list, 2 * (i & 1), 2 * (i >> 1)) : 0);
+          }
+        for (int list = 0; list < nlists; list++)
+          for (int i = 0; i < 4; i++) {
+            const int sp = (sub >> (8 * i)) & 7, sv = (sub >> (8 * i + 3)) & 1, spr = (sub >> (8 * i + 4)) & 3;
+            if (!sp || !(spr & (1 << list))) continue;
+            const int x0 = 2 * (i & 1), y0 = 2 * (i >> 1);
+            for (int j = 0; j < sp; j++) {
+              if (sp == 1) mvd_part(list, x0, y0, 2, 2);
+              else if (sp == 4) mvd_part(list, x0 + (j & 1), y0 + (j >> 1), 1, 1);
+              else if (!sv) mvd_part(list, x0, y0 + j, 2, 1);
+              else mvd_part(list, x0 + j, y0, 1, 2);
+            }
+          }
+      }
+    } else {
+      for (int list = 0; list < nlists; list++)
+        for (int i = 0; i < nparts; i++) {
+          const int pr = i ? pred1 : pred0;
+          if (!(pr & (1 << list))) continue;
+          const int px = (nparts == 2 && vertical) ? 2 * i : 0, py = (nparts == 2 && !vertical) ? 2 * i : 0;
+          const int nref = list ? d->num_ref_idx_l1 : d->num_ref_idx_l0;
+          const int ref = nref > 1 ? decode_ref(list, px, py) : 0;
+          if (nparts == 1) cur.ref[list][0] = cur.ref[list][1] = cur.ref[list][2] = cur.ref[list][3] = (int8_t)ref;
+          else if (!vertical) cur.ref[list][2 * i] = cur.ref[list][2 * i + 1] = (int8_t)ref;
+          else cur.ref[list][i] = cur.ref[list][i + 2] = (int8_t)ref;
+        }
+      for (int list = 0; list < nlists; list++)
+        for (int i = 0; i < nparts; i++) {
+          const int pr = i ? pred1 : pred0;
+          if (!(pr & (1 << list))) continue;
+          if (nparts == 1) mvd_part(list, 0, 0, 4, 4);
+          else if (vertical) mvd_part(list, 2 * i, 0, 2, 4);
+          else mvd_part(list, 0, 2 * i, 4, 2);
+        }
+    }
+    if (err) return;
+    int cbp;
+    if (intra && kind == 1) {
+      cbp = i16_cbp;
+    } else {
+      const uint16_t ca = nb_cbp_left(), cb = nb_cbp_top();
+      int c = 0;
+      c |= bin(SE_OTHER, 0, 73 + !(ca & 0x02) + 2 * !(cb & 0x04));
+      c |= bin(SE_OTHER, 0, 73 + !(c & 0x01) + 2 * !(cb & 0x08)) << 1;
+      c |= bin(SE_OTHER, 0, 73 + !(ca & 0x08) + 2 * !(c & 0x01)) << 2;
+      c |= bin(SE_OTHER, 0, 73 + !(c & 0x04) + 2 * !(c & 0x02)) << 3;
+      if (cat_ == 1 || cat_ == 2) {
+        const int a = (ca >> 4) & 3, b = (cb >> 4) & 3;
+        if (bin(SE_OTHER, 0, 77 + (a > 0) + 2 * (b > 0)))
+          c |= (1 + bin(SE_OTHER, 0, 77 + 4 + (a == 2) + 2 * (b == 2))) << 4;
+      }
+      cbp = c;
+      if ((cbp & 15) && t8mode && !intra && no_sub_lt8x8 && (!direct16 || d->direct_8x8_inference)) {
+        if (bin(SE_OTHER, 0, 399 + (left_ok && (sh->left.flags & F_T8)) + (top_ok && (ring[mb_x].flags & F_T8))))
+          cur.flags |= F_T8;
+      }
+    }
+    cur.cbp = (uint16_t)cbp;
+    if ((cbp & 0x3f) || (intra && kind == 1)) {
+      int ctx = last_dqp_nz ? 1 : 0, val = 0;
+      while (bin(SE_QPDELTA, val, 60 + ctx)) {
+        ctx = ctx < 2 ? 2 : 3;
+        if (++val > 102) { err = -6; return; }
+      }
+      last_dqp_nz = val != 0;
+      residual(intra && kind == 1, cbp);
+    } else {
+      last_dqp_nz = 0;
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+template <int MODE, bool RM>
+AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
+  const int lane = threadIdx.x;
+  const avr_slice_desc* d = w.d;
+  // cabac contexts: 9.3.1.1
+  const int tbl = d->slice_type == 2 ? 0 : 1 + d->cabac_init_idc;
+  const int qp = d->slice_qp < 0 ? 0 : d->slice_qp > 51 ? 51 : d->slice_qp;
+  for (int i = lane; i < 1024; i += 64) {
+    int m = T->mn[tbl][i][0], n = T->mn[tbl][i][1];
+    int pre = ((m * qp) >> 4) + n;
+    pre = pre < 1 ? 1 : pre > 126 ? 126 : pre;
+    uint8_t s = pre <= 63 ? (uint8_t)((63 - pre) << 1) : (uint8_t)(((pre - 64) << 1) | 1);
+    w.sh->state[i] = s;
+    if (MODE == MODE_GENERATE) {
+      // P(bin = 1) of the initial state: p_LPS = 0.5 * alpha^pStateIdx
+      uint32_t plps = T->gen_plps[s >> 1];
+      w.sh->gen_p[i] = (uint16_t)((s & 1) ? 65536 - plps : plps);
+    }
+  }
+  if (!RM) {
+    for (int i = lane; i < kEstDefault + 2; i += 64) w.sh->est[i] = 0;
+  }
+  uint32_t* ring32 = (uint32_t*)w.ring;
+  for (int i = lane; i < w.W * (int)sizeof(EdgeRec) / 4; i += 64) ring32[i] = 0;
+  __syncthreads();
+}
+
+template <int MODE, bool RM>
+AVR_FI void walk_slice(Walker<MODE, RM>& w) {
+  const avr_slice_desc* d = w.d;
+  w.W = d->mb_width;
+  w.H = d->mb_height;
+  w.slice_type = d->slice_type;
+  w.is_b = d->slice_type == 1;
+  w.cat_ = d->chroma_array_type;
+  w.t8mode = d->transform_8x8_mode;
+  w.last_dqp_nz = 0;
+  w.err = 0;
+  w.finished = 0;
+  w.bins = 0;
+  w.mbs_done = 0;
+  int addr = d->first_mb;
+  const int lane = threadIdx.x;
+  for (;;) {
+    if (addr >= w.W * w.H) { w.err = -7; break; }
+    w.mb_x = addr % w.W;
+    w.mb_y = addr / w.W;
+    w.left_ok = w.mb_x > 0 && addr - 1 >= d->first_mb;
+    w.top_ok = (w.ring[w.mb_x].flags & F_DEC) != 0;
+    // clear the current record (64 lanes)
+    {
+      uint32_t* c32 = (uint32_t*)&w.sh->cur;
+      for (int i = lane; i < (int)sizeof(MbRec) / 4; i += 64) c32[i] = 0;
+      __syncthreads();
+      for (int i = lane; i < 8; i += 64) ((int8_t*)w.sh->cur.ref)[i] = -1;
+      __syncthreads();
+    }
+    w.decode_mb();
+    if (w.err) break;
+    w.sh->cur.flags |= F_DEC;
+    w.mbs_done++;
+    w.last_mb = addr + 1 >= w.W * w.H;
+    // publish: bottom edge to the ring, full record to `left`, model bytes to the frame (RM)
+    __syncthreads();
+    {
+      const MbRec& c = w.sh->cur;
+      EdgeRec& e = w.ring[w.mb_x];
+      const int ph_c = w.cat_ == 2 ? 4 : w.cat_ == 3 ? 4 : 2;
+      if (lane < 52) e.mnnz[lane] = c.mnnz[lane];
+      if (lane < 12) {
+        int p = lane / 4, x = lane % 4;
+        int ph = p == 0 ? 4 : ph_c;
+        e.nnz[p][x] = c.nnz[p][(ph - 1) * 4 + x];
+      }
+      if (lane < 16) {
+        int l = lane / 8, x = (lane / 2) % 4, comp = lane % 2;
+        e.mvd[l][x][comp] = c.mvd[l][12 + x][comp];
+      }
+      if (lane < 4) e.ref[lane / 2][lane % 2] = c.ref[lane / 2][2 + lane % 2];
+      if (lane < 2) e.direct8[lane] = c.direct8[2 + lane];
+      if (lane == 0) {
+        e.flags = c.flags;
+        e.cbp = c.cbp;
+      }
+      if (RM) {
+        uint8_t* f = w.frames + (size_t)w.cur_frame * w.W * w.H * 52 + ((size_t)w.mb_y * w.W + w.mb_x) * 52;
+        if (lane < 52) f[lane] = c.mnnz[lane];
+      }
+      __syncthreads();
+      uint32_t* l32 = (uint32_t*)&w.sh->left;
+      const uint32_t* c32 = (const uint32_t*)&w.sh->cur;
+      for (int i = lane; i < (int)sizeof(MbRec) / 4; i += 64) l32[i] = c32[i];
+      __syncthreads();
+    }
+    if (w.terminate(SE_EOS)) break;
+    if (MODE == MODE_COMPRESS && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
+    addr++;
+  }
+}
+
+// --------------------------------------------------------------------------- kernel bodies
+template <int MODE, bool RM>
+AVR_FI void run_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
+                          avr_slice_result* res) {
+  const int lane = threadIdx.x;
+  w.d = d;
+  w.in.g = in + d->payload_offset;
+  w.in.limit = MODE == MODE_GENERATE ? 0 : d->read_limit;
+  w.in.lds = w.sh->in_stage;
+  w.in.win = 0xffffffffu - kStage;  // force a fill on first use
+  w.out.g = out + d->out_offset;
+  w.out.cap = d->out_capacity;
+  w.out.flushed = 0;
+  w.out.fill = 0;
+  w.out.lds = w.sh->out_stage;
+  w.out.overflow = 0;
+  w.out.last = 0;
+  if (MODE == MODE_COMPRESS) {
+    cd_init(w.cd, w.in);
+    re_init(w.re);
+  } else if (MODE == MODE_DECOMPRESS) {
+    rd_init(w.rd, w.in);
+    ce_init(w.ce);
+  } else {
+    ce_init(w.ce);
+    w.rng = d->payload_offset * 0x9E3779B97F4A7C15ull + 0x1234567ull + (uint64_t)d->picture_id;
+    w.target_mbs = d->payload_size ? (int)d->payload_size : 1 << 30;
+  }
+  walk_slice(w);
+  int status = w.err;
+  if (!status && !w.finished) status = -9;
+  if (MODE == MODE_COMPRESS) {
+    if (w.re.err) status = -10;
+    if (!status) {
+      // predicted decompressor output (recode.cpp:1345-1356, 1503-1505): the regenerated CABAC
+      // bytes equal the payload through the stop bit, then zero bits
+      const uint32_t sbi = cd_bitpos(w.cd) - 1;
+      const uint32_t k = sbi >> 3, size = d->payload_size;
+      const uint32_t b = in_byte(w.in, k);
+      const uint32_t masked = b & (0xffu << (7 - (sbi & 7))) & 0xff;
+      int ok;
+      if (masked == 0x80) ok = (k == size) || (k + 1 == size);
+      else ok = (k + 1 == size) || (k + 2 == size && b == masked);
+      if (!ok) status = -11;
+    }
+  } else if (MODE == MODE_DECOMPRESS || MODE == MODE_GENERATE) {
+    if (w.ce.err) status = -10;
+  }
+  out_flush(w.out);
+  if (w.out.overflow) status = -12;
+  uint32_t len = out_total(w.out);
+  if (MODE == MODE_DECOMPRESS && !status && len && w.out.last == 0x80) len--;  // recode.cpp:1503-1505
+  if (lane == 0) {
+    res->out_len = len;
+    res->status = status;
+    res->bins = w.bins;
+    res->mbs = (uint32_t)w.mbs_done;
+  }
+}
+
+// Copy the per-bin lookup tables into this workgroup's LDS (16 B per lane per step).
+AVR_FI void load_hot_tables(Shared* sh, const EngineTables* G) {
+  const uint4* src = (const uint4*)&G->hot;
+  uint4* dst = (uint4*)&sh->tab;
+  for (int i = threadIdx.x; i < (int)(sizeof(HotTables) / 16); i += 64) dst[i] = src[i];
+  __syncthreads();
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+                                                               const uint8_t* in, uint8_t* out, avr_slice_result* res,
+                                                               uint16_t* est_scratch) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const int s = blockIdx.x;
+  if (s >= n) return;
+  const avr_slice_desc* d = &descs[s];
+  Walker<MODE, false> w;
+  w.sh = (Shared*)smem;
+  w.ring = (EdgeRec*)(smem + sizeof(Shared));
+  load_hot_tables(w.sh, G);
+  w.T = &w.sh->tab;
+  w.G = G;
+  w.frames = nullptr;
+  w.cur_frame = 0;
+  w.est_g = est_scratch + (size_t)s * kEstGlobal;
+  if (!d->coded) {
+    if (threadIdx.x == 0) {
+      res[s].out_len = 0;
+      res[s].status = 1;
+      res[s].bins = 0;
+      res[s].mbs = 0;
+    }
+    return;
+  }
+  // fresh model for this slice: clear the dense SIG/NZ estimators (16 B per lane per step)
+  if (MODE != MODE_GENERATE) {
+    uint4* e4 = (uint4*)w.est_g;
+    for (int i = threadIdx.x; i < kEstGlobal / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
+  }
+  w.d = d;
+  w.W = d->mb_width;
+  init_slice_state(w, G);
+  run_slice(w, d, in, out, &res[s]);
+}
+
+// Reference model: one wavefront walks every slice in file order with persistent state.
+template <int MODE>
+__global__ __launch_bounds__(64) void slices_sequential_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+                                                                 const uint8_t* in, uint8_t* out,
+                                                                 avr_slice_result* res, uint16_t* est_g,
+                                                                 uint8_t* frames, int* frame_meta) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const int lane = threadIdx.x;
+  Walker<MODE, true> w;
+  w.sh = (Shared*)smem;
+  w.ring = (EdgeRec*)(smem + sizeof(Shared));
+  load_hot_tables(w.sh, G);
+  w.T = &w.sh->tab;
+  w.G = G;
+  w.est_g = est_g;
+  w.frames = frames;
+  // fresh global model
+  {
+    uint4* e4 = (uint4*)est_g;
+    for (int i = lane; i < kEstGlobal / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
+    for (int i = lane; i < kEstDefault + 2; i += 64) w.sh->est[i] = 0;
+  }
+  // frame_meta: [0] cur_frame.  Frame ids / sizes of the two frames, as scalars (no private arrays).
+  int cur = 0, fid0 = 0, fid1 = 0, fw0 = 0, fw1 = 0, fh0 = 0, fh1 = 0;
+  __syncthreads();
+  for (int s = 0; s < n; s++) {
+    const avr_slice_desc* d = &descs[s];
+    const int W = d->mb_width, H = d->mb_height;
+    // update_frame_spec (recode.cpp:824-843)
+    const int fwc = cur ? fw1 : fw0, fhc = cur ? fh1 : fh0, fidc = cur ? fid1 : fid0;
+    if (fwc != W || fhc != H || !(fidc == d->picture_id && fwc && fhc)) {
+      cur = 1 - cur;
+      const int fwn = cur ? fw1 : fw0, fhn = cur ? fh1 : fh0;   // the new current frame
+      const int fwo = cur ? fw0 : fw1, fho = cur ? fh0 : fh1;   // the other one
+      const bool reinit_other = (fwn != W || fhn != H) && (fwo != W || fho != H);
+      // fresh/cleared current frame; a dimension change also clears the other one
+      uint32_t* f32 = (uint32_t*)(frames + (size_t)cur * W * H * 52);
+      for (int i = lane; i < W * H * 13; i += 64) f32[i] = 0;
+      if (reinit_other) {
+        uint32_t* o32 = (uint32_t*)(frames + (size_t)(1 - cur) * W * H * 52);
+        for (int i = lane; i < W * H * 13; i += 64) o32[i] = 0;
+        if (cur) { fw0 = W; fh0 = H; } else { fw1 = W; fh1 = H; }
+      }
+      if (cur) { fw1 = W; fh1 = H; fid1 = d->picture_id; } else { fw0 = W; fh0 = H; fid0 = d->picture_id; }
+      __syncthreads();
+    }
+    if (!d->coded) {
+      if (lane == 0) {
+        res[s].out_len = 0;
+        res[s].status = 1;
+        res[s].bins = 0;
+        res[s].mbs = 0;
+      }
+      continue;
+    }
+    w.cur_frame = cur;
+    w.d = d;
+    w.W = W;
+    init_slice_state(w, G);
+    run_slice(w, d, in, out, &res[s]);
+    __syncthreads();
+  }
+  if (lane == 0) frame_meta[0] = cur;
+}
+
+}  // namespace avr
