@@ -39,6 +39,10 @@ struct EngineTables {
 };
 
 // ------------------------------------------------------------------------- byte staging (LDS)
+// The refill / flush paths run once per kStage bytes.  They are real calls (__noinline__), so
+// their code exists once in the kernel instead of at every bin site: with everything inlined
+// the compress kernel was 1 MB of code and instruction fetch dominated.  They take and return
+// plain values, never a pointer to the caller's walker, so the caller's state stays in registers.
 struct InStream {
   const uint8_t* g;     // global base (payload start)
   uint32_t limit;       // readable bytes; beyond -> 0
@@ -46,54 +50,57 @@ struct InStream {
   uint8_t* lds;         // kStage bytes
 };
 
-__device__ __forceinline__ void in_fill(InStream& s, uint32_t at) {
+// Load the window [at, at + kStage) into LDS, bytes at or past `limit` as 0.  Returns `at`.
+__device__ __noinline__ uint32_t in_fill_call(uint8_t* lds, const uint8_t* g, uint32_t limit, uint32_t at) {
   __syncthreads();
   const int lane = threadIdx.x;
-  s.win = at;
   const uint32_t base = at + 16u * lane;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     uint32_t i = base + k;
-    s.lds[16 * lane + k] = i < s.limit ? s.g[i] : 0;
+    lds[16 * lane + k] = i < limit ? g[i] : 0;
   }
   __syncthreads();
+  return at;
 }
+// byte i of the stream (0 at or past limit: the window is zero-filled there)
 __device__ __forceinline__ uint32_t in_byte(InStream& s, uint32_t i) {
-  if (i >= s.limit) return 0;
-  if (i - s.win >= (uint32_t)kStage) in_fill(s, i);
+  if (i - s.win >= (uint32_t)kStage) s.win = in_fill_call(s.lds, s.g, s.limit, i);
   return s.lds[i - s.win];
 }
+// big-endian 32 bits at i..i+3 with a single window check
+__device__ __forceinline__ uint32_t in_be32(InStream& s, uint32_t i) {
+  if (i - s.win > (uint32_t)kStage - 4) s.win = in_fill_call(s.lds, s.g, s.limit, i);
+  const uint8_t* p = s.lds + (i - s.win);
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
 
+// Output bytes go straight to global memory from lane 0 (fire-and-forget stores: nothing in
+// the serial chain waits on them, and no staging buffer needs a flush path at every bin site).
 struct OutStream {
   uint8_t* g;          // global base (slice output region)
   uint32_t cap;        // capacity
-  uint32_t flushed;    // bytes already written to g
-  uint32_t fill;       // bytes in the LDS window
-  uint8_t* lds;
-  int overflow;
+  uint32_t n;          // bytes emitted (written while n < cap)
   uint32_t last;       // last byte emitted
 };
-__device__ __forceinline__ void out_flush(OutStream& o) {
-  __syncthreads();
-  const int lane = threadIdx.x;
-  for (uint32_t k = 0; k < 16; k++) {
-    uint32_t j = 16u * lane + k;
-    if (j < o.fill) {
-      uint32_t d = o.flushed + j;
-      if (d < o.cap) o.g[d] = o.lds[j];
-    }
-  }
-  o.flushed += o.fill;
-  if (o.flushed > o.cap) o.overflow = 1;
-  o.fill = 0;
-  __syncthreads();
-}
 __device__ __forceinline__ void out_byte(OutStream& o, uint32_t v) {
-  if (o.fill == kStage) out_flush(o);
-  o.lds[o.fill++] = (uint8_t)v;
+  if (o.n < o.cap && threadIdx.x == 0) o.g[o.n] = (uint8_t)v;
+  o.n++;
   o.last = v & 0xff;
 }
-__device__ __forceinline__ uint32_t out_total(const OutStream& o) { return o.flushed + o.fill; }
+// k copies of byte v at g[n..n+k) (the deferred 0xFF runs of the carry handling).  Rare: a real
+// call, so the loop exists once (inlined, the compiler unrolls it at every bin site).
+__device__ __noinline__ void out_run_call(uint8_t* g, uint32_t cap, uint32_t n, uint32_t v, uint32_t k) {
+  for (uint32_t i = threadIdx.x; i < k; i += 64)
+    if (n + i < cap) g[n + i] = (uint8_t)v;
+}
+__device__ __forceinline__ void out_repeat(OutStream& o, uint32_t v, uint32_t k) {
+  out_run_call(o.g, o.cap, o.n, v, k);
+  o.n += k;
+  if (k) o.last = v & 0xff;
+}
+__device__ __forceinline__ uint32_t out_total(const OutStream& o) { return o.n; }
+__device__ __forceinline__ bool out_overflow(const OutStream& o) { return o.n > o.cap; }
 
 // ---------------------------------------------------------------------- CABAC decoding engine
 struct CabacDecoder {
@@ -104,8 +111,7 @@ struct CabacDecoder {
 };
 
 __device__ __forceinline__ void cd_refill(CabacDecoder& d, InStream& in) {
-  uint32_t w = (in_byte(in, d.next) << 24) | (in_byte(in, d.next + 1) << 16) | (in_byte(in, d.next + 2) << 8) |
-               in_byte(in, d.next + 3);
+  uint32_t w = in_be32(in, d.next);
   d.next += 4;
   d.value = (d.value << 32) | w;
   d.avail += 32;
@@ -186,6 +192,7 @@ __device__ __forceinline__ void ce_init(CabacEncoder& e) {
   e.err = 0;
 }
 __device__ __forceinline__ void ce_putbyte(CabacEncoder& e, OutStream& o) {
+  #pragma clang loop unroll(disable)
   while (e.queue >= 0) {
     uint32_t out = (uint32_t)(e.low >> (e.queue + 10));
     e.low &= (0x400ull << e.queue) - 1;
@@ -200,7 +207,8 @@ __device__ __forceinline__ void ce_putbyte(CabacEncoder& e, OutStream& o) {
       } else if (carry) {
         e.err = 1;
       }
-      for (; e.outstanding; e.outstanding--) out_byte(o, (0xff + carry) & 0xff);
+      if (e.outstanding) out_repeat(o, (0xff + carry) & 0xff, e.outstanding);
+      e.outstanding = 0;
       e.cache = byte;
       e.have_cache = 1;
     }
@@ -248,7 +256,8 @@ __device__ __forceinline__ void ce_terminate(CabacEncoder& e, OutStream& o, int 
   e.queue += pad;
   ce_putbyte(e, o);
   if (e.have_cache) out_byte(o, e.cache);
-  for (; e.outstanding; e.outstanding--) out_byte(o, 0xff);
+  if (e.outstanding) out_repeat(o, 0xff, e.outstanding);
+  e.outstanding = 0;
   e.have_cache = 0;
 }
 
@@ -297,7 +306,8 @@ __device__ __forceinline__ void re_shift(RecodedEncoder& e, OutStream& o) {
     } else if (carry) {
       e.err = 1;
     }
-    for (; e.pending; e.pending--) out_byte(o, (0xff + carry) & 0xff);
+    if (e.pending) out_repeat(o, (0xff + carry) & 0xff, e.pending);
+    e.pending = 0;
     e.cache = digit;
     e.have_cache = 1;
   } else {
@@ -314,6 +324,7 @@ __device__ __forceinline__ void re_put(RecodedEncoder& e, OutStream& o, int bin,
   }
   if (e.range < (1ull << 51)) {  // min_range = (fixed_one/digit_base)/16
     if (e.range == 0) e.err = 1;
+    #pragma clang loop unroll(disable)
     while (e.range < (1ull << 55)) {
       re_shift(e, o);
       e.range <<= 8;
@@ -321,6 +332,7 @@ __device__ __forceinline__ void re_put(RecodedEncoder& e, OutStream& o, int bin,
   }
 }
 __device__ __forceinline__ void re_finish(RecodedEncoder& e, OutStream& o) {  // arith:128-144
+  #pragma clang loop unroll(disable)
   for (uint64_t sb = 1ull << 62; sb; sb >>= 1) {
     uint64_t x = (e.low | sb) & ~(sb - 1);
     if (sb < e.range && e.low <= x && x < e.low + e.range) {
@@ -328,9 +340,11 @@ __device__ __forceinline__ void re_finish(RecodedEncoder& e, OutStream& o) {  //
       break;
     }
   }
+  #pragma clang loop unroll(disable)
   while (e.low != 0) re_shift(e, o);
   if (e.have_cache) out_byte(o, e.cache);
-  for (; e.pending; e.pending--) out_byte(o, 0xff);
+  if (e.pending) out_repeat(o, 0xff, e.pending);
+  e.pending = 0;
   e.have_cache = 0;
 }
 
@@ -351,6 +365,7 @@ __device__ __forceinline__ void rd_init(RecodedDecoder& d, InStream& in) {  // a
   d.next_digit = in_byte(in, d.next++);
   d.low = d.next_digit >> 1;
   d.range = 128;
+  #pragma clang loop unroll(disable)
   while (d.range < (1ull << 63)) rd_consume(d, in);
 }
 __device__ __forceinline__ int rd_get(RecodedDecoder& d, InStream& in, uint64_t r1) {
@@ -363,6 +378,7 @@ __device__ __forceinline__ int rd_get(RecodedDecoder& d, InStream& in, uint64_t 
     d.range = r0;
   }
   if (d.range < (1ull << 51))
+    #pragma clang loop unroll(disable)
     while (d.range < (1ull << 55)) rd_consume(d, in);
   return bin;
 }

@@ -82,15 +82,24 @@ struct EdgeRec {        // bottom edge of the macroblock above
 static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
 
 // LDS layout (per workgroup = one wavefront); the ring is sized by mb_width at launch.
+// LDS cache of the dense SIG + NZ estimator table (kEstGlobal u16 entries in HBM per model):
+// direct mapped, entry = (tag + 1) << 16 | estimator, 0 = empty; write-back on eviction.  The
+// significance-map bins (a third or more of all bins) then cost an LDS access, not an HBM round
+// trip.
+constexpr int kEcacheBits = 12;
+constexpr int kEcacheSize = 1 << kEcacheBits;
+
 struct Shared {
   HotTables tab;          // copy of EngineTables::hot (per-bin lookups stay in LDS)
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
   uint8_t state[1024];
   uint16_t est[kEstDefault + 2];
   uint8_t in_stage[kStage];
-  uint8_t out_stage[kStage];
   MbRec cur, left;
-  uint16_t gen_p[1024];   // generator: P(bin = 1) in 1/65536 per context
+  union {
+    uint32_t ecache[kEcacheSize];  // compress/decompress: LDS cache of the SIG + NZ estimators
+    uint16_t gen_p[1024];          // generator: P(bin = 1) in 1/65536 per context
+  };
 };
 
 template <int MODE, bool RM>
@@ -117,6 +126,7 @@ struct Walker {
   int err, finished;
   uint32_t bins;
   int target_mbs, mbs_done, last_mb;
+  int nref0, nref1, d8x8inf, x264_build, first_mb;
 
   // ------------------------------------------------------------------ bins through the model
   AVR_FI int bin(int se, int k, int ctx) {
@@ -210,7 +220,7 @@ struct Walker {
   // FFmpeg 4:4:4 8x8 coded_block_flag quirk for x264 < r151 (see oracle_walker.c)
   AVR_FI int nnz_override(uint8_t nbflags, int* v) const {
     if (cat_ != 3 || !(sh->cur.flags & F_T8) || (nbflags & F_T8)) return 0;
-    *v = (uint32_t)d->x264_build < 151u ? ((sh->cur.flags & F_INTRA) ? 64 : 0) : 0;
+    *v = (uint32_t)x264_build < 151u ? ((sh->cur.flags & F_INTRA) ? 64 : 0) : 0;
     return 1;
   }
   AVR_FI int nnz_left(int p, int pw, int x4, int y4) const {
@@ -243,6 +253,25 @@ struct Walker {
     return 0;
   }
 
+  // ------------------------------------------------------------------ SIG / NZ estimators
+  AVR_FI static uint32_t ec_hash(uint32_t tag) { return (tag * 0x9E3779B1u) >> (32 - kEcacheBits); }
+  AVR_FI uint32_t est_load(int idx, uint32_t* slot) {
+    const uint32_t tag = (uint32_t)idx >> kEcacheBits;
+    const uint32_t set = ((uint32_t)idx ^ ec_hash(tag)) & (kEcacheSize - 1);
+    *slot = set;
+    const uint32_t ent = sh->ecache[set];
+    if ((ent >> 16) == tag + 1) return ent & 0xffff;
+    if (ent) {  // evict: write the old estimator back
+      const uint32_t otag = (ent >> 16) - 1;
+      const uint32_t oidx = otag << kEcacheBits | ((set ^ ec_hash(otag)) & (kEcacheSize - 1));
+      if (threadIdx.x == 0) est_g[oidx] = (uint16_t)ent;
+    }
+    return est_g[idx];
+  }
+  AVR_FI void est_store(int idx, uint32_t slot, uint32_t e) {
+    sh->ecache[slot] = (((uint32_t)idx >> kEcacheBits) + 1) << 16 | e;
+  }
+
   // finished_queueing (recode.cpp:845-930): the 2/4/6 nnz bits, LSB first
   AVR_FI int nz_bits(int cat, int n, int max, int is_dc, int c422, int count) {
     const int bits = max > 16 ? 6 : max > 4 ? 4 : 2;
@@ -270,7 +299,8 @@ struct Walker {
       const int ab = av ? (av >= cur_bit) : 2;
       const int pb = pv >= cur_bit;
       const int idx = kSigEst + (((((cur_bit - 1 + so_far) * 2 + pb) * 3 + lb) * 3 + ab) * 57 + t);
-      uint32_t e = est_g[idx];
+      uint32_t slot;
+      uint32_t e = est_load(idx, &slot);
       int b;
       if (MODE == MODE_COMPRESS) {
         b = (count >> i) & 1;
@@ -278,7 +308,7 @@ struct Walker {
       } else {
         b = rd_get(rd, in, rc_p1(rd.range, e, T));
       }
-      est_g[idx] = (uint16_t)est_update(e, b, 0x60);
+      est_store(idx, slot, est_update(e, b, 0x60));
       if (b) so_far |= cur_bit;
     }
     return so_far;
@@ -321,9 +351,10 @@ struct Walker {
       for (int zz = 0; zz <= end; zz++) {
         int b = (int)((sigmask >> zz) & 1);
         int idx = sig_est_index(cat, max, is_dc, c422, zz, nnz_m, obs);
-        uint32_t e = est_g[idx];
+        uint32_t slot;
+        uint32_t e = est_load(idx, &slot);
         re_put(re, out, b, rc_p1(re.range, e, T));
-        est_g[idx] = (uint16_t)est_update(e, b, 0x50);
+        est_store(idx, slot, est_update(e, b, 0x50));
         obs += b;
       }
     } else if (MODE == MODE_DECOMPRESS) {
@@ -335,9 +366,10 @@ struct Walker {
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
         int idx = sig_est_index(cat, max, is_dc, c422, pos, nnz_m, cnt);
-        uint32_t e = est_g[idx];
+        uint32_t slot;
+        uint32_t e = est_load(idx, &slot);
         int b = rd_get(rd, in, rc_p1(rd.range, e, T));
-        est_g[idx] = (uint16_t)est_update(e, b, 0x50);
+        est_store(idx, slot, est_update(e, b, 0x50));
         bins++;
         ce_decision(ce, out, b, &sh->state[sb + sc], T);
         if (b) {
@@ -523,7 +555,7 @@ struct Walker {
   AVR_FI int decode_ref(int list, int x4, int y4) {
     int ctx = ref_gt0(list, x4, y4, 1) + 2 * ref_gt0(list, x4, y4, 0);
     int ref = 0;
-    avr_limit = (list ? d->num_ref_idx_l1 : d->num_ref_idx_l0) - 1;
+    avr_limit = (list ? nref1 : nref0) - 1;
     while (bin(SE_REF, ref, 54 + ctx)) {
       ref++;
       ctx = (ctx >> 2) + 4;
@@ -691,7 +723,7 @@ struct Walker {
       if (direct16) {
         cur.flags |= F_D16;
         cur.direct8[0] = cur.direct8[1] = cur.direct8[2] = cur.direct8[3] = 1;
-        if (!d->direct_8x8_inference) no_sub_lt8x8 = 0;
+        if (!d8x8inf) no_sub_lt8x8 = 0;
       } else {
         uint32_t sub = 0;  // per 8x8: parts b0-2, vertical b3, pred b4-5 (no private arrays)
         for (int i = 0; i < 4; i++) {
@@ -729,7 +761,7 @@ struct Walker {
           sub |= (uint32_t)(sp | sv << 3 | spr << 4) << (8 * i);
           if (sp == 0) {
             cur.direct8[i] = 1;
-            if (!d->direct_8x8_inference) no_sub_lt8x8 = 0;
+            if (!d8x8inf) no_sub_lt8x8 = 0;
           } else if (sp > 1) {
             no_sub_lt8x8 = 0;
           }
@@ -738,7 +770,7 @@ struct Walker {
           for (int i = 0; i < 4; i++) {
             const int sp = (sub >> (8 * i)) & 7, spr = (sub >> (8 * i + 4)) & 3;
             if (!sp || !(spr & (1 << list))) continue;
-            int nref = list ? d->num_ref_idx_l1 : d->num_ref_idx_l0;
+            int nref = list ? nref1 : nref0;
             cur.ref[list][i] = (int8_t)(nref > 1 ? decode_ref(list, 2 * (i & 1), 2 * (i >> 1)) : 0);
           }
         for (int list = 0; list < nlists; list++)
@@ -760,7 +792,7 @@ struct Walker {
           const int pr = i ? pred1 : pred0;
           if (!(pr & (1 << list))) continue;
           const int px = (nparts == 2 && vertical) ? 2 * i : 0, py = (nparts == 2 && !vertical) ? 2 * i : 0;
-          const int nref = list ? d->num_ref_idx_l1 : d->num_ref_idx_l0;
+          const int nref = list ? nref1 : nref0;
           const int ref = nref > 1 ? decode_ref(list, px, py) : 0;
           if (nparts == 1) cur.ref[list][0] = cur.ref[list][1] = cur.ref[list][2] = cur.ref[list][3] = (int8_t)ref;
           else if (!vertical) cur.ref[list][2 * i] = cur.ref[list][2 * i + 1] = (int8_t)ref;
@@ -792,7 +824,7 @@ struct Walker {
           c |= (1 + bin(SE_OTHER, 0, 77 + 4 + (a == 2) + 2 * (b == 2))) << 4;
       }
       cbp = c;
-      if ((cbp & 15) && t8mode && !intra && no_sub_lt8x8 && (!direct16 || d->direct_8x8_inference)) {
+      if ((cbp & 15) && t8mode && !intra && no_sub_lt8x8 && (!direct16 || d8x8inf)) {
         if (bin(SE_OTHER, 0, 399 + (left_ok && (sh->left.flags & F_T8)) + (top_ok && (ring[mb_x].flags & F_T8))))
           cur.flags |= F_T8;
       }
@@ -834,6 +866,8 @@ AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
   }
   if (!RM) {
     for (int i = lane; i < kEstDefault + 2; i += 64) w.sh->est[i] = 0;
+    if (MODE != MODE_GENERATE)
+      for (int i = lane; i < kEcacheSize; i += 64) w.sh->ecache[i] = 0;
   }
   uint32_t* ring32 = (uint32_t*)w.ring;
   for (int i = lane; i < w.W * (int)sizeof(EdgeRec) / 4; i += 64) ring32[i] = 0;
@@ -849,6 +883,11 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
   w.is_b = d->slice_type == 1;
   w.cat_ = d->chroma_array_type;
   w.t8mode = d->transform_8x8_mode;
+  w.nref0 = d->num_ref_idx_l0;   // descriptor fields used while parsing: kept in registers
+  w.nref1 = d->num_ref_idx_l1;
+  w.d8x8inf = d->direct_8x8_inference;
+  w.x264_build = d->x264_build;
+  w.first_mb = d->first_mb;
   w.last_dqp_nz = 0;
   w.err = 0;
   w.finished = 0;
@@ -860,7 +899,7 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
     if (addr >= w.W * w.H) { w.err = -7; break; }
     w.mb_x = addr % w.W;
     w.mb_y = addr / w.W;
-    w.left_ok = w.mb_x > 0 && addr - 1 >= d->first_mb;
+    w.left_ok = w.mb_x > 0 && addr - 1 >= w.first_mb;
     w.top_ok = (w.ring[w.mb_x].flags & F_DEC) != 0;
     // clear the current record (64 lanes)
     {
@@ -925,10 +964,7 @@ AVR_FI void run_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_
   w.in.win = 0xffffffffu - kStage;  // force a fill on first use
   w.out.g = out + d->out_offset;
   w.out.cap = d->out_capacity;
-  w.out.flushed = 0;
-  w.out.fill = 0;
-  w.out.lds = w.sh->out_stage;
-  w.out.overflow = 0;
+  w.out.n = 0;
   w.out.last = 0;
   if (MODE == MODE_COMPRESS) {
     cd_init(w.cd, w.in);
@@ -961,8 +997,7 @@ AVR_FI void run_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_
   } else if (MODE == MODE_DECOMPRESS || MODE == MODE_GENERATE) {
     if (w.ce.err) status = -10;
   }
-  out_flush(w.out);
-  if (w.out.overflow) status = -12;
+  if (out_overflow(w.out)) status = -12;
   uint32_t len = out_total(w.out);
   if (MODE == MODE_DECOMPRESS && !status && len && w.out.last == 0x80) len--;  // recode.cpp:1503-1505
   if (lane == 0) {
@@ -1039,6 +1074,7 @@ __global__ __launch_bounds__(64) void slices_sequential_kernel(const EngineTable
     uint4* e4 = (uint4*)est_g;
     for (int i = lane; i < kEstGlobal / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
     for (int i = lane; i < kEstDefault + 2; i += 64) w.sh->est[i] = 0;
+    for (int i = lane; i < kEcacheSize; i += 64) w.sh->ecache[i] = 0;
   }
   // frame_meta: [0] cur_frame.  Frame ids / sizes of the two frames, as scalars (no private arrays).
   int cur = 0, fid0 = 0, fid1 = 0, fw0 = 0, fw1 = 0, fh0 = 0, fh1 = 0;
