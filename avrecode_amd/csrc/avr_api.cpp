@@ -81,14 +81,24 @@ int fail(avr_ctx* c, int code, const std::string& msg) {
 // coder's (range/(pos+neg)) and the model's neighbour geometry.
 void build_tables(avr::EngineTables* t) {
   memset(t, 0, sizeof(*t));
+  // FFmpeg-layout LPS range [q*128 + state] and transitions ([128+s] MPS, [127-s] LPS), state =
+  // 2*pStateIdx + valMPS; packed per state into one 64-bit record (HotTables::cabac)
+  uint8_t lps[512], mlps[256];
   for (int q = 0; q < 4; q++)
-    for (int i = 0; i < 64; i++) t->hot.lps[q * 128 + 2 * i] = t->hot.lps[q * 128 + 2 * i + 1] = avr::kRangeTabLPS[i][q];
+    for (int i = 0; i < 64; i++) lps[q * 128 + 2 * i] = lps[q * 128 + 2 * i + 1] = avr::kRangeTabLPS[i][q];
   for (int i = 0; i < 64; i++) {
     int mps = i < 62 ? i + 1 : i;
-    t->hot.mlps[128 + 2 * i] = (uint8_t)(2 * mps);
-    t->hot.mlps[128 + 2 * i + 1] = (uint8_t)(2 * mps + 1);
-    t->hot.mlps[127 - 2 * i] = (uint8_t)(i == 0 ? 1 : 2 * avr::kTransIdxLPS[i]);
-    t->hot.mlps[127 - (2 * i + 1)] = (uint8_t)(i == 0 ? 0 : 2 * avr::kTransIdxLPS[i] + 1);
+    mlps[128 + 2 * i] = (uint8_t)(2 * mps);
+    mlps[128 + 2 * i + 1] = (uint8_t)(2 * mps + 1);
+    mlps[127 - 2 * i] = (uint8_t)(i == 0 ? 1 : 2 * avr::kTransIdxLPS[i]);
+    mlps[127 - (2 * i + 1)] = (uint8_t)(i == 0 ? 0 : 2 * avr::kTransIdxLPS[i] + 1);
+  }
+  for (int st = 0; st < 128; st++) {
+    uint64_t r = 0;
+    for (int q = 0; q < 4; q++) r |= (uint64_t)lps[q * 128 + st] << (8 * q);
+    r |= (uint64_t)mlps[128 + st] << 32;
+    r |= (uint64_t)mlps[127 - st] << 40;
+    t->hot.cabac[st] = r;
   }
   for (int tbl = 0; tbl < 4; tbl++)
     for (int c = 0; c < 1024; c++) {
@@ -101,9 +111,8 @@ void build_tables(avr::EngineTables* t) {
     int l = 0;
     while ((1u << l) < d) l++;
     unsigned __int128 num = (unsigned __int128)1 << (63 + l);
-    t->hot.div_m[d] = (uint64_t)((num + d - 1) / d);
-    t->hot.div_s[d] = (uint8_t)(l - 1);
-    t->hot.div_top[d] = (1ull << 63) / d;
+    t->hot.div[d][0] = (uint64_t)((num + d - 1) / d);
+    t->hot.div[d][1] = (uint64_t)(l - 1);
   }
   // reverse_scan_8 neighbours (recode.cpp:279-312, 444-447)
   static const uint8_t scan8[48] = {
@@ -130,6 +139,31 @@ void build_tables(avr::EngineTables* t) {
     int u = cell_block((s >> 3) - 1, s & 7, &cr);
     t->hot.nb_up[n] = (uint8_t)(u | (cr ? 128 : 0));
   }
+  // ctxIdx bases per ctxBlockCat (9.3.3.1.1.9, frame coded) and the 8x8 ctxIdxInc maps
+  static const int16_t cbf[14] = {85, 89, 93, 97, 101, 1012, 460, 464, 468, 1016, 472, 476, 480, 1020};
+  static const int16_t sig[14] = {105, 120, 134, 149, 152, 402, 484, 499, 513, 660, 528, 543, 557, 718};
+  static const int16_t last[14] = {166, 181, 195, 210, 213, 417, 572, 587, 601, 690, 616, 631, 645, 748};
+  static const int16_t abs_[14] = {227, 237, 247, 257, 266, 426, 952, 962, 972, 708, 982, 992, 1002, 766};
+  // dense SIG estimator base per ctxBlockCat: 4096 per 4x4-class cat, 61440 for 8x8 cats (5, 9, 13)
+  static const int32_t seb[14] = {0, 4096, 8192, 12288, 16384, 20480, 81920, 86016, 90112,
+                                  94208, 155648, 159744, 163840, 167936};
+  static const uint8_t sig8[63] = {
+    0, 1, 2, 3, 4, 5, 5, 4, 4, 3, 3, 4, 4, 4, 5, 5, 4, 4, 4, 4, 3, 3, 6, 7, 7, 7, 8, 9, 10, 9, 8, 7,
+    7, 6, 11, 12, 13, 11, 6, 7, 8, 9, 14, 10, 9, 8, 6, 11, 12, 13, 11, 6, 9, 14, 10, 9, 11, 12, 13, 11, 14, 10, 12};
+  static const uint8_t last8[63] = {
+    0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
+    3, 3, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7, 8, 8, 8};
+  for (int c = 0; c < 14; c++) {
+    t->hot.cbf_base[c] = cbf[c];
+    t->hot.sig_base[c] = sig[c];
+    t->hot.last_base[c] = last[c];
+    t->hot.abs_base[c] = abs_[c];
+    t->hot.sig_est_base[c] = seb[c];
+  }
+  for (int i = 0; i < 63; i++) {
+    t->hot.sig8x8[i] = sig8[i];
+    t->hot.last8x8[i] = last8[i];
+  }
   const double alpha = std::pow(0.01875 / 0.5, 1.0 / 63.0);
   for (int s = 0; s < 64; s++) t->gen_plps[s] = (uint16_t)std::lround(65536.0 * 0.5 * std::pow(alpha, s));
 }
@@ -138,8 +172,7 @@ bool check_reciprocals(const avr::EngineTables& t) {
   uint64_t x = 0x9E3779B97F4A7C15ull;
   for (uint32_t d = 2; d < 128; d++) {
     auto q = [&](uint64_t v) -> uint64_t {
-      if (v >> 63) return t.hot.div_top[d];
-      return (uint64_t)(((unsigned __int128)v * t.hot.div_m[d]) >> 64) >> t.hot.div_s[d];
+      return (uint64_t)(((unsigned __int128)v * t.hot.div[d][0]) >> 64) >> t.hot.div[d][1];
     };
     const uint64_t edge[] = {0, 1, d - 1, d, d + 1, (1ull << 63) - 1, 1ull << 63, (1ull << 62) + 12345};
     for (uint64_t v : edge)

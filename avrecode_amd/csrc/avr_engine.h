@@ -22,13 +22,19 @@ constexpr int kStage = 1024;  // bytes per LDS staging window
 
 // Tables read on every bin: copied into each workgroup's LDS at kernel start.
 struct HotTables {
-  uint64_t div_m[128];    // ceil(2^(63+l)/d), l = ceil(log2 d)
-  uint64_t div_top[128];  // floor(2^63 / d)
-  uint8_t lps[512];       // [q*128 + state]
-  uint8_t mlps[256];      // [128+s] after MPS, [127-s] after LPS
-  uint8_t div_s[128];     // l - 1
-  uint8_t nb_left[48];    // get_neighbor_sub_mb: block left of n (| 128 if in the left macroblock)
-  uint8_t nb_up[48];      //                      block above n (| 128 if in the upper macroblock)
+  uint64_t div[128][2];     // [d] = {m, shift}: floor(n/d) = umulhi(n, m) >> shift for n <= 2^63,
+                            //   m = ceil(2^(63+l)/d), l = ceil(log2 d), shift = l - 1 (one 16-B read)
+  uint64_t cabac[128];      // [state]: LPS range for q = (range >> 6) & 3 in byte q, successor state
+                            //   after an MPS in byte 4, after an LPS in byte 5 (one 8-B read per bin)
+  uint8_t nb_left[48];      // get_neighbor_sub_mb: block left of n (| 128 if in the left macroblock)
+  uint8_t nb_up[48];        //                      block above n (| 128 if in the upper macroblock)
+  uint8_t sig8x8[64];       // significant_coeff_flag ctxIdxInc of 8x8 blocks (frame coded)
+  uint8_t last8x8[64];      // last_significant_coeff_flag ctxIdxInc of 8x8 blocks
+  int16_t cbf_base[16];     // ctxIdxOffset + ctxBlockCatOffset per ctxBlockCat, 9.3.3.1.1.9
+  int16_t sig_base[16];
+  int16_t last_base[16];
+  int16_t abs_base[16];
+  int32_t sig_est_base[16]; // first dense SIG estimator of each ctxBlockCat
 };
 static_assert(sizeof(HotTables) % 16 == 0, "HotTables is copied in 16-byte units");
 
@@ -103,69 +109,65 @@ __device__ __forceinline__ uint32_t out_total(const OutStream& o) { return o.n; 
 __device__ __forceinline__ bool out_overflow(const OutStream& o) { return o.n > o.cap; }
 
 // ---------------------------------------------------------------------- CABAC decoding engine
+// 32-bit form of the 9.3.3.2 engine: low = codIOffset << k | the next k stream bits, k >= 8 at
+// the start of every operation (one operation consumes at most 7 bits), refilled 16 bits at a
+// time so low stays below 2^32.  Every quantity fits a scalar register.
 struct CabacDecoder {
-  uint64_t value;      // offset << avail | lookahead bits
+  uint32_t low;        // offset << k | lookahead bits
   uint32_t range;      // 9-bit codIRange
-  int avail;           // lookahead bits below the 9-bit offset
+  int k;               // lookahead bits below the 9-bit offset
   uint32_t next;       // next byte to load
 };
 
 __device__ __forceinline__ void cd_refill(CabacDecoder& d, InStream& in) {
-  uint32_t w = in_be32(in, d.next);
-  d.next += 4;
-  d.value = (d.value << 32) | w;
-  d.avail += 32;
+  if (d.k < 8) {
+    d.low = (d.low << 16) | (in_be32(in, d.next) >> 16);
+    d.next += 2;
+    d.k += 16;
+  }
 }
 __device__ __forceinline__ void cd_init(CabacDecoder& d, InStream& in) {  // 9.3.1.2
-  d.value = 0;
-  d.avail = -9;
-  d.next = 0;
+  d.low = in_be32(in, 0) >> 8;   // 9 offset bits + 15 lookahead bits
+  d.k = 15;
+  d.next = 3;
   d.range = 510;
-  cd_refill(d, in);
 }
 // bits consumed by the spec decoder so far (9 + renormalisation shifts)
-__device__ __forceinline__ uint32_t cd_bitpos(const CabacDecoder& d) { return 8u * d.next - (uint32_t)d.avail; }
+__device__ __forceinline__ uint32_t cd_bitpos(const CabacDecoder& d) { return 8u * d.next - (uint32_t)d.k; }
 
+// state byte = 2*pStateIdx + valMPS (FFmpeg's cabac_state layout); rec = HotTables::cabac[state]
 __device__ __forceinline__ int cd_decision(CabacDecoder& d, InStream& in, uint8_t* state, const HotTables* T) {
-  uint32_t s = *state;
-  uint32_t lps = T->lps[((d.range >> 6) & 3) * 128 + s];
-  d.range -= lps;
-  uint64_t scaled = (uint64_t)d.range << d.avail;
-  int bin;
-  if (d.value >= scaled) {
-    bin = !(s & 1);
-    d.value -= scaled;
-    d.range = lps;
-    *state = T->mlps[127 - s];
-  } else {
-    bin = s & 1;
-    *state = T->mlps[128 + s];
-  }
-  int n = __clz(d.range) - 23;
+  const uint32_t s = *state;
+  const uint64_t rec = T->cabac[s];
+  const uint32_t lps = (uint32_t)(rec >> ((d.range >> 3) & 0x18)) & 0xff;
+  const uint32_t rmps = d.range - lps;
+  const uint32_t scaled = rmps << d.k;
+  const bool is_lps = d.low >= scaled;
+  d.low -= is_lps ? scaled : 0;
+  d.range = is_lps ? lps : rmps;
+  *state = (uint8_t)(rec >> (is_lps ? 40 : 32));
+  const int n = __clz(d.range) - 23;
   d.range <<= n;
-  d.avail -= n;
-  if (d.avail < 16) cd_refill(d, in);
-  return bin;
+  d.k -= n;
+  cd_refill(d, in);
+  return (int)(s & 1) ^ (int)is_lps;
 }
 __device__ __forceinline__ int cd_bypass(CabacDecoder& d, InStream& in) {
-  d.avail -= 1;
-  uint64_t scaled = (uint64_t)d.range << d.avail;
-  int bin = 0;
-  if (d.value >= scaled) {
-    d.value -= scaled;
-    bin = 1;
-  }
-  if (d.avail < 16) cd_refill(d, in);
-  return bin;
+  d.k -= 1;
+  const uint32_t scaled = d.range << d.k;
+  const bool one = d.low >= scaled;
+  d.low -= one ? scaled : 0;
+  cd_refill(d, in);
+  return one;
 }
 __device__ __forceinline__ int cd_terminate(CabacDecoder& d, InStream& in) {
   d.range -= 2;
-  uint64_t scaled = (uint64_t)d.range << d.avail;
-  if (d.value >= scaled) return 1;  // no renormalisation: the last bit read is rbsp_stop_one_bit
+  const uint32_t scaled = d.range << d.k;
+  if (d.low >= scaled) return 1;  // no renormalisation: the last bit read is rbsp_stop_one_bit
   if (d.range < 256) {
     d.range <<= 1;
-    d.avail -= 1;
-    if (d.avail < 16) cd_refill(d, in);
+    d.k -= 1;
+    cd_refill(d, in);
   }
   return 0;
 }
@@ -173,8 +175,9 @@ __device__ __forceinline__ int cd_terminate(CabacDecoder& d, InStream& in) {
 // ---------------------------------------------------------------------- CABAC re-encoder
 // Interval arithmetic identical to the spec encoder; the flush writes x = (low' | 1) through its
 // last set bit, which is the value arithmetic_code::finish() selects for cabac_code.h.
+// low holds the pending bits plus a 10-bit window; queue <= 7 keeps it below 2^25.
 struct CabacEncoder {
-  uint64_t low;        // pending bits + 10-bit window (bit 9 = carry into the window)
+  uint32_t low;        // pending bits + 10-bit window (bit 9 = carry into the window)
   uint32_t range;      // 9-bit
   int queue;           // (pending bits above the window) - 8
   uint32_t outstanding;
@@ -191,13 +194,72 @@ __device__ __forceinline__ void ce_init(CabacEncoder& e) {
   e.cache = 0;
   e.err = 0;
 }
-__device__ __forceinline__ void ce_putbyte(CabacEncoder& e, OutStream& o) {
+// one byte out of the window (called with queue >= 0)
+__device__ __forceinline__ void ce_putbyte1(CabacEncoder& e, OutStream& o) {
+  const uint32_t out = e.low >> (e.queue + 10);
+  e.low &= (0x400u << e.queue) - 1;
+  e.queue -= 8;
+  const uint32_t carry = out >> 8, byte = out & 0xff;
+  if (byte == 0xff && !carry) {
+    e.outstanding++;
+  } else {
+    if (e.have_cache) {
+      if (e.cache + carry > 0xff) e.err = 1;
+      out_byte(o, e.cache + carry);
+    } else if (carry) {
+      e.err = 1;
+    }
+    if (e.outstanding) out_repeat(o, (0xff + carry) & 0xff, e.outstanding);
+    e.outstanding = 0;
+    e.cache = byte;
+    e.have_cache = 1;
+  }
+}
+__device__ __forceinline__ void ce_decision(CabacEncoder& e, OutStream& o, int bin, uint8_t* state,
+                                            const HotTables* T) {
+  const uint32_t s = *state;
+  const uint64_t rec = T->cabac[s];
+  const uint32_t lps = (uint32_t)(rec >> ((e.range >> 3) & 0x18)) & 0xff;
+  const uint32_t rmps = e.range - lps;
+  const bool is_lps = bin != (int)(s & 1);
+  e.low += is_lps ? rmps : 0;
+  e.range = is_lps ? lps : rmps;
+  *state = (uint8_t)(rec >> (is_lps ? 40 : 32));
+  const int n = __clz(e.range) - 23;   // <= 6: at most one byte per decision
+  e.range <<= n;
+  e.low <<= n;
+  e.queue += n;
+  if (e.queue >= 0) ce_putbyte1(e, o);
+}
+__device__ __forceinline__ void ce_bypass(CabacEncoder& e, OutStream& o, int bin) {
+  e.low = (e.low << 1) + (bin ? e.range : 0);
+  e.queue += 1;
+  if (e.queue >= 0) ce_putbyte1(e, o);
+}
+__device__ __forceinline__ void ce_terminate(CabacEncoder& e, OutStream& o, int bin) {
+  e.range -= 2;
+  if (!bin) {
+    const int n = __clz(e.range) - 23;
+    e.range <<= n;
+    e.low <<= n;
+    e.queue += n;
+    if (e.queue >= 0) ce_putbyte1(e, o);
+    return;
+  }
+  // flush: x = (low + range - 2) | 1 in units of the window LSB, written through that bit.
+  // Up to 25 pending bits + 10 + 7 pad: done in 64 bits, once per slice.
+  uint64_t low = (uint64_t)((e.low + e.range) | 1) << 10;
+  int queue = e.queue + 10;
+  const int total = queue + 8;  // bits still pending
+  const int pad = (8 - (total & 7)) & 7;
+  low <<= pad;
+  queue += pad;
   #pragma clang loop unroll(disable)
-  while (e.queue >= 0) {
-    uint32_t out = (uint32_t)(e.low >> (e.queue + 10));
-    e.low &= (0x400ull << e.queue) - 1;
-    e.queue -= 8;
-    uint32_t carry = out >> 8, byte = out & 0xff;
+  while (queue >= 0) {
+    const uint32_t out = (uint32_t)(low >> (queue + 10));
+    low &= (0x400ull << queue) - 1;
+    queue -= 8;
+    const uint32_t carry = out >> 8, byte = out & 0xff;
     if (byte == 0xff && !carry) {
       e.outstanding++;
     } else {
@@ -213,48 +275,8 @@ __device__ __forceinline__ void ce_putbyte(CabacEncoder& e, OutStream& o) {
       e.have_cache = 1;
     }
   }
-}
-__device__ __forceinline__ void ce_renorm(CabacEncoder& e, OutStream& o) {
-  int n = __clz(e.range) - 23;
-  e.range <<= n;
-  e.low <<= n;
-  e.queue += n;
-  if (e.queue >= 0) ce_putbyte(e, o);
-}
-__device__ __forceinline__ void ce_decision(CabacEncoder& e, OutStream& o, int bin, uint8_t* state,
-                                            const HotTables* T) {
-  uint32_t s = *state;
-  uint32_t lps = T->lps[((e.range >> 6) & 3) * 128 + s];
-  e.range -= lps;
-  if (bin != (int)(s & 1)) {
-    e.low += e.range;
-    e.range = lps;
-    *state = T->mlps[127 - s];
-  } else {
-    *state = T->mlps[128 + s];
-  }
-  ce_renorm(e, o);
-}
-__device__ __forceinline__ void ce_bypass(CabacEncoder& e, OutStream& o, int bin) {
-  e.low = (e.low << 1) + (bin ? e.range : 0);
-  e.queue += 1;
-  if (e.queue >= 0) ce_putbyte(e, o);
-}
-__device__ __forceinline__ void ce_terminate(CabacEncoder& e, OutStream& o, int bin) {
-  e.range -= 2;
-  if (!bin) {
-    ce_renorm(e, o);
-    return;
-  }
-  // flush: x = (low + range - 2) | 1 in units of the window LSB, written through that bit
-  e.low = (e.low + e.range) | 1;
-  e.low <<= 10;
-  e.queue += 10;
-  int total = e.queue + 8;  // bits still pending
-  int pad = (8 - (total & 7)) & 7;
-  e.low <<= pad;
-  e.queue += pad;
-  ce_putbyte(e, o);
+  e.low = 0;
+  e.queue = queue;
   if (e.have_cache) out_byte(o, e.cache);
   if (e.outstanding) out_repeat(o, 0xff, e.outstanding);
   e.outstanding = 0;
@@ -262,9 +284,9 @@ __device__ __forceinline__ void ce_terminate(CabacEncoder& e, OutStream& o, int 
 }
 
 // ----------------------------------------------------------------- recoded coder (u64 / u8)
+// floor(range / d) for range <= 2^63 (exact at 2^63 too: see check_reciprocals in avr_api.cpp)
 __device__ __forceinline__ uint64_t rc_div(uint64_t range, uint32_t d, const HotTables* T) {
-  if (range >> 63) return T->div_top[d];
-  return __umul64hi(range, T->div_m[d]) >> T->div_s[d];
+  return __umul64hi(range, T->div[d][0]) >> (uint32_t)T->div[d][1];
 }
 // p1 = (range/(pos+neg))*pos  (recode.cpp:819); est = (pos-1) | (neg-1) << 8
 __device__ __forceinline__ uint64_t rc_p1(uint64_t range, uint32_t est, const HotTables* T) {
@@ -296,9 +318,11 @@ __device__ __forceinline__ void re_init(RecodedEncoder& e) {
   e.cache = 0;
   e.err = 0;
 }
+__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
 __device__ __forceinline__ void re_shift(RecodedEncoder& e, OutStream& o) {
-  uint32_t carry = (uint32_t)(e.low >> 63);
-  uint32_t digit = (uint32_t)(e.low >> 55) & 0xff;
+  const uint32_t h = hi32(e.low);
+  const uint32_t carry = h >> 31;
+  const uint32_t digit = (h >> 23) & 0xff;
   if (digit != 0xff || carry) {
     if (e.have_cache) {
       if (e.cache + carry > 0xff) e.err = 1;
@@ -316,19 +340,16 @@ __device__ __forceinline__ void re_shift(RecodedEncoder& e, OutStream& o) {
   e.low = (e.low & ((1ull << 55) - 1)) << 8;
 }
 __device__ __forceinline__ void re_put(RecodedEncoder& e, OutStream& o, int bin, uint64_t r1) {
-  if (bin) {
-    e.low += e.range - r1;
-    e.range = r1;
-  } else {
-    e.range -= r1;
-  }
-  if (e.range < (1ull << 51)) {  // min_range = (fixed_one/digit_base)/16
+  const uint64_t r0 = e.range - r1;
+  e.low += bin ? r0 : 0;
+  e.range = bin ? r1 : r0;
+  if (hi32(e.range) < (1u << 19)) {  // range < min_range = (fixed_one/digit_base)/16 = 2^51
     if (e.range == 0) e.err = 1;
     #pragma clang loop unroll(disable)
-    while (e.range < (1ull << 55)) {
+    do {  // at most twice: r1, r0 >= range/96 and range >= 2^51 before the put
       re_shift(e, o);
       e.range <<= 8;
-    }
+    } while (hi32(e.range) < (1u << 23) && e.range != 0);  // until range >= 2^55
   }
 }
 __device__ __forceinline__ void re_finish(RecodedEncoder& e, OutStream& o) {  // arith:128-144
@@ -369,17 +390,14 @@ __device__ __forceinline__ void rd_init(RecodedDecoder& d, InStream& in) {  // a
   while (d.range < (1ull << 63)) rd_consume(d, in);
 }
 __device__ __forceinline__ int rd_get(RecodedDecoder& d, InStream& in, uint64_t r1) {
-  uint64_t r0 = d.range - r1;
-  int bin = d.low >= r0;
-  if (bin) {
-    d.low -= r0;
-    d.range = r1;
-  } else {
-    d.range = r0;
-  }
-  if (d.range < (1ull << 51))
+  const uint64_t r0 = d.range - r1;
+  const bool bin = d.low >= r0;
+  d.low -= bin ? r0 : 0;
+  d.range = bin ? r1 : r0;
+  if (hi32(d.range) < (1u << 19)) {
     #pragma clang loop unroll(disable)
-    while (d.range < (1ull << 55)) rd_consume(d, in);
+    while (hi32(d.range) < (1u << 23) && d.range != 0) rd_consume(d, in);
+  }
   return bin;
 }
 

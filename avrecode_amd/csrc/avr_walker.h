@@ -41,20 +41,7 @@ static __constant__ uint8_t c_scan8[51] = {
   4 + 13 * 8, 5 + 13 * 8, 4 + 14 * 8, 5 + 14 * 8, 6 + 13 * 8, 7 + 13 * 8, 6 + 14 * 8, 7 + 14 * 8,
   0 + 0 * 8,  0 + 5 * 8,  0 + 10 * 8,
 };
-static __constant__ int16_t c_cbf_base[14] = {85, 89, 93, 97, 101, 1012, 460, 464, 468, 1016, 472, 476, 480, 1020};
-static __constant__ int16_t c_sig_base[14] = {105, 120, 134, 149, 152, 402, 484, 499, 513, 660, 528, 543, 557, 718};
-static __constant__ int16_t c_last_base[14] = {166, 181, 195, 210, 213, 417, 572, 587, 601, 690, 616, 631, 645, 748};
-static __constant__ int16_t c_abs_base[14] = {227, 237, 247, 257, 266, 426, 952, 962, 972, 708, 982, 992, 1002, 766};
-static __constant__ uint8_t c_sig8x8[63] = {
-  0, 1, 2, 3, 4, 5, 5, 4, 4, 3, 3, 4, 4, 4, 5, 5, 4, 4, 4, 4, 3, 3, 6, 7, 7, 7, 8, 9, 10, 9, 8, 7,
-  7, 6, 11, 12, 13, 11, 6, 7, 8, 9, 14, 10, 9, 8, 6, 11, 12, 13, 11, 6, 9, 14, 10, 9, 11, 12, 13, 11, 14, 10, 12};
-static __constant__ uint8_t c_last8x8[63] = {
-  0, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2,
-  3, 3, 3, 3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 7, 8, 8, 8};
 static __constant__ uint8_t c_b_pairs[9][2] = {{1, 1}, {2, 2}, {1, 2}, {2, 1}, {1, 3}, {2, 3}, {3, 1}, {3, 2}, {3, 3}};
-// dense SIG estimator base per ctxBlockCat: 4096 per 4x4-class cat, 61440 for 8x8 cats (5, 9, 13)
-static __constant__ int32_t c_sig_est_base[14] = {0, 4096, 8192, 12288, 16384, 20480, 81920, 86016, 90112,
-                                           94208, 155648, 159744, 163840, 167936};
 constexpr int kSigEst = 229376;
 constexpr int kNzEst = 63 * 2 * 3 * 3 * 57;
 constexpr int kEstDefault = 1026;
@@ -315,15 +302,15 @@ struct Walker {
   }
 
   AVR_FI int sig_est_index(int cat, int max, int is_dc, int c422, int zz, int nnz_m, int obs) const {
-    if (max == 64) return c_sig_est_base[cat] + (c_sig8x8[zz] * 64 + nnz_m) * 64 + obs;
+    if (max == 64) return T->sig_est_base[cat] + (T->sig8x8[zz] * 64 + nnz_m) * 64 + obs;
     int zo = (is_dc && c422) ? (zz < 2 ? 0 : zz < 4 ? 1 : 2) : zz;
-    return c_sig_est_base[cat] + (zo * 16 + nnz_m) * 16 + obs;
+    return T->sig_est_base[cat] + (zo * 16 + nnz_m) * 16 + obs;
   }
 
   // significance map of one residual block; returns the coefficient count
   AVR_FI int sig_map(int cat, int n, int max, int is_dc, int c422) {
     const int numc8x8 = cat_ == 2 ? 2 : 1;
-    const int sb = c_sig_base[cat], lb = c_last_base[cat];
+    const int sb = T->sig_base[cat], lb = T->last_base[cat];
     const int bits = max > 16 ? 6 : max > 4 ? 4 : 2;
     const int mask = (1 << bits) - 1;
     int cnt = 0;
@@ -332,7 +319,7 @@ struct Walker {
       int pos, end = max - 2;
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
-        if (max == 64) { sc = c_sig8x8[pos]; lc = c_last8x8[pos]; }
+        if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
         bins++;
@@ -362,7 +349,7 @@ struct Walker {
       int pos;
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
-        if (max == 64) { sc = c_sig8x8[pos]; lc = c_last8x8[pos]; }
+        if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
         int idx = sig_est_index(cat, max, is_dc, c422, pos, nnz_m, cnt);
@@ -385,7 +372,7 @@ struct Walker {
       int pos;
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
-        if (max == 64) { sc = c_sig8x8[pos]; lc = c_last8x8[pos]; }
+        if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
         if (bin(SE_OTHER, 0, sb + sc)) {
@@ -413,13 +400,13 @@ struct Walker {
         nza = nnz_left(p, pw, x4, y4) > 0;
         nzb = nnz_top(p, x4, y4) > 0;
       }
-      coded = bin(SE_OTHER, 0, c_cbf_base[cat] + nza + 2 * nzb);
+      coded = bin(SE_OTHER, 0, T->cbf_base[cat] + nza + 2 * nzb);
     }
     int cnt = 0;
     if (coded) {
       cnt = sig_map(cat, n, max, is_dc, c422);
       // coeff_abs_level_minus1 + sign, reverse scan order
-      const int ab = c_abs_base[cat];
+      const int ab = T->abs_base[cat];
       int gt1 = 0, eq1 = 0;
       for (int i = cnt - 1; i >= 0 && !err; i--) {
         int absl;
