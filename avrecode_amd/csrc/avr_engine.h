@@ -20,6 +20,13 @@ namespace avr {
 
 constexpr int kStage = 1024;  // bytes per LDS staging window
 
+// The serial state is wave-uniform and lives in SGPRs.  LLVM folds a compare of the high word of
+// a 64-bit value back into a 64-bit compare, which the scalar unit lacks (it becomes a VALU
+// compare + a VCC round trip); readfirstlane on the high word (free on a uniform value) keeps
+// the compare 32-bit scalar.
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t hi32(uint64_t x) { return opaque_u32((uint32_t)(x >> 32)); }
+
 // Tables read on every bin: copied into each workgroup's LDS at kernel start.
 struct HotTables {
   uint64_t div[128][2];     // [d] = {m, shift}: floor(n/d) = umulhi(n, m) >> shift for n <= 2^63,
@@ -135,22 +142,29 @@ __device__ __forceinline__ void cd_init(CabacDecoder& d, InStream& in) {  // 9.3
 // bits consumed by the spec decoder so far (9 + renormalisation shifts)
 __device__ __forceinline__ uint32_t cd_bitpos(const CabacDecoder& d) { return 8u * d.next - (uint32_t)d.k; }
 
-// state byte = 2*pStateIdx + valMPS (FFmpeg's cabac_state layout); rec = HotTables::cabac[state]
-__device__ __forceinline__ int cd_decision(CabacDecoder& d, InStream& in, uint8_t* state, const HotTables* T) {
-  const uint32_t s = *state;
-  const uint64_t rec = T->cabac[s];
+// One decision given the context's state byte s (2*pStateIdx + valMPS, FFmpeg's cabac_state
+// layout) and rec = HotTables::cabac[s]; *ns receives the successor state.  No memory access, so
+// the caller can issue the state / record reads of the model side at the same time.
+__device__ __forceinline__ int cd_decide(CabacDecoder& d, InStream& in, uint32_t s, uint64_t rec, uint32_t* ns) {
   const uint32_t lps = (uint32_t)(rec >> ((d.range >> 3) & 0x18)) & 0xff;
   const uint32_t rmps = d.range - lps;
   const uint32_t scaled = rmps << d.k;
   const bool is_lps = d.low >= scaled;
   d.low -= is_lps ? scaled : 0;
   d.range = is_lps ? lps : rmps;
-  *state = (uint8_t)(rec >> (is_lps ? 40 : 32));
+  *ns = (uint32_t)(rec >> (is_lps ? 40 : 32)) & 0xff;
   const int n = __clz(d.range) - 23;
   d.range <<= n;
   d.k -= n;
   cd_refill(d, in);
   return (int)(s & 1) ^ (int)is_lps;
+}
+__device__ __forceinline__ int cd_decision(CabacDecoder& d, InStream& in, uint8_t* state, const HotTables* T) {
+  const uint32_t s = *state;
+  uint32_t ns;
+  const int b = cd_decide(d, in, s, T->cabac[s], &ns);
+  *state = (uint8_t)ns;
+  return b;
 }
 __device__ __forceinline__ int cd_bypass(CabacDecoder& d, InStream& in) {
   d.k -= 1;
@@ -215,21 +229,26 @@ __device__ __forceinline__ void ce_putbyte1(CabacEncoder& e, OutStream& o) {
     e.have_cache = 1;
   }
 }
-__device__ __forceinline__ void ce_decision(CabacEncoder& e, OutStream& o, int bin, uint8_t* state,
-                                            const HotTables* T) {
-  const uint32_t s = *state;
-  const uint64_t rec = T->cabac[s];
+__device__ __forceinline__ void ce_encode(CabacEncoder& e, OutStream& o, int bin, uint32_t s, uint64_t rec,
+                                          uint32_t* ns) {
   const uint32_t lps = (uint32_t)(rec >> ((e.range >> 3) & 0x18)) & 0xff;
   const uint32_t rmps = e.range - lps;
   const bool is_lps = bin != (int)(s & 1);
   e.low += is_lps ? rmps : 0;
   e.range = is_lps ? lps : rmps;
-  *state = (uint8_t)(rec >> (is_lps ? 40 : 32));
+  *ns = (uint32_t)(rec >> (is_lps ? 40 : 32)) & 0xff;
   const int n = __clz(e.range) - 23;   // <= 6: at most one byte per decision
   e.range <<= n;
   e.low <<= n;
   e.queue += n;
   if (e.queue >= 0) ce_putbyte1(e, o);
+}
+__device__ __forceinline__ void ce_decision(CabacEncoder& e, OutStream& o, int bin, uint8_t* state,
+                                            const HotTables* T) {
+  const uint32_t s = *state;
+  uint32_t ns;
+  ce_encode(e, o, bin, s, T->cabac[s], &ns);
+  *state = (uint8_t)ns;
 }
 __device__ __forceinline__ void ce_bypass(CabacEncoder& e, OutStream& o, int bin) {
   e.low = (e.low << 1) + (bin ? e.range : 0);
@@ -290,8 +309,8 @@ __device__ __forceinline__ uint64_t rc_div(uint64_t range, uint32_t d, const Hot
 }
 // p1 = (range/(pos+neg))*pos  (recode.cpp:819); est = (pos-1) | (neg-1) << 8
 __device__ __forceinline__ uint64_t rc_p1(uint64_t range, uint32_t est, const HotTables* T) {
-  uint32_t pos = (est & 0xff) + 1, neg = (est >> 8) + 1;
-  return rc_div(range, pos + neg, T) * pos;
+  const uint32_t pos = (est & 0xff) + 1, tot = pos + (est >> 8) + 1;
+  return rc_div(range, tot, T) * pos;
 }
 // update_state_for_model_key (recode.cpp:1036-1045)
 __device__ __forceinline__ uint32_t est_update(uint32_t est, int bin, uint32_t thresh) {
@@ -318,7 +337,6 @@ __device__ __forceinline__ void re_init(RecodedEncoder& e) {
   e.cache = 0;
   e.err = 0;
 }
-__device__ __forceinline__ uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
 __device__ __forceinline__ void re_shift(RecodedEncoder& e, OutStream& o) {
   const uint32_t h = hi32(e.low);
   const uint32_t carry = h >> 31;
@@ -389,10 +407,13 @@ __device__ __forceinline__ void rd_init(RecodedDecoder& d, InStream& in) {  // a
   #pragma clang loop unroll(disable)
   while (d.range < (1ull << 63)) rd_consume(d, in);
 }
+// low < range <= 2^63, so low - r0 fits a signed 64-bit value: its sign bit is the decision
+// (two scalar subtracts and a 32-bit shift instead of a vector 64-bit compare).
 __device__ __forceinline__ int rd_get(RecodedDecoder& d, InStream& in, uint64_t r1) {
   const uint64_t r0 = d.range - r1;
-  const bool bin = d.low >= r0;
-  d.low -= bin ? r0 : 0;
+  const uint64_t diff = d.low - r0;
+  const bool bin = (hi32(diff) >> 31) == 0;
+  d.low = bin ? diff : d.low;
   d.range = bin ? r1 : r0;
   if (hi32(d.range) < (1u << 19)) {
     #pragma clang loop unroll(disable)

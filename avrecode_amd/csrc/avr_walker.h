@@ -119,16 +119,24 @@ struct Walker {
   AVR_FI int bin(int se, int k, int ctx) {
     bins++;
     if (MODE == MODE_COMPRESS) {
-      int b = cd_decision(cd, in, &sh->state[ctx], T);
-      uint32_t e = sh->est[ctx];
-      re_put(re, out, b, rc_p1(re.range, e, T));
+      // both reads first (no store in between), then both dependent record reads
+      const uint32_t e = sh->est[ctx], s = sh->state[ctx];
+      const uint64_t rec = T->cabac[s];
+      const uint64_t p1 = rc_p1(re.range, e, T);
+      uint32_t ns;
+      const int b = cd_decide(cd, in, s, rec, &ns);
+      re_put(re, out, b, p1);
+      sh->state[ctx] = (uint8_t)ns;
       sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
-      uint32_t e = sh->est[ctx];
-      int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      const uint32_t e = sh->est[ctx], s = sh->state[ctx];
+      const uint64_t rec = T->cabac[s];
+      const int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      uint32_t ns;
+      ce_encode(ce, out, b, s, rec, &ns);
+      sh->state[ctx] = (uint8_t)ns;
       sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
-      ce_decision(ce, out, b, &sh->state[ctx], T);
       return b;
     } else {
       int b = gen_bin(se, k, ctx);
@@ -415,7 +423,9 @@ struct Walker {
         } else {
           const int c1 = ab + 5 + min(4 - (cat == 3), gt1);
           absl = 2;
+          asm volatile("; MARK_LEVEL_BEGIN");
           while (absl < 15 && bin(SE_OTHER, 0, c1)) absl++;
+          asm volatile("; MARK_LEVEL_END");
           if (absl >= 15) {
             int k = 0;
             while (bypass(SE_LEVEL_SUFFIX, k)) {
