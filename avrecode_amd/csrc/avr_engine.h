@@ -65,15 +65,19 @@ struct InStream {
 
 // Load the window [at, at + kStage) into LDS, bytes at or past `limit` as 0.  Returns `at`.
 __device__ __noinline__ uint32_t in_fill_call(uint8_t* lds, const uint8_t* g, uint32_t limit, uint32_t at) {
-  __syncthreads();
-  const int lane = threadIdx.x;
+  // one wave fills and reads the window: its LDS operations execute in order, so only the
+  // compiler needs fencing (the other wave of the workgroup never touches the window)
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  const int lane = __lane_id();
   const uint32_t base = at + 16u * lane;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     uint32_t i = base + k;
     lds[16 * lane + k] = i < limit ? g[i] : 0;
   }
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
   return at;
 }
 // byte i of the stream (0 at or past limit: the window is zero-filled there)
@@ -97,14 +101,14 @@ struct OutStream {
   uint32_t last;       // last byte emitted
 };
 __device__ __forceinline__ void out_byte(OutStream& o, uint32_t v) {
-  if (o.n < o.cap && threadIdx.x == 0) o.g[o.n] = (uint8_t)v;
+  if (o.n < o.cap && __lane_id() == 0) o.g[o.n] = (uint8_t)v;
   o.n++;
   o.last = v & 0xff;
 }
 // k copies of byte v at g[n..n+k) (the deferred 0xFF runs of the carry handling).  Rare: a real
 // call, so the loop exists once (inlined, the compiler unrolls it at every bin site).
 __device__ __noinline__ void out_run_call(uint8_t* g, uint32_t cap, uint32_t n, uint32_t v, uint32_t k) {
-  for (uint32_t i = threadIdx.x; i < k; i += 64)
+  for (uint32_t i = __lane_id(); i < k; i += 64)
     if (n + i < cap) g[n + i] = (uint8_t)v;
 }
 __device__ __forceinline__ void out_repeat(OutStream& o, uint32_t v, uint32_t k) {

@@ -6,9 +6,22 @@ namespace avr {
 hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
                     uint8_t* out, avr_slice_result* res, uint16_t* est, uint8_t* frames, int* frame_meta,
                     hipStream_t stream) {
-  hipLaunchKernelGGL(slices_sequential_kernel<MODE_COMPRESS>, dim3(1), dim3(64), lds, stream, T, descs, n, in, out, res, est,
+  hipLaunchKernelGGL(slices_sequential_kernel<MODE_COMPRESS>, dim3(1), dim3(128), lds, stream, T, descs, n, in, out, res, est,
                      frames, frame_meta);
   return hipGetLastError();
+}
+
+// AVR_PROFILE builds: read (and clear) this kernel's section cycle counters; zeros otherwise.
+hipError_t profile_sequential_compress(unsigned long long* out16) {
+#ifdef AVR_PROFILE
+  hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(avr_prof), sizeof(unsigned long long) * 16);
+  unsigned long long z[16] = {};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(avr_prof), z, sizeof(z));
+  return e;
+#else
+  for (int i = 0; i < 16; i++) out16[i] = 0;
+  return hipSuccess;
+#endif
 }
 
 }  // namespace avr

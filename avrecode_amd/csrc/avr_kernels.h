@@ -34,6 +34,12 @@ hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_des
 hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                         const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                         uint8_t* frames, int* frame_meta, hipStream_t stream);
+// section cycle counters of AVR_PROFILE builds (avr_walker.h); zeros otherwise
+hipError_t profile_parallel_compress(unsigned long long* out16);
+hipError_t profile_parallel_decompress(unsigned long long* out16);
+hipError_t profile_parallel_generate(unsigned long long* out16);
+hipError_t profile_sequential_compress(unsigned long long* out16);
+hipError_t profile_sequential_decompress(unsigned long long* out16);
 hipError_t launch_derive_decompress(const avr_slice_desc* descs, const avr_slice_result* rc, int n,
                                     avr_slice_desc* dd, hipStream_t stream);
 hipError_t launch_verify(const avr_slice_desc* descs, const avr_slice_result* rc, const avr_slice_result* rd, int n,

@@ -26,7 +26,27 @@
 
 #define AVR_FI __device__ __forceinline__
 
+// Cycle accounting per walker section, compiled in with -DAVR_PROFILE only (scripts/prof_sections):
+// 0 slice, 1 macroblock syntax, 2 residual, 3 map decode, 4 nnz bins, 5 map re-code, 6 levels,
+// 7 per-macroblock bookkeeping; [8 + i] bins coded in section i.  Summed over slices into avr_prof (one copy per TU).
+#ifdef AVR_PROFILE
+#define PROF_T() ((uint64_t)__builtin_readcyclecounter())
+#define PROF_BEGIN(v) const uint64_t v = PROF_T(); const uint32_t v##_b = bins
+#define PROF_BEGINW(v) const uint64_t v = PROF_T(); const uint32_t v##_b = w.bins
+#define PROF_END(i, v) prof[i] += PROF_T() - (v), profb[i] += bins - v##_b
+#define PROF_ENDW(i, v) w.prof[i] += PROF_T() - (v), w.profb[i] += w.bins - v##_b
+#else
+#define PROF_BEGINW(v)
+#define PROF_ENDW(i, v)
+#define PROF_BEGIN(v)
+#define PROF_END(i, v)
+#endif
+
 namespace avr {
+
+#ifdef AVR_PROFILE
+static __device__ unsigned long long avr_prof[16];
+#endif
 
 enum { MODE_COMPRESS = 0, MODE_DECOMPRESS = 1, MODE_GENERATE = 2 };
 enum { F_DEC = 1, F_SKIP = 2, F_INTRA = 4, F_I16 = 8, F_D16 = 16, F_T8 = 32, F_CPRED = 64 };
@@ -68,7 +88,7 @@ struct EdgeRec {        // bottom edge of the macroblock above
 };
 static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
 
-// LDS layout (per workgroup = one wavefront); the ring is sized by mb_width at launch.
+// LDS layout (per workgroup = one slice); the ring is sized by mb_width at launch.
 // LDS cache of the dense SIG + NZ estimator table (kEstGlobal u16 entries in HBM per model):
 // direct mapped, entry = (tag + 1) << 16 | estimator, 0 = empty; write-back on eviction.  The
 // significance-map bins (a third or more of all bins) then cost an LDS access, not an HBM round
@@ -76,8 +96,16 @@ static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
 constexpr int kEcacheBits = 12;
 constexpr int kEcacheSize = 1 << kEcacheBits;
 
+// Producer -> consumer ring of coding operations (see "Two waves per slice" below).
+constexpr int kFifo = 512;
+
 struct Shared {
   HotTables tab;          // copy of EngineTables::hot (per-bin lookups stay in LDS)
+  uint32_t fifo[kFifo];   // coding operations, walker wave -> coder wave
+  uint32_t fifo_head;     // operations published by the walker (monotonic)
+  uint32_t fifo_tail;     // operations retired by the coder (monotonic)
+  int32_t p_status, p_stop_ok, c_err;  // slice results of the two waves
+  uint32_t c_len, c_last;
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
   uint8_t state[1024];
   uint16_t est[kEstDefault + 2];
@@ -88,6 +116,47 @@ struct Shared {
     uint16_t gen_p[1024];          // generator: P(bin = 1) in 1/65536 per context
   };
 };
+
+// ---------------------------------------------------------------------------------------
+// Two waves per slice.  Compress and decompress each have two serial chains that only meet in
+// the bin value: the walker wave runs the CABAC parse and the model (compress: CABAC decode +
+// syntax + estimators; decompress: recoded decode + syntax + estimators) and pushes one coding
+// operation per bin into an LDS ring; the coder wave retires them in order (compress: the
+// 64-bit recoded encoder; decompress: the CABAC re-encoder).  The two chains then overlap on the
+// SIMD instead of adding up, and the coder gathers a whole batch's table records with one LDS
+// access per lane.
+//
+// Compress ops: bit 0 bin, bits 1-7 pos, bits 8-14 pos+neg (the estimator before the update,
+// recode.cpp:816-820); OP_FINISH = arithmetic_code::encoder::finish (terminate = 1).
+// Decompress ops: bit 0 bin, bits 1-2 kind (0 decision, 1 bypass, 2 terminate), bits 3-12 ctxIdx.
+// OP_END closes the slice's stream in both directions.
+constexpr uint32_t OP_FINISH = 1u << 30;
+constexpr uint32_t OP_END = 1u << 31;
+enum { OPK_DECISION = 0, OPK_BYPASS = 1, OPK_TERMINATE = 2 };
+
+AVR_FI uint32_t op_recode(int bin, uint32_t est) {
+  const uint32_t pos = (est & 0xff) + 1, tot = pos + (est >> 8) + 1;
+  return (uint32_t)bin | pos << 1 | tot << 8;
+}
+// Ring counters: plain LDS accesses.  LDS is one memory per CU and executes each wave's accesses
+// in program order, so a counter store issued after the entry stores cannot be seen before them;
+// the asm statements only keep the compiler from reordering (an acquire/release fence would
+// also wait for, or write back, this wave's outstanding global stores).
+AVR_FI uint32_t ld_volatile(const uint32_t* p) {
+  const uint32_t v = *(const volatile uint32_t*)p;
+  asm volatile("" ::: "memory");
+  return v;
+}
+AVR_FI void st_volatile(uint32_t* p, uint32_t v) {
+  asm volatile("" ::: "memory");
+  *(volatile uint32_t*)p = v;
+}
+// LDS hand-offs between the lanes of ONE wave need no barrier (a wave's LDS operations execute in
+// order); only the compiler must not move memory operations across the hand-off.
+AVR_FI void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
 template <int MODE, bool RM>
 struct Walker {
@@ -114,29 +183,46 @@ struct Walker {
   uint32_t bins;
   int target_mbs, mbs_done, last_mb;
   int nref0, nref1, d8x8inf, x264_build, first_mb;
+  uint32_t fifo_head, fifo_room;   // ops pushed; ops that fit before the next tail check
+
+  // ------------------------------------------------------------------ walker -> coder ring
+  AVR_FI void publish() { st_volatile(&sh->fifo_head, fifo_head); }
+  AVR_FI void push(uint32_t op) {
+    if (fifo_room == 0) {
+      publish();
+      for (;;) {
+        const uint32_t used = fifo_head - ld_volatile(&sh->fifo_tail);
+        if (used < (uint32_t)kFifo) { fifo_room = kFifo - used; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    sh->fifo[fifo_head & (kFifo - 1)] = op;
+    fifo_head++;
+    fifo_room--;
+    if ((fifo_head & 31) == 0) publish();
+  }
+#ifdef AVR_PROFILE
+  uint64_t prof[8];
+  uint32_t profb[8];
+#endif
 
   // ------------------------------------------------------------------ bins through the model
   AVR_FI int bin(int se, int k, int ctx) {
     bins++;
     if (MODE == MODE_COMPRESS) {
-      // both reads first (no store in between), then both dependent record reads
+      // both reads first (no store in between), then the dependent state record
       const uint32_t e = sh->est[ctx], s = sh->state[ctx];
-      const uint64_t rec = T->cabac[s];
-      const uint64_t p1 = rc_p1(re.range, e, T);
       uint32_t ns;
-      const int b = cd_decide(cd, in, s, rec, &ns);
-      re_put(re, out, b, p1);
+      const int b = cd_decide(cd, in, s, T->cabac[s], &ns);
       sh->state[ctx] = (uint8_t)ns;
       sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
+      push(op_recode(b, e));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
-      const uint32_t e = sh->est[ctx], s = sh->state[ctx];
-      const uint64_t rec = T->cabac[s];
+      const uint32_t e = sh->est[ctx];
       const int b = rd_get(rd, in, rc_p1(rd.range, e, T));
-      uint32_t ns;
-      ce_encode(ce, out, b, s, rec, &ns);
-      sh->state[ctx] = (uint8_t)ns;
       sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
+      push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
       return b;
     } else {
       int b = gen_bin(se, k, ctx);
@@ -147,16 +233,16 @@ struct Walker {
   AVR_FI int bypass(int se, int k) {
     bins++;
     if (MODE == MODE_COMPRESS) {
-      int b = cd_bypass(cd, in);
-      uint32_t e = sh->est[1024];
-      re_put(re, out, b, rc_p1(re.range, e, T));
+      const uint32_t e = sh->est[1024];
+      const int b = cd_bypass(cd, in);
       sh->est[1024] = (uint16_t)est_update(e, b, 0x60);
+      push(op_recode(b, e));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
-      uint32_t e = sh->est[1024];
-      int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      const uint32_t e = sh->est[1024];
+      const int b = rd_get(rd, in, rc_p1(rd.range, e, T));
       sh->est[1024] = (uint16_t)est_update(e, b, 0x60);
-      ce_bypass(ce, out, b);
+      push((uint32_t)b | OPK_BYPASS << 1);
       return b;
     } else {
       int b = gen_bypass(se, k);
@@ -168,16 +254,16 @@ struct Walker {
     bins++;
     int b;
     if (MODE == MODE_COMPRESS) {
+      const uint32_t e = sh->est[1025];
       b = cd_terminate(cd, in);
-      uint32_t e = sh->est[1025];
-      re_put(re, out, b, rc_p1(re.range, e, T));
       sh->est[1025] = (uint16_t)est_update(e, b, 0x60);
-      if (b) re_finish(re, out);
+      push(op_recode(b, e));
+      if (b) push(OP_FINISH);
     } else if (MODE == MODE_DECOMPRESS) {
-      uint32_t e = sh->est[1025];
+      const uint32_t e = sh->est[1025];
       b = rd_get(rd, in, rc_p1(rd.range, e, T));
       sh->est[1025] = (uint16_t)est_update(e, b, 0x60);
-      ce_terminate(ce, out, b);
+      push((uint32_t)b | OPK_TERMINATE << 1);
     } else {
       b = se == SE_EOS ? (mbs_done >= target_mbs || last_mb) : 0;
       ce_terminate(ce, out, b);
@@ -259,7 +345,7 @@ struct Walker {
     if (ent) {  // evict: write the old estimator back
       const uint32_t otag = (ent >> 16) - 1;
       const uint32_t oidx = otag << kEcacheBits | ((set ^ ec_hash(otag)) & (kEcacheSize - 1));
-      if (threadIdx.x == 0) est_g[oidx] = (uint16_t)ent;
+      if (__lane_id() == 0) est_g[oidx] = (uint16_t)ent;
     }
     return est_g[idx];
   }
@@ -299,7 +385,7 @@ struct Walker {
       int b;
       if (MODE == MODE_COMPRESS) {
         b = (count >> i) & 1;
-        re_put(re, out, b, rc_p1(re.range, e, T));
+        push(op_recode(b, e));
       } else {
         b = rd_get(rd, in, rc_p1(rd.range, e, T));
       }
@@ -325,6 +411,7 @@ struct Walker {
     if (MODE == MODE_COMPRESS) {
       uint64_t sigmask = 0;
       int pos, end = max - 2;
+      PROF_BEGIN(t3);
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
         if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
@@ -339,8 +426,12 @@ struct Walker {
         }
       }
       if (pos == max - 1) cnt++;
+      PROF_END(3, t3);
       // model: nnz first (recode.cpp:1208-1221), then the buffered map (1244-1255)
+      PROF_BEGIN(t4);
       nz_bits(cat, n, max, is_dc, c422, cnt);
+      PROF_END(4, t4);
+      PROF_BEGIN(t5);
       const int nnz_m = cnt & mask;
       int obs = 0;
       for (int zz = 0; zz <= end; zz++) {
@@ -348,10 +439,11 @@ struct Walker {
         int idx = sig_est_index(cat, max, is_dc, c422, zz, nnz_m, obs);
         uint32_t slot;
         uint32_t e = est_load(idx, &slot);
-        re_put(re, out, b, rc_p1(re.range, e, T));
+        push(op_recode(b, e));
         est_store(idx, slot, est_update(e, b, 0x50));
         obs += b;
       }
+      PROF_END(5, t5);
     } else if (MODE == MODE_DECOMPRESS) {
       const int nnz_m = nz_bits(cat, n, max, is_dc, c422, 0);   // recode.cpp:1476-1486
       int pos;
@@ -366,12 +458,12 @@ struct Walker {
         int b = rd_get(rd, in, rc_p1(rd.range, e, T));
         est_store(idx, slot, est_update(e, b, 0x50));
         bins++;
-        ce_decision(ce, out, b, &sh->state[sb + sc], T);
+        push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3);
         if (b) {
           cnt++;
           int last = nnz_m == cnt;   // derived EOB (recode.cpp:1437-1438)
           bins++;
-          ce_decision(ce, out, last, &sh->state[lb + lc], T);
+          push((uint32_t)last | OPK_DECISION << 1 | (uint32_t)(lb + lc) << 3);
           if (last) break;
         }
       }
@@ -416,6 +508,7 @@ struct Walker {
       // coeff_abs_level_minus1 + sign, reverse scan order
       const int ab = T->abs_base[cat];
       int gt1 = 0, eq1 = 0;
+      PROF_BEGIN(t6);
       for (int i = cnt - 1; i >= 0 && !err; i--) {
         int absl;
         if (!bin(SE_OTHER, 0, ab + (gt1 ? 0 : min(4, 1 + eq1)))) {
@@ -440,6 +533,7 @@ struct Walker {
         if (absl == 1) eq1++;
         else gt1++;
       }
+      PROF_END(6, t6);
       cur.mnnz[n] = (uint8_t)cnt;             // end_coding_type recount (recode.cpp:935-947)
       if (max > 32) cur.is8x8 = 1;
     }
@@ -516,11 +610,13 @@ struct Walker {
               nb = push_block(nb, 4, n, 15, 0, 0, 1 + c, 2, x4, y4);
             }
     }
+    PROF_BEGIN(t2);
     for (int j = 0; j < nb && !err; j++) {
       const uint32_t b = sh->blk[j];
       residual_block(b & 15, (b >> 4) & 63, (b >> 10) & 127, (b >> 17) & 1, (b >> 18) & 1, (b >> 19) & 3,
                      (b >> 21) & 7, (b >> 24) & 3, (b >> 26) & 3);
     }
+    PROF_END(2, t2);
   }
 
   // ------------------------------------------------------------------ prediction syntax
@@ -844,12 +940,12 @@ struct Walker {
 // ---------------------------------------------------------------------------------------
 template <int MODE, bool RM>
 AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x, nt = blockDim.x;  // every wave of the workgroup takes part
   const avr_slice_desc* d = w.d;
   // cabac contexts: 9.3.1.1
   const int tbl = d->slice_type == 2 ? 0 : 1 + d->cabac_init_idc;
   const int qp = d->slice_qp < 0 ? 0 : d->slice_qp > 51 ? 51 : d->slice_qp;
-  for (int i = lane; i < 1024; i += 64) {
+  for (int i = lane; i < 1024; i += nt) {
     int m = T->mn[tbl][i][0], n = T->mn[tbl][i][1];
     int pre = ((m * qp) >> 4) + n;
     pre = pre < 1 ? 1 : pre > 126 ? 126 : pre;
@@ -862,12 +958,16 @@ AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
     }
   }
   if (!RM) {
-    for (int i = lane; i < kEstDefault + 2; i += 64) w.sh->est[i] = 0;
+    for (int i = lane; i < kEstDefault + 2; i += nt) w.sh->est[i] = 0;
     if (MODE != MODE_GENERATE)
-      for (int i = lane; i < kEcacheSize; i += 64) w.sh->ecache[i] = 0;
+      for (int i = lane; i < kEcacheSize; i += nt) w.sh->ecache[i] = 0;
   }
   uint32_t* ring32 = (uint32_t*)w.ring;
-  for (int i = lane; i < w.W * (int)sizeof(EdgeRec) / 4; i += 64) ring32[i] = 0;
+  for (int i = lane; i < w.W * (int)sizeof(EdgeRec) / 4; i += nt) ring32[i] = 0;
+  if (lane == 0) {
+    w.sh->fifo_head = 0;
+    w.sh->fifo_tail = 0;
+  }
   __syncthreads();
 }
 
@@ -902,17 +1002,20 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
     {
       uint32_t* c32 = (uint32_t*)&w.sh->cur;
       for (int i = lane; i < (int)sizeof(MbRec) / 4; i += 64) c32[i] = 0;
-      __syncthreads();
+      wave_sync();
       for (int i = lane; i < 8; i += 64) ((int8_t*)w.sh->cur.ref)[i] = -1;
-      __syncthreads();
+      wave_sync();
     }
+    PROF_BEGINW(t1);
     w.decode_mb();
+    PROF_ENDW(1, t1);
+    PROF_BEGINW(t7);
     if (w.err) break;
     w.sh->cur.flags |= F_DEC;
     w.mbs_done++;
     w.last_mb = addr + 1 >= w.W * w.H;
     // publish: bottom edge to the ring, full record to `left`, model bytes to the frame (RM)
-    __syncthreads();
+    wave_sync();
     {
       const MbRec& c = w.sh->cur;
       EdgeRec& e = w.ring[w.mb_x];
@@ -937,12 +1040,14 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
         uint8_t* f = w.frames + (size_t)w.cur_frame * w.W * w.H * 52 + ((size_t)w.mb_y * w.W + w.mb_x) * 52;
         if (lane < 52) f[lane] = c.mnnz[lane];
       }
-      __syncthreads();
+      wave_sync();
       uint32_t* l32 = (uint32_t*)&w.sh->left;
       const uint32_t* c32 = (const uint32_t*)&w.sh->cur;
       for (int i = lane; i < (int)sizeof(MbRec) / 4; i += 64) l32[i] = c32[i];
-      __syncthreads();
+      wave_sync();
     }
+    PROF_ENDW(7, t7);
+    if (MODE != MODE_GENERATE) w.publish();
     if (w.terminate(SE_EOS)) break;
     if (MODE == MODE_COMPRESS && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
     addr++;
@@ -951,9 +1056,7 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
 
 // --------------------------------------------------------------------------- kernel bodies
 template <int MODE, bool RM>
-AVR_FI void run_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
-                          avr_slice_result* res) {
-  const int lane = threadIdx.x;
+AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out) {
   w.d = d;
   w.in.g = in + d->payload_offset;
   w.in.limit = MODE == MODE_GENERATE ? 0 : d->read_limit;
@@ -963,60 +1066,186 @@ AVR_FI void run_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_
   w.out.cap = d->out_capacity;
   w.out.n = 0;
   w.out.last = 0;
+  w.fifo_head = 0;
+  w.fifo_room = kFifo;
   if (MODE == MODE_COMPRESS) {
     cd_init(w.cd, w.in);
-    re_init(w.re);
   } else if (MODE == MODE_DECOMPRESS) {
     rd_init(w.rd, w.in);
-    ce_init(w.ce);
   } else {
     ce_init(w.ce);
     w.rng = d->payload_offset * 0x9E3779B97F4A7C15ull + 0x1234567ull + (uint64_t)d->picture_id;
     w.target_mbs = d->payload_size ? (int)d->payload_size : 1 << 30;
   }
+#ifdef AVR_PROFILE
+  for (int i = 0; i < 8; i++) w.prof[i] = 0, w.profb[i] = 0;
+#endif
+}
+
+template <int MODE, bool RM>
+AVR_FI void profile_slice(Walker<MODE, RM>& w) {
+#ifdef AVR_PROFILE
+  w.bins = 0;
+  const uint64_t t0 = PROF_T();
+  const uint32_t t0_b = 0;
   walk_slice(w);
+  PROF_ENDW(0, t0);
+  if (__lane_id() == 0) {
+    for (int i = 0; i < 8; i++) {
+      atomicAdd(&avr_prof[i], (unsigned long long)w.prof[i]);
+      atomicAdd(&avr_prof[8 + i], (unsigned long long)w.profb[i]);
+    }
+  }
+#else
+  walk_slice(w);
+#endif
+}
+
+// The walker wave of a pipelined slice: parse + model, one op per bin into the ring, OP_END at
+// the end whatever happened.  Leaves its status in LDS for finish_slice.
+template <int MODE, bool RM>
+AVR_FI void walker_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
+  begin_slice(w, d, in, nullptr);
+  profile_slice(w);
+  w.push(OP_END);
+  w.publish();
   int status = w.err;
   if (!status && !w.finished) status = -9;
-  if (MODE == MODE_COMPRESS) {
-    if (w.re.err) status = -10;
-    if (!status) {
-      // predicted decompressor output (recode.cpp:1345-1356, 1503-1505): the regenerated CABAC
-      // bytes equal the payload through the stop bit, then zero bits
-      const uint32_t sbi = cd_bitpos(w.cd) - 1;
-      const uint32_t k = sbi >> 3, size = d->payload_size;
-      const uint32_t b = in_byte(w.in, k);
-      const uint32_t masked = b & (0xffu << (7 - (sbi & 7))) & 0xff;
-      int ok;
-      if (masked == 0x80) ok = (k == size) || (k + 1 == size);
-      else ok = (k + 1 == size) || (k + 2 == size && b == masked);
-      if (!ok) status = -11;
-    }
-  } else if (MODE == MODE_DECOMPRESS || MODE == MODE_GENERATE) {
-    if (w.ce.err) status = -10;
+  int stop_ok = 1;
+  if (MODE == MODE_COMPRESS && !status) {
+    // predicted decompressor output (recode.cpp:1345-1356, 1503-1505): the regenerated CABAC
+    // bytes equal the payload through the stop bit, then zero bits
+    const uint32_t sbi = cd_bitpos(w.cd) - 1;
+    const uint32_t k = sbi >> 3, size = d->payload_size;
+    const uint32_t b = in_byte(w.in, k);
+    const uint32_t masked = b & (0xffu << (7 - (sbi & 7))) & 0xff;
+    if (masked == 0x80) stop_ok = (k == size) || (k + 1 == size);
+    else stop_ok = (k + 1 == size) || (k + 2 == size && b == masked);
   }
-  if (out_overflow(w.out)) status = -12;
-  uint32_t len = out_total(w.out);
-  if (MODE == MODE_DECOMPRESS && !status && len && w.out.last == 0x80) len--;  // recode.cpp:1503-1505
+  if (__lane_id() == 0) {
+    w.sh->p_status = status;
+    w.sh->p_stop_ok = stop_ok;
+    res->bins = w.bins;
+    res->mbs = (uint32_t)w.mbs_done;
+  }
+}
+
+AVR_FI uint64_t readlane64(uint64_t v, uint32_t j) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
+  return (uint64_t)hi << 32 | lo;
+}
+
+// The coder wave: retire ops in batches of up to 64 (one ring entry per lane, plus, in compress,
+// that op's reciprocal record gathered by the same lane), then run the serial coder over the
+// batch from registers.  compress: arithmetic_code<uint64_t,uint8_t>::encoder::put / finish
+// (recode.cpp:1074, 1092-1094); decompress: cabac::encoder::put / put_bypass / put_terminate
+// (recode.cpp:1443-1474, cabac_code.h:33-67).
+template <int MODE>
+AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out) {
+  OutStream o;
+  o.g = out + d->out_offset;
+  o.cap = d->out_capacity;
+  o.n = 0;
+  o.last = 0;
+  RecodedEncoder re;
+  CabacEncoder ce;
+  if (MODE == MODE_COMPRESS) re_init(re);
+  else ce_init(ce);
+  const uint32_t lane = __lane_id();
+  uint32_t tail = 0;
+  for (bool done = false; !done;) {
+    uint32_t head;
+    for (;;) {
+      head = *(volatile uint32_t*)&sh->fifo_head;
+      asm volatile("" ::: "memory");
+      if (head != tail) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const uint32_t n = min(head - tail, 64u);
+    const uint32_t op_v = lane < n ? sh->fifo[(tail + lane) & (kFifo - 1)] : 0u;
+    if (MODE == MODE_COMPRESS) {
+      const uint32_t tot_v = (op_v >> 8) & 127;
+      const uint64_t m_v = T->div[tot_v][0];
+      const uint32_t s_v = (uint32_t)T->div[tot_v][1];
+      for (uint32_t j = 0; j < n; j++) {
+        const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
+        if (op & OP_END) { done = true; break; }
+        if (op & OP_FINISH) { re_finish(re, o); continue; }
+        const uint64_t m = readlane64(m_v, j);
+        const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
+        const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
+        re_put(re, o, op & 1, p1);
+      }
+    } else {
+      for (uint32_t j = 0; j < n; j++) {
+        const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
+        if (op & OP_END) { done = true; break; }
+        const int b = op & 1;
+        const uint32_t kind = (op >> 1) & 3;
+        if (kind == OPK_DECISION) ce_decision(ce, o, b, &sh->state[(op >> 3) & 1023], T);
+        else if (kind == OPK_BYPASS) ce_bypass(ce, o, b);
+        else ce_terminate(ce, o, b);
+      }
+    }
+    tail += n;
+    asm volatile("" ::: "memory");
+    *(volatile uint32_t*)&sh->fifo_tail = tail;
+  }
   if (lane == 0) {
-    res->out_len = len;
+    sh->c_err = MODE == MODE_COMPRESS ? re.err : ce.err;
+    sh->c_len = out_total(o);
+    sh->c_last = o.last;
+  }
+}
+
+// Combine the two waves' results (after a workgroup barrier), with run_slice_inline's semantics.
+template <int MODE>
+AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_result* res) {
+  int status = sh->p_status;
+  if (sh->c_err) status = -10;
+  if (MODE == MODE_COMPRESS && !status && !sh->p_stop_ok) status = -11;
+  if (sh->c_len > d->out_capacity) status = -12;
+  uint32_t len = sh->c_len;
+  if (MODE == MODE_DECOMPRESS && !status && len && sh->c_last == 0x80) len--;  // recode.cpp:1503-1505
+  res->out_len = len;
+  res->status = status;
+}
+
+// Single-wave slice (the generator: CABAC encode inline, no coder wave).
+template <int MODE, bool RM>
+AVR_FI void run_slice_inline(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
+                             avr_slice_result* res) {
+  begin_slice(w, d, in, out);
+  profile_slice(w);
+  int status = w.err;
+  if (!status && !w.finished) status = -9;
+  if (w.ce.err) status = -10;
+  if (out_overflow(w.out)) status = -12;
+  if (__lane_id() == 0) {
+    res->out_len = out_total(w.out);
     res->status = status;
     res->bins = w.bins;
     res->mbs = (uint32_t)w.mbs_done;
   }
 }
 
-// Copy the per-bin lookup tables into this workgroup's LDS (16 B per lane per step).
+// Copy the per-bin lookup tables into this workgroup's LDS (16 B per thread per step).
 AVR_FI void load_hot_tables(Shared* sh, const EngineTables* G) {
   const uint4* src = (const uint4*)&G->hot;
   uint4* dst = (uint4*)&sh->tab;
-  for (int i = threadIdx.x; i < (int)(sizeof(HotTables) / 16); i += 64) dst[i] = src[i];
+  for (int i = threadIdx.x; i < (int)(sizeof(HotTables) / 16); i += blockDim.x) dst[i] = src[i];
   __syncthreads();
 }
 
+// Threads per workgroup: two waves (walker + coder) for compress / decompress, one for generate.
 template <int MODE>
-__global__ __launch_bounds__(64) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
-                                                               const uint8_t* in, uint8_t* out, avr_slice_result* res,
-                                                               uint16_t* est_scratch) {
+constexpr int slice_threads() { return MODE == MODE_GENERATE ? 64 : 128; }
+
+template <int MODE>
+__global__ __launch_bounds__(128) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+                                                                const uint8_t* in, uint8_t* out, avr_slice_result* res,
+                                                                uint16_t* est_scratch) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int s = blockIdx.x;
   if (s >= n) return;
@@ -1039,25 +1268,33 @@ __global__ __launch_bounds__(64) void slices_parallel_kernel(const EngineTables*
     }
     return;
   }
-  // fresh model for this slice: clear the dense SIG/NZ estimators (16 B per lane per step)
+  // fresh model for this slice: clear the dense SIG/NZ estimators (16 B per thread per step)
   if (MODE != MODE_GENERATE) {
     uint4* e4 = (uint4*)w.est_g;
-    for (int i = threadIdx.x; i < kEstGlobal / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < kEstGlobal / 8; i += blockDim.x) e4[i] = make_uint4(0, 0, 0, 0);
   }
   w.d = d;
   w.W = d->mb_width;
   init_slice_state(w, G);
-  run_slice(w, d, in, out, &res[s]);
+  if (MODE == MODE_GENERATE) {
+    run_slice_inline(w, d, in, out, &res[s]);
+    return;
+  }
+  if (threadIdx.x < 64) walker_slice(w, d, in, &res[s]);
+  else coder_slice<MODE>(w.sh, w.T, d, out);
+  __syncthreads();
+  if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
 }
 
-// Reference model: one wavefront walks every slice in file order with persistent state.
+// Reference model: one workgroup (walker + coder wave) walks every slice in file order with
+// persistent estimators and frame metadata.
 template <int MODE>
-__global__ __launch_bounds__(64) void slices_sequential_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
-                                                                 const uint8_t* in, uint8_t* out,
-                                                                 avr_slice_result* res, uint16_t* est_g,
-                                                                 uint8_t* frames, int* frame_meta) {
+__global__ __launch_bounds__(128) void slices_sequential_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+                                                                  const uint8_t* in, uint8_t* out,
+                                                                  avr_slice_result* res, uint16_t* est_g,
+                                                                  uint8_t* frames, int* frame_meta) {
   extern __shared__ __align__(16) uint8_t smem[];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, nt = blockDim.x;
   Walker<MODE, true> w;
   w.sh = (Shared*)smem;
   w.ring = (EdgeRec*)(smem + sizeof(Shared));
@@ -1069,9 +1306,9 @@ __global__ __launch_bounds__(64) void slices_sequential_kernel(const EngineTable
   // fresh global model
   {
     uint4* e4 = (uint4*)est_g;
-    for (int i = lane; i < kEstGlobal / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
-    for (int i = lane; i < kEstDefault + 2; i += 64) w.sh->est[i] = 0;
-    for (int i = lane; i < kEcacheSize; i += 64) w.sh->ecache[i] = 0;
+    for (int i = tid; i < kEstGlobal / 8; i += nt) e4[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < kEstDefault + 2; i += nt) w.sh->est[i] = 0;
+    for (int i = tid; i < kEcacheSize; i += nt) w.sh->ecache[i] = 0;
   }
   // frame_meta: [0] cur_frame.  Frame ids / sizes of the two frames, as scalars (no private arrays).
   int cur = 0, fid0 = 0, fid1 = 0, fw0 = 0, fw1 = 0, fh0 = 0, fh1 = 0;
@@ -1088,17 +1325,18 @@ __global__ __launch_bounds__(64) void slices_sequential_kernel(const EngineTable
       const bool reinit_other = (fwn != W || fhn != H) && (fwo != W || fho != H);
       // fresh/cleared current frame; a dimension change also clears the other one
       uint32_t* f32 = (uint32_t*)(frames + (size_t)cur * W * H * 52);
-      for (int i = lane; i < W * H * 13; i += 64) f32[i] = 0;
+      for (int i = tid; i < W * H * 13; i += nt) f32[i] = 0;
       if (reinit_other) {
         uint32_t* o32 = (uint32_t*)(frames + (size_t)(1 - cur) * W * H * 52);
-        for (int i = lane; i < W * H * 13; i += 64) o32[i] = 0;
+        for (int i = tid; i < W * H * 13; i += nt) o32[i] = 0;
         if (cur) { fw0 = W; fh0 = H; } else { fw1 = W; fh1 = H; }
       }
       if (cur) { fw1 = W; fh1 = H; fid1 = d->picture_id; } else { fw0 = W; fh0 = H; fid0 = d->picture_id; }
+      __threadfence_block();
       __syncthreads();
     }
     if (!d->coded) {
-      if (lane == 0) {
+      if (tid == 0) {
         res[s].out_len = 0;
         res[s].status = 1;
         res[s].bins = 0;
@@ -1110,10 +1348,13 @@ __global__ __launch_bounds__(64) void slices_sequential_kernel(const EngineTable
     w.d = d;
     w.W = W;
     init_slice_state(w, G);
-    run_slice(w, d, in, out, &res[s]);
+    if (tid < 64) walker_slice(w, d, in, &res[s]);
+    else coder_slice<MODE>(w.sh, w.T, d, out);
+    __syncthreads();
+    if (tid == 0) finish_slice<MODE>(w.sh, d, &res[s]);
     __syncthreads();
   }
-  if (lane == 0) frame_meta[0] = cur;
+  if (tid == 0) frame_meta[0] = cur;
 }
 
 }  // namespace avr
