@@ -119,6 +119,27 @@ __device__ __forceinline__ void out_repeat(OutStream& o, uint32_t v, uint32_t k)
 __device__ __forceinline__ uint32_t out_total(const OutStream& o) { return o.n; }
 __device__ __forceinline__ bool out_overflow(const OutStream& o) { return o.n > o.cap; }
 
+// ------------------------------------------------------------- CABAC state records in VGPRs
+// HotTables::cabac held in four per-lane registers (lane j: states j and 64 + j); a lookup with
+// a wave-uniform state is two v_readlane, no LDS round trip.
+struct VTab {
+  uint32_t lo0, hi0, lo1, hi1;
+};
+__device__ __forceinline__ void vtab_load(VTab& v, const HotTables* T) {
+  const uint32_t j = __lane_id();
+  const uint64_t a = T->cabac[j], b = T->cabac[64 + j];
+  v.lo0 = (uint32_t)a;
+  v.hi0 = (uint32_t)(a >> 32);
+  v.lo1 = (uint32_t)b;
+  v.hi1 = (uint32_t)(b >> 32);
+}
+__device__ __forceinline__ uint64_t vtab_rec(const VTab& v, uint32_t s) {
+  const uint32_t j = s & 63;
+  const uint32_t lo = s < 64 ? __builtin_amdgcn_readlane(v.lo0, j) : __builtin_amdgcn_readlane(v.lo1, j);
+  const uint32_t hi = s < 64 ? __builtin_amdgcn_readlane(v.hi0, j) : __builtin_amdgcn_readlane(v.hi1, j);
+  return (uint64_t)hi << 32 | lo;
+}
+
 // ---------------------------------------------------------------------- CABAC decoding engine
 // 32-bit form of the 9.3.3.2 engine: low = codIOffset << k | the next k stream bits, k >= 8 at
 // the start of every operation (one operation consumes at most 7 bits), refilled 16 bits at a
@@ -162,6 +183,13 @@ __device__ __forceinline__ int cd_decide(CabacDecoder& d, InStream& in, uint32_t
   d.k -= n;
   cd_refill(d, in);
   return (int)(s & 1) ^ (int)is_lps;
+}
+__device__ __forceinline__ int cd_decision_v(CabacDecoder& d, InStream& in, uint8_t* state, const VTab& v) {
+  const uint32_t s = *state;
+  uint32_t ns;
+  const int b = cd_decide(d, in, s, vtab_rec(v, s), &ns);
+  *state = (uint8_t)ns;
+  return b;
 }
 __device__ __forceinline__ int cd_decision(CabacDecoder& d, InStream& in, uint8_t* state, const HotTables* T) {
   const uint32_t s = *state;
@@ -252,6 +280,12 @@ __device__ __forceinline__ void ce_decision(CabacEncoder& e, OutStream& o, int b
   const uint32_t s = *state;
   uint32_t ns;
   ce_encode(e, o, bin, s, T->cabac[s], &ns);
+  *state = (uint8_t)ns;
+}
+__device__ __forceinline__ void ce_decision_v(CabacEncoder& e, OutStream& o, int bin, uint8_t* state, const VTab& v) {
+  const uint32_t s = *state;
+  uint32_t ns;
+  ce_encode(e, o, bin, s, vtab_rec(v, s), &ns);
   *state = (uint8_t)ns;
 }
 __device__ __forceinline__ void ce_bypass(CabacEncoder& e, OutStream& o, int bin) {

@@ -6,7 +6,7 @@ namespace avr {
 hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
                     uint8_t* out, avr_slice_result* res, uint16_t* est, uint8_t* frames, int* frame_meta,
                     hipStream_t stream) {
-  hipLaunchKernelGGL(slices_sequential_kernel<MODE_COMPRESS>, dim3(1), dim3(128), lds, stream, T, descs, n, in, out, res, est,
+  hipLaunchKernelGGL(slices_sequential_kernel<MODE_COMPRESS>, dim3(1), dim3(slice_threads<MODE_COMPRESS>()), lds, stream, T, descs, n, in, out, res, est,
                      frames, frame_meta);
   return hipGetLastError();
 }

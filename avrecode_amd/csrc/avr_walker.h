@@ -101,9 +101,9 @@ constexpr int kFifo = 512;
 
 struct Shared {
   HotTables tab;          // copy of EngineTables::hot (per-bin lookups stay in LDS)
-  uint32_t fifo[kFifo];   // coding operations, walker wave -> coder wave
-  uint32_t fifo_head;     // operations published by the walker (monotonic)
-  uint32_t fifo_tail;     // operations retired by the coder (monotonic)
+  uint32_t fifo[2][kFifo];   // [0] walker -> next wave, [1] modeler -> coder (compress only)
+  uint32_t fifo_head[2];     // operations published by the ring's producer (monotonic)
+  uint32_t fifo_tail[2];     // operations retired by the ring's consumer (monotonic)
   int32_t p_status, p_stop_ok, c_err;  // slice results of the two waves
   uint32_t c_len, c_last;
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
@@ -118,22 +118,29 @@ struct Shared {
 };
 
 // ---------------------------------------------------------------------------------------
-// Two waves per slice.  Compress and decompress each have two serial chains that only meet in
-// the bin value: the walker wave runs the CABAC parse and the model (compress: CABAC decode +
-// syntax + estimators; decompress: recoded decode + syntax + estimators) and pushes one coding
-// operation per bin into an LDS ring; the coder wave retires them in order (compress: the
-// 64-bit recoded encoder; decompress: the CABAC re-encoder).  The two chains then overlap on the
-// SIMD instead of adding up, and the coder gathers a whole batch's table records with one LDS
-// access per lane.
+// Several waves per slice.  The hot path is a chain of serial recurrences that only meet in the
+// bin value, so each runs on its own wave and they overlap on the SIMD instead of adding up:
+//   compress:   walker (CABAC decode + slice_data parse + model keys)  --ring 0-->
+//               modeler (estimator lookup/update, recode.cpp:816-820, 1030-1047)  --ring 1-->
+//               coder (arithmetic_code<uint64_t,uint8_t> encoder, recode.cpp:1074, 1092-1094)
+//   decompress: walker (recoded decode + model + parse: the parse needs each bin at once)
+//               --ring 0--> coder (cabac::encoder, cabac_code.h:33-67)
+// Consumers retire a ring in batches of up to 64 ops (one entry per lane, plus whatever table
+// record that lane can gather), then run their serial chain over the batch from registers.
 //
-// Compress ops: bit 0 bin, bits 1-7 pos, bits 8-14 pos+neg (the estimator before the update,
-// recode.cpp:816-820); OP_FINISH = arithmetic_code::encoder::finish (terminate = 1).
-// Decompress ops: bit 0 bin, bits 1-2 kind (0 decision, 1 bypass, 2 terminate), bits 3-12 ctxIdx.
-// OP_END closes the slice's stream in both directions.
+// ring 0, compress (model ops): bit 0 bin, bit 1 SIG/NZ estimator (else per-context), bit 2
+//   significance-map threshold 0x50 (else 0x60), bits 3-21 estimator index.
+// ring 1, compress (coder ops): bit 0 bin, bits 1-7 pos, bits 8-14 pos+neg of the estimator
+//   before its update.
+// ring 0, decompress: bit 0 bin, bits 1-2 kind (0 decision, 1 bypass, 2 terminate), bits 3-12
+//   ctxIdx.
+// OP_FINISH = arithmetic_code::encoder::finish (terminate = 1); OP_END closes a slice's stream.
 constexpr uint32_t OP_FINISH = 1u << 30;
 constexpr uint32_t OP_END = 1u << 31;
 enum { OPK_DECISION = 0, OPK_BYPASS = 1, OPK_TERMINATE = 2 };
 
+constexpr uint32_t OPM_CACHE = 2, OPM_THR50 = 4;
+AVR_FI uint32_t op_model(int bin, uint32_t flags, uint32_t idx) { return (uint32_t)bin | flags | idx << 3; }
 AVR_FI uint32_t op_recode(int bin, uint32_t est) {
   const uint32_t pos = (est & 0xff) + 1, tot = pos + (est >> 8) + 1;
   return (uint32_t)bin | pos << 1 | tot << 8;
@@ -156,6 +163,68 @@ AVR_FI void st_volatile(uint32_t* p, uint32_t v) {
 AVR_FI void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+}
+
+// Producer end of ring r: entries go to LDS at once, the head counter every 32 entries (and on
+// demand), the tail is re-read only when the ring looks full.
+struct RingOut {
+  Shared* sh;
+  int r;
+  uint32_t head, room;
+  AVR_FI void init(Shared* s, int ring) {
+    sh = s;
+    r = ring;
+    head = 0;
+    room = kFifo;
+  }
+  AVR_FI void publish() { st_volatile(&sh->fifo_head[r], head); }
+  AVR_FI void push(uint32_t op) {
+    if (room == 0) {
+      publish();
+      for (;;) {
+        const uint32_t used = head - ld_volatile(&sh->fifo_tail[r]);
+        if (used < (uint32_t)kFifo) { room = kFifo - used; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    sh->fifo[r][head & (kFifo - 1)] = op;
+    head++;
+    room--;
+    if ((head & 31) == 0) publish();
+  }
+};
+// Consumer end: wait for a batch, load it one entry per lane.  Returns the batch size.
+AVR_FI uint32_t ring_take(Shared* sh, int r, uint32_t tail, uint32_t* op_v) {
+  uint32_t head;
+  for (;;) {
+    head = ld_volatile(&sh->fifo_head[r]);
+    if (head != tail) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  const uint32_t n = min(head - tail, 64u);
+  const uint32_t lane = __lane_id();
+  *op_v = lane < n ? sh->fifo[r][(tail + lane) & (kFifo - 1)] : 0u;
+  return n;
+}
+AVR_FI void ring_retire(Shared* sh, int r, uint32_t tail) { st_volatile(&sh->fifo_tail[r], tail); }
+
+// SIG / NZ estimators: LDS write-back cache over the dense HBM table (see kEcacheBits).
+AVR_FI uint32_t ec_hash(uint32_t tag) { return (tag * 0x9E3779B1u) >> (32 - kEcacheBits); }
+AVR_FI uint32_t est_load(Shared* sh, uint16_t* est_g, uint32_t idx, uint32_t* slot) {
+  const uint32_t tag = idx >> kEcacheBits;
+  const uint32_t set = (idx ^ ec_hash(tag)) & (kEcacheSize - 1);
+  *slot = set;
+  const uint32_t ent = sh->ecache[set];
+  if ((ent >> 16) == tag + 1) return ent & 0xffff;
+  if (ent) {  // evict: write the old estimator back
+    const uint32_t otag = (ent >> 16) - 1;
+    const uint32_t oidx = otag << kEcacheBits | ((set ^ ec_hash(otag)) & (kEcacheSize - 1));
+    if (__lane_id() == 0) est_g[oidx] = (uint16_t)ent;
+  }
+  return est_g[idx];
+}
+AVR_FI void est_store(Shared* sh, uint32_t idx, uint32_t slot, uint32_t e) {
+  sh->ecache[slot] = ((idx >> kEcacheBits) + 1) << 16 | e;
 }
 
 template <int MODE, bool RM>
@@ -183,24 +252,11 @@ struct Walker {
   uint32_t bins;
   int target_mbs, mbs_done, last_mb;
   int nref0, nref1, d8x8inf, x264_build, first_mb;
-  uint32_t fifo_head, fifo_room;   // ops pushed; ops that fit before the next tail check
+  RingOut ring0;          // walker -> modeler (compress) / coder (decompress)
+  VTab vt;                // CABAC state records (compress: decoder side)
 
-  // ------------------------------------------------------------------ walker -> coder ring
-  AVR_FI void publish() { st_volatile(&sh->fifo_head, fifo_head); }
-  AVR_FI void push(uint32_t op) {
-    if (fifo_room == 0) {
-      publish();
-      for (;;) {
-        const uint32_t used = fifo_head - ld_volatile(&sh->fifo_tail);
-        if (used < (uint32_t)kFifo) { fifo_room = kFifo - used; break; }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    sh->fifo[fifo_head & (kFifo - 1)] = op;
-    fifo_head++;
-    fifo_room--;
-    if ((fifo_head & 31) == 0) publish();
-  }
+  AVR_FI void publish() { ring0.publish(); }
+  AVR_FI void push(uint32_t op) { ring0.push(op); }
 #ifdef AVR_PROFILE
   uint64_t prof[8];
   uint32_t profb[8];
@@ -210,13 +266,8 @@ struct Walker {
   AVR_FI int bin(int se, int k, int ctx) {
     bins++;
     if (MODE == MODE_COMPRESS) {
-      // both reads first (no store in between), then the dependent state record
-      const uint32_t e = sh->est[ctx], s = sh->state[ctx];
-      uint32_t ns;
-      const int b = cd_decide(cd, in, s, T->cabac[s], &ns);
-      sh->state[ctx] = (uint8_t)ns;
-      sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
-      push(op_recode(b, e));
+      const int b = cd_decision_v(cd, in, &sh->state[ctx], vt);
+      push(op_model(b, 0, ctx));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[ctx];
@@ -233,10 +284,8 @@ struct Walker {
   AVR_FI int bypass(int se, int k) {
     bins++;
     if (MODE == MODE_COMPRESS) {
-      const uint32_t e = sh->est[1024];
       const int b = cd_bypass(cd, in);
-      sh->est[1024] = (uint16_t)est_update(e, b, 0x60);
-      push(op_recode(b, e));
+      push(op_model(b, 0, 1024));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1024];
@@ -254,10 +303,8 @@ struct Walker {
     bins++;
     int b;
     if (MODE == MODE_COMPRESS) {
-      const uint32_t e = sh->est[1025];
       b = cd_terminate(cd, in);
-      sh->est[1025] = (uint16_t)est_update(e, b, 0x60);
-      push(op_recode(b, e));
+      push(op_model(b, 0, 1025));
       if (b) push(OP_FINISH);
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1025];
@@ -334,25 +381,6 @@ struct Walker {
     return 0;
   }
 
-  // ------------------------------------------------------------------ SIG / NZ estimators
-  AVR_FI static uint32_t ec_hash(uint32_t tag) { return (tag * 0x9E3779B1u) >> (32 - kEcacheBits); }
-  AVR_FI uint32_t est_load(int idx, uint32_t* slot) {
-    const uint32_t tag = (uint32_t)idx >> kEcacheBits;
-    const uint32_t set = ((uint32_t)idx ^ ec_hash(tag)) & (kEcacheSize - 1);
-    *slot = set;
-    const uint32_t ent = sh->ecache[set];
-    if ((ent >> 16) == tag + 1) return ent & 0xffff;
-    if (ent) {  // evict: write the old estimator back
-      const uint32_t otag = (ent >> 16) - 1;
-      const uint32_t oidx = otag << kEcacheBits | ((set ^ ec_hash(otag)) & (kEcacheSize - 1));
-      if (__lane_id() == 0) est_g[oidx] = (uint16_t)ent;
-    }
-    return est_g[idx];
-  }
-  AVR_FI void est_store(int idx, uint32_t slot, uint32_t e) {
-    sh->ecache[slot] = (((uint32_t)idx >> kEcacheBits) + 1) << 16 | e;
-  }
-
   // finished_queueing (recode.cpp:845-930): the 2/4/6 nnz bits, LSB first
   AVR_FI int nz_bits(int cat, int n, int max, int is_dc, int c422, int count) {
     const int bits = max > 16 ? 6 : max > 4 ? 4 : 2;
@@ -380,16 +408,16 @@ struct Walker {
       const int ab = av ? (av >= cur_bit) : 2;
       const int pb = pv >= cur_bit;
       const int idx = kSigEst + (((((cur_bit - 1 + so_far) * 2 + pb) * 3 + lb) * 3 + ab) * 57 + t);
-      uint32_t slot;
-      uint32_t e = est_load(idx, &slot);
       int b;
       if (MODE == MODE_COMPRESS) {
         b = (count >> i) & 1;
-        push(op_recode(b, e));
+        push(op_model(b, OPM_CACHE, idx));
       } else {
+        uint32_t slot;
+        const uint32_t e = est_load(sh, est_g, idx, &slot);
         b = rd_get(rd, in, rc_p1(rd.range, e, T));
+        est_store(sh, idx, slot, est_update(e, b, 0x60));
       }
-      est_store(idx, slot, est_update(e, b, 0x60));
       if (b) so_far |= cur_bit;
     }
     return so_far;
@@ -412,19 +440,21 @@ struct Walker {
       uint64_t sigmask = 0;
       int pos, end = max - 2;
       PROF_BEGIN(t3);
+      asm volatile("; MARK_MAP_BEGIN");
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
         if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
         bins++;
-        if (cd_decision(cd, in, &sh->state[sb + sc], T)) {
+        if (cd_decision_v(cd, in, &sh->state[sb + sc], vt)) {
           sigmask |= 1ull << pos;
           cnt++;
           bins++;
-          if (cd_decision(cd, in, &sh->state[lb + lc], T)) { end = pos; break; }
+          if (cd_decision_v(cd, in, &sh->state[lb + lc], vt)) { end = pos; break; }
         }
       }
+      asm volatile("; MARK_MAP_END");
       if (pos == max - 1) cnt++;
       PROF_END(3, t3);
       // model: nnz first (recode.cpp:1208-1221), then the buffered map (1244-1255)
@@ -437,10 +467,7 @@ struct Walker {
       for (int zz = 0; zz <= end; zz++) {
         int b = (int)((sigmask >> zz) & 1);
         int idx = sig_est_index(cat, max, is_dc, c422, zz, nnz_m, obs);
-        uint32_t slot;
-        uint32_t e = est_load(idx, &slot);
-        push(op_recode(b, e));
-        est_store(idx, slot, est_update(e, b, 0x50));
+        push(op_model(b, OPM_CACHE | OPM_THR50, idx));
         obs += b;
       }
       PROF_END(5, t5);
@@ -454,9 +481,9 @@ struct Walker {
         else sc = lc = pos;
         int idx = sig_est_index(cat, max, is_dc, c422, pos, nnz_m, cnt);
         uint32_t slot;
-        uint32_t e = est_load(idx, &slot);
+        uint32_t e = est_load(sh, est_g, idx, &slot);
         int b = rd_get(rd, in, rc_p1(rd.range, e, T));
-        est_store(idx, slot, est_update(e, b, 0x50));
+        est_store(sh, idx, slot, est_update(e, b, 0x50));
         bins++;
         push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3);
         if (b) {
@@ -964,9 +991,9 @@ AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
   }
   uint32_t* ring32 = (uint32_t*)w.ring;
   for (int i = lane; i < w.W * (int)sizeof(EdgeRec) / 4; i += nt) ring32[i] = 0;
-  if (lane == 0) {
-    w.sh->fifo_head = 0;
-    w.sh->fifo_tail = 0;
+  if (lane < 2) {
+    w.sh->fifo_head[lane] = 0;
+    w.sh->fifo_tail[lane] = 0;
   }
   __syncthreads();
 }
@@ -1066,8 +1093,8 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   w.out.cap = d->out_capacity;
   w.out.n = 0;
   w.out.last = 0;
-  w.fifo_head = 0;
-  w.fifo_room = kFifo;
+  w.ring0.init(w.sh, 0);
+  if (MODE == MODE_COMPRESS) vtab_load(w.vt, w.T);
   if (MODE == MODE_COMPRESS) {
     cd_init(w.cd, w.in);
   } else if (MODE == MODE_DECOMPRESS) {
@@ -1136,11 +1163,46 @@ AVR_FI uint64_t readlane64(uint64_t v, uint32_t j) {
   return (uint64_t)hi << 32 | lo;
 }
 
-// The coder wave: retire ops in batches of up to 64 (one ring entry per lane, plus, in compress,
-// that op's reciprocal record gathered by the same lane), then run the serial coder over the
-// batch from registers.  compress: arithmetic_code<uint64_t,uint8_t>::encoder::put / finish
-// (recode.cpp:1074, 1092-1094); decompress: cabac::encoder::put / put_bypass / put_terminate
-// (recode.cpp:1443-1474, cabac_code.h:33-67).
+// The modeler wave (compress): the estimator recurrences.  Per-context estimators live in LDS
+// (Shared::est), the SIG/NZ ones in the LDS cache over HBM; each op's estimator before the update
+// goes to the coder as (pos, pos + neg).
+AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
+  RingOut out;
+  out.init(sh, 1);
+  uint32_t tail = 0;
+  for (bool done = false; !done;) {
+    uint32_t op_v;
+    const uint32_t n = ring_take(sh, 0, tail, &op_v);
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
+      if (op & (OP_END | OP_FINISH)) {
+        out.push(op);
+        if (op & OP_END) { done = true; break; }
+        continue;
+      }
+      const int b = op & 1;
+      const uint32_t idx = (op >> 3) & 0x7ffff;
+      uint32_t e;
+      if (op & OPM_CACHE) {
+        uint32_t slot;
+        e = est_load(sh, est_g, idx, &slot);
+        est_store(sh, idx, slot, est_update(e, b, (op & OPM_THR50) ? 0x50 : 0x60));
+      } else {
+        e = sh->est[idx];
+        sh->est[idx] = (uint16_t)est_update(e, b, 0x60);
+      }
+      out.push(op_recode(b, e));
+    }
+    tail += n;
+    ring_retire(sh, 0, tail);
+    out.publish();
+  }
+}
+
+// The coder wave: compress retires ring 1 (arithmetic_code<uint64_t,uint8_t>::encoder::put /
+// finish, recode.cpp:1074, 1092-1094), gathering each op's reciprocal record with its lane;
+// decompress retires ring 0 (cabac::encoder::put / put_bypass / put_terminate,
+// recode.cpp:1443-1474, cabac_code.h:33-67).
 template <int MODE>
 AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out) {
   OutStream o;
@@ -1150,20 +1212,17 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
   o.last = 0;
   RecodedEncoder re;
   CabacEncoder ce;
+  VTab vt;
   if (MODE == MODE_COMPRESS) re_init(re);
-  else ce_init(ce);
-  const uint32_t lane = __lane_id();
+  else {
+    ce_init(ce);
+    vtab_load(vt, T);
+  }
+  const int r = MODE == MODE_COMPRESS ? 1 : 0;
   uint32_t tail = 0;
   for (bool done = false; !done;) {
-    uint32_t head;
-    for (;;) {
-      head = *(volatile uint32_t*)&sh->fifo_head;
-      asm volatile("" ::: "memory");
-      if (head != tail) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const uint32_t n = min(head - tail, 64u);
-    const uint32_t op_v = lane < n ? sh->fifo[(tail + lane) & (kFifo - 1)] : 0u;
+    uint32_t op_v;
+    const uint32_t n = ring_take(sh, r, tail, &op_v);
     if (MODE == MODE_COMPRESS) {
       const uint32_t tot_v = (op_v >> 8) & 127;
       const uint64_t m_v = T->div[tot_v][0];
@@ -1183,16 +1242,15 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
         if (op & OP_END) { done = true; break; }
         const int b = op & 1;
         const uint32_t kind = (op >> 1) & 3;
-        if (kind == OPK_DECISION) ce_decision(ce, o, b, &sh->state[(op >> 3) & 1023], T);
+        if (kind == OPK_DECISION) ce_decision_v(ce, o, b, &sh->state[(op >> 3) & 1023], vt);
         else if (kind == OPK_BYPASS) ce_bypass(ce, o, b);
         else ce_terminate(ce, o, b);
       }
     }
     tail += n;
-    asm volatile("" ::: "memory");
-    *(volatile uint32_t*)&sh->fifo_tail = tail;
+    ring_retire(sh, r, tail);
   }
-  if (lane == 0) {
+  if (__lane_id() == 0) {
     sh->c_err = MODE == MODE_COMPRESS ? re.err : ce.err;
     sh->c_len = out_total(o);
     sh->c_last = o.last;
@@ -1240,10 +1298,10 @@ AVR_FI void load_hot_tables(Shared* sh, const EngineTables* G) {
 
 // Threads per workgroup: two waves (walker + coder) for compress / decompress, one for generate.
 template <int MODE>
-constexpr int slice_threads() { return MODE == MODE_GENERATE ? 64 : 128; }
+constexpr int slice_threads() { return MODE == MODE_GENERATE ? 64 : MODE == MODE_COMPRESS ? 192 : 128; }
 
 template <int MODE>
-__global__ __launch_bounds__(128) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+__global__ __launch_bounds__(192, 3) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                 const uint8_t* in, uint8_t* out, avr_slice_result* res,
                                                                 uint16_t* est_scratch) {
   extern __shared__ __align__(16) uint8_t smem[];
@@ -1280,7 +1338,9 @@ __global__ __launch_bounds__(128) void slices_parallel_kernel(const EngineTables
     run_slice_inline(w, d, in, out, &res[s]);
     return;
   }
-  if (threadIdx.x < 64) walker_slice(w, d, in, &res[s]);
+  const int wave = threadIdx.x >> 6;
+  if (wave == 0) walker_slice(w, d, in, &res[s]);
+  else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
   else coder_slice<MODE>(w.sh, w.T, d, out);
   __syncthreads();
   if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
@@ -1289,7 +1349,7 @@ __global__ __launch_bounds__(128) void slices_parallel_kernel(const EngineTables
 // Reference model: one workgroup (walker + coder wave) walks every slice in file order with
 // persistent estimators and frame metadata.
 template <int MODE>
-__global__ __launch_bounds__(128) void slices_sequential_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+__global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                   const uint8_t* in, uint8_t* out,
                                                                   avr_slice_result* res, uint16_t* est_g,
                                                                   uint8_t* frames, int* frame_meta) {
@@ -1348,7 +1408,9 @@ __global__ __launch_bounds__(128) void slices_sequential_kernel(const EngineTabl
     w.d = d;
     w.W = W;
     init_slice_state(w, G);
-    if (tid < 64) walker_slice(w, d, in, &res[s]);
+    const int wave = tid >> 6;
+    if (wave == 0) walker_slice(w, d, in, &res[s]);
+    else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
     else coder_slice<MODE>(w.sh, w.T, d, out);
     __syncthreads();
     if (tid == 0) finish_slice<MODE>(w.sh, d, &res[s]);
