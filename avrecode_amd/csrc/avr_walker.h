@@ -253,7 +253,70 @@ struct Walker {
   int target_mbs, mbs_done, last_mb;
   int nref0, nref1, d8x8inf, x264_build, first_mb;
   RingOut ring0;          // walker -> modeler (compress) / coder (decompress)
-  VTab vt;                // CABAC state records (compress: decoder side)
+  VTab vt;                // CABAC state records (compress / generate: the walker's engine)
+
+  // ------------------------------------------------------------------ residual context registers
+  // The residual contexts of one ctxBlockCat (significant_coeff_flag lanes 0-15,
+  // last_significant lanes 16-31, coeff_abs_level_minus1 lanes 32-41) live in one VGPR, lane j
+  // holding the walker's per-context value for ctx rc_addr(j): the CABAC state byte (compress,
+  // generate) or the estimator (decompress).  A residual bin then costs a v_readlane /
+  // v_writelane instead of an LDS round trip.  Switching category writes the lanes back.
+  uint32_t rc_v;
+  int rc_cat;
+  AVR_FI static uint32_t wlane(uint32_t v, uint32_t L, uint32_t x) { return __lane_id() == L ? x : v; }
+  AVR_FI int rc_addr(int cat, uint32_t j) const {
+    return j < 16 ? T->sig_base[cat] + (int)j : j < 32 ? T->last_base[cat] + (int)j - 16
+         : j < 42 ? T->abs_base[cat] + (int)j - 32 : -1;
+  }
+  AVR_FI void rc_writeback() {
+    if (rc_cat < 0) return;
+    const int a = rc_addr(rc_cat, __lane_id());
+    if (a >= 0) {
+      if (MODE == MODE_DECOMPRESS) sh->est[a] = (uint16_t)rc_v;
+      else sh->state[a] = (uint8_t)rc_v;
+    }
+    wave_sync();
+    rc_cat = -1;
+  }
+  AVR_FI void rc_select(int cat) {
+    if (cat == rc_cat) return;
+    rc_writeback();
+    const int a = rc_addr(cat, __lane_id());
+    rc_v = a < 0 ? 0u : MODE == MODE_DECOMPRESS ? (uint32_t)sh->est[a] : (uint32_t)sh->state[a];
+    rc_cat = cat;
+  }
+  // compress: one CABAC decision on cached context lane L (no op pushed)
+  AVR_FI int rdecide(uint32_t L) {
+    bins++;
+    const uint32_t s = __builtin_amdgcn_readlane(rc_v, L);
+    uint32_t ns;
+    const int b = cd_decide(cd, in, s, vtab_rec(vt, s), &ns);
+    rc_v = wlane(rc_v, L, ns);
+    return b;
+  }
+  // a residual bin through the model on cached lane L; ctx = rc_addr(rc_cat, L)
+  AVR_FI int rbin(uint32_t L, int ctx) {
+    if (MODE == MODE_COMPRESS) {
+      const int b = rdecide(L);
+      push(op_model(b, 0, ctx));
+      return b;
+    } else if (MODE == MODE_DECOMPRESS) {
+      bins++;
+      const uint32_t e = __builtin_amdgcn_readlane(rc_v, L);
+      const int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      rc_v = wlane(rc_v, L, est_update(e, b, 0x60));
+      push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
+      return b;
+    } else {
+      bins++;
+      const uint32_t s = __builtin_amdgcn_readlane(rc_v, L);
+      const int b = rnd() < sh->gen_p[ctx];
+      uint32_t ns;
+      ce_encode(ce, out, b, s, vtab_rec(vt, s), &ns);
+      rc_v = wlane(rc_v, L, ns);
+      return b;
+    }
+  }
 
   AVR_FI void publish() { ring0.publish(); }
   AVR_FI void push(uint32_t op) { ring0.push(op); }
@@ -440,21 +503,17 @@ struct Walker {
       uint64_t sigmask = 0;
       int pos, end = max - 2;
       PROF_BEGIN(t3);
-      asm volatile("; MARK_MAP_BEGIN");
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
         if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
-        bins++;
-        if (cd_decision_v(cd, in, &sh->state[sb + sc], vt)) {
+        if (rdecide(sc)) {
           sigmask |= 1ull << pos;
           cnt++;
-          bins++;
-          if (cd_decision_v(cd, in, &sh->state[lb + lc], vt)) { end = pos; break; }
+          if (rdecide(16 + lc)) { end = pos; break; }
         }
       }
-      asm volatile("; MARK_MAP_END");
       if (pos == max - 1) cnt++;
       PROF_END(3, t3);
       // model: nnz first (recode.cpp:1208-1221), then the buffered map (1244-1255)
@@ -502,9 +561,9 @@ struct Walker {
         if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
-        if (bin(SE_OTHER, 0, sb + sc)) {
+        if (rbin(sc, sb + sc)) {
           cnt++;
-          if (bin(SE_OTHER, 0, lb + lc)) break;
+          if (rbin(16 + lc, lb + lc)) break;
         }
       }
       if (pos == max - 1) cnt++;
@@ -531,6 +590,7 @@ struct Walker {
     }
     int cnt = 0;
     if (coded) {
+      rc_select(cat);
       cnt = sig_map(cat, n, max, is_dc, c422);
       // coeff_abs_level_minus1 + sign, reverse scan order
       const int ab = T->abs_base[cat];
@@ -538,14 +598,13 @@ struct Walker {
       PROF_BEGIN(t6);
       for (int i = cnt - 1; i >= 0 && !err; i--) {
         int absl;
-        if (!bin(SE_OTHER, 0, ab + (gt1 ? 0 : min(4, 1 + eq1)))) {
+        const int i0 = gt1 ? 0 : min(4, 1 + eq1);
+        if (!rbin(32 + i0, ab + i0)) {
           absl = 1;
         } else {
-          const int c1 = ab + 5 + min(4 - (cat == 3), gt1);
+          const int i1 = 5 + min(4 - (cat == 3), gt1);
           absl = 2;
-          asm volatile("; MARK_LEVEL_BEGIN");
-          while (absl < 15 && bin(SE_OTHER, 0, c1)) absl++;
-          asm volatile("; MARK_LEVEL_END");
+          while (absl < 15 && rbin(32 + i1, ab + i1)) absl++;
           if (absl >= 15) {
             int k = 0;
             while (bypass(SE_LEVEL_SUFFIX, k)) {
@@ -1094,7 +1153,9 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   w.out.n = 0;
   w.out.last = 0;
   w.ring0.init(w.sh, 0);
-  if (MODE == MODE_COMPRESS) vtab_load(w.vt, w.T);
+  vtab_load(w.vt, w.T);
+  w.rc_cat = -1;
+  w.rc_v = 0;
   if (MODE == MODE_COMPRESS) {
     cd_init(w.cd, w.in);
   } else if (MODE == MODE_DECOMPRESS) {
@@ -1134,6 +1195,7 @@ template <int MODE, bool RM>
 AVR_FI void walker_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
   begin_slice(w, d, in, nullptr);
   profile_slice(w);
+  w.rc_writeback();  // estimators persist across slices in the reference model
   w.push(OP_END);
   w.publish();
   int status = w.err;
@@ -1276,6 +1338,7 @@ AVR_FI void run_slice_inline(Walker<MODE, RM>& w, const avr_slice_desc* d, const
                              avr_slice_result* res) {
   begin_slice(w, d, in, out);
   profile_slice(w);
+  w.rc_writeback();
   int status = w.err;
   if (!status && !w.finished) status = -9;
   if (w.ce.err) status = -10;
