@@ -796,7 +796,7 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
 
 }  // extern "C"
 
-// Debug only (not part of include/avrecode.h): section cycle counters of an AVR_PROFILE build of
+// Debug only (not part of include/avrecode.h): section cycle counters (32 slots) of an AVR_PROFILE build of
 // the parallel kernels (mode 0 compress, 1 decompress, 2 generate), read and cleared.
 extern "C" int avr_debug_profile(int mode, unsigned long long* out16) {
   hipError_t e = mode == 0 ? avr::profile_parallel_compress(out16)

@@ -120,24 +120,43 @@ __device__ __forceinline__ uint32_t out_total(const OutStream& o) { return o.n; 
 __device__ __forceinline__ bool out_overflow(const OutStream& o) { return o.n > o.cap; }
 
 // ------------------------------------------------------------- CABAC state records in VGPRs
-// HotTables::cabac held in four per-lane registers (lane j: states j and 64 + j); a lookup with
-// a wave-uniform state is two v_readlane, no LDS round trip.
+// Per pStateIdx p (state byte s = 2p + valMPS): the four LPS ranges (byte q for
+// q = (range >> 6) & 3) and transIdxLPS[p].  Successor states follow arithmetically:
+// MPS -> s + 2 while p < 62; LPS -> 2 transIdxLPS[p] + (valMPS ^ (p == 0)).
+struct CabacRec {
+  uint32_t lps4, tlps;
+};
+__device__ __forceinline__ CabacRec rec_of(uint64_t packed) {  // from HotTables::cabac[s]
+  CabacRec r;
+  r.lps4 = (uint32_t)packed;
+  r.tlps = (uint32_t)(packed >> 41) & 63;
+  return r;
+}
+// The table in two VGPRs (lane p); a lookup with a wave-uniform state is two independent
+// v_readlane, no LDS round trip and no branch.
 struct VTab {
-  uint32_t lo0, hi0, lo1, hi1;
+  uint32_t lps4, tlps;
 };
 __device__ __forceinline__ void vtab_load(VTab& v, const HotTables* T) {
-  const uint32_t j = __lane_id();
-  const uint64_t a = T->cabac[j], b = T->cabac[64 + j];
-  v.lo0 = (uint32_t)a;
-  v.hi0 = (uint32_t)(a >> 32);
-  v.lo1 = (uint32_t)b;
-  v.hi1 = (uint32_t)(b >> 32);
+  const CabacRec r = rec_of(T->cabac[2 * __lane_id()]);
+  v.lps4 = r.lps4;
+  v.tlps = r.tlps;
 }
-__device__ __forceinline__ uint64_t vtab_rec(const VTab& v, uint32_t s) {
-  const uint32_t j = s & 63;
-  const uint32_t lo = s < 64 ? __builtin_amdgcn_readlane(v.lo0, j) : __builtin_amdgcn_readlane(v.lo1, j);
-  const uint32_t hi = s < 64 ? __builtin_amdgcn_readlane(v.hi0, j) : __builtin_amdgcn_readlane(v.hi1, j);
-  return (uint64_t)hi << 32 | lo;
+__device__ __forceinline__ CabacRec vtab_rec(const VTab& v, uint32_t s) {
+  CabacRec r;
+  r.lps4 = __builtin_amdgcn_readlane(v.lps4, s >> 1);
+  r.tlps = __builtin_amdgcn_readlane(v.tlps, s >> 1);
+  return r;
+}
+// Shared by the decoder and the encoder: the LPS range for the current range and the successor
+// state for either outcome; is_lps is 0 or 1 and selects through masks, not booleans (a boolean
+// turned back into an integer costs a vector select and a scalar<->vector round trip).
+__device__ __forceinline__ uint32_t cabac_lps(uint32_t range, CabacRec r) { return (r.lps4 >> ((range >> 3) & 0x18)) & 0xff; }
+__device__ __forceinline__ uint32_t cabac_next(uint32_t s, CabacRec r, uint32_t is_lps) {
+  const uint32_t p = s >> 1;
+  const uint32_t ns_mps = s + (p < 62 ? 2u : 0u);
+  const uint32_t ns_lps = (r.tlps << 1) | ((s & 1) ^ (p == 0 ? 1u : 0u));
+  return ns_mps ^ ((ns_lps ^ ns_mps) & (0u - is_lps));
 }
 
 // ---------------------------------------------------------------------- CABAC decoding engine
@@ -168,21 +187,23 @@ __device__ __forceinline__ void cd_init(CabacDecoder& d, InStream& in) {  // 9.3
 __device__ __forceinline__ uint32_t cd_bitpos(const CabacDecoder& d) { return 8u * d.next - (uint32_t)d.k; }
 
 // One decision given the context's state byte s (2*pStateIdx + valMPS, FFmpeg's cabac_state
-// layout) and rec = HotTables::cabac[s]; *ns receives the successor state.  No memory access, so
-// the caller can issue the state / record reads of the model side at the same time.
-__device__ __forceinline__ int cd_decide(CabacDecoder& d, InStream& in, uint32_t s, uint64_t rec, uint32_t* ns) {
-  const uint32_t lps = (uint32_t)(rec >> ((d.range >> 3) & 0x18)) & 0xff;
+// layout) and its record; *ns receives the successor state.  No memory access, so the caller can
+// issue the context read of the model side at the same time.
+__device__ __forceinline__ int cd_decide(CabacDecoder& d, InStream& in, uint32_t s, CabacRec r, uint32_t* ns) {
+  const uint32_t lps = cabac_lps(d.range, r);
   const uint32_t rmps = d.range - lps;
   const uint32_t scaled = rmps << d.k;
-  const bool is_lps = d.low >= scaled;
-  d.low -= is_lps ? scaled : 0;
-  d.range = is_lps ? lps : rmps;
-  *ns = (uint32_t)(rec >> (is_lps ? 40 : 32)) & 0xff;
+  // low >= scaled  <=>  no borrow out of the 64-bit difference (scalar sub + subb)
+  const uint32_t is_lps = ~(uint32_t)(((uint64_t)d.low - scaled) >> 32) & 1u;
+  const uint32_t m = 0u - is_lps;
+  d.low -= scaled & m;
+  d.range = rmps ^ ((lps ^ rmps) & m);
+  *ns = cabac_next(s, r, is_lps);
   const int n = __clz(d.range) - 23;
   d.range <<= n;
   d.k -= n;
   cd_refill(d, in);
-  return (int)(s & 1) ^ (int)is_lps;
+  return (int)((s & 1) ^ is_lps);
 }
 __device__ __forceinline__ int cd_decision_v(CabacDecoder& d, InStream& in, uint8_t* state, const VTab& v) {
   const uint32_t s = *state;
@@ -194,7 +215,7 @@ __device__ __forceinline__ int cd_decision_v(CabacDecoder& d, InStream& in, uint
 __device__ __forceinline__ int cd_decision(CabacDecoder& d, InStream& in, uint8_t* state, const HotTables* T) {
   const uint32_t s = *state;
   uint32_t ns;
-  const int b = cd_decide(d, in, s, T->cabac[s], &ns);
+  const int b = cd_decide(d, in, s, rec_of(T->cabac[s]), &ns);
   *state = (uint8_t)ns;
   return b;
 }
@@ -261,14 +282,14 @@ __device__ __forceinline__ void ce_putbyte1(CabacEncoder& e, OutStream& o) {
     e.have_cache = 1;
   }
 }
-__device__ __forceinline__ void ce_encode(CabacEncoder& e, OutStream& o, int bin, uint32_t s, uint64_t rec,
-                                          uint32_t* ns) {
-  const uint32_t lps = (uint32_t)(rec >> ((e.range >> 3) & 0x18)) & 0xff;
+__device__ __forceinline__ void ce_encode(CabacEncoder& e, OutStream& o, int bin, uint32_t s, CabacRec r, uint32_t* ns) {
+  const uint32_t lps = cabac_lps(e.range, r);
   const uint32_t rmps = e.range - lps;
-  const bool is_lps = bin != (int)(s & 1);
-  e.low += is_lps ? rmps : 0;
-  e.range = is_lps ? lps : rmps;
-  *ns = (uint32_t)(rec >> (is_lps ? 40 : 32)) & 0xff;
+  const uint32_t is_lps = ((uint32_t)bin ^ s) & 1u;
+  const uint32_t m = 0u - is_lps;
+  e.low += rmps & m;
+  e.range = rmps ^ ((lps ^ rmps) & m);
+  *ns = cabac_next(s, r, is_lps);
   const int n = __clz(e.range) - 23;   // <= 6: at most one byte per decision
   e.range <<= n;
   e.low <<= n;
@@ -279,7 +300,7 @@ __device__ __forceinline__ void ce_decision(CabacEncoder& e, OutStream& o, int b
                                             const HotTables* T) {
   const uint32_t s = *state;
   uint32_t ns;
-  ce_encode(e, o, bin, s, T->cabac[s], &ns);
+  ce_encode(e, o, bin, s, rec_of(T->cabac[s]), &ns);
   *state = (uint8_t)ns;
 }
 __device__ __forceinline__ void ce_decision_v(CabacEncoder& e, OutStream& o, int bin, uint8_t* state, const VTab& v) {

@@ -45,7 +45,7 @@
 namespace avr {
 
 #ifdef AVR_PROFILE
-static __device__ unsigned long long avr_prof[16];
+static __device__ unsigned long long avr_prof[32];
 #endif
 
 enum { MODE_COMPRESS = 0, MODE_DECOMPRESS = 1, MODE_GENERATE = 2 };
@@ -149,14 +149,18 @@ AVR_FI uint32_t op_recode(int bin, uint32_t est) {
 // in program order, so a counter store issued after the entry stores cannot be seen before them;
 // the asm statements only keep the compiler from reordering (an acquire/release fence would
 // also wait for, or write back, this wave's outstanding global stores).
+// The casts to address space 3 matter: a volatile access through a generic pointer stays a
+// flat access with cache-bypass bits and a vmcnt(0) wait (the address-space inference pass does
+// not rewrite volatile accesses), which costs a global-memory round trip per counter update.
+typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
 AVR_FI uint32_t ld_volatile(const uint32_t* p) {
-  const uint32_t v = *(const volatile uint32_t*)p;
+  const uint32_t v = *(lds_vu32*)p;
   asm volatile("" ::: "memory");
-  return v;
+  return __builtin_amdgcn_readfirstlane(v);
 }
 AVR_FI void st_volatile(uint32_t* p, uint32_t v) {
   asm volatile("" ::: "memory");
-  *(volatile uint32_t*)p = v;
+  *(lds_vu32*)p = v;
 }
 // LDS hand-offs between the lanes of ONE wave need no barrier (a wave's LDS operations execute in
 // order); only the compiler must not move memory operations across the hand-off.
@@ -178,14 +182,23 @@ struct RingOut {
     room = kFifo;
   }
   AVR_FI void publish() { st_volatile(&sh->fifo_head[r], head); }
+#ifdef AVR_PROFILE
+  uint64_t wait_cycles = 0;
+#endif
   AVR_FI void push(uint32_t op) {
     if (room == 0) {
       publish();
+#ifdef AVR_PROFILE
+      const uint64_t tw = PROF_T();
+#endif
       for (;;) {
         const uint32_t used = head - ld_volatile(&sh->fifo_tail[r]);
         if (used < (uint32_t)kFifo) { room = kFifo - used; break; }
         __builtin_amdgcn_s_sleep(1);
       }
+#ifdef AVR_PROFILE
+      wait_cycles += PROF_T() - tw;
+#endif
     }
     sh->fifo[r][head & (kFifo - 1)] = op;
     head++;
@@ -194,13 +207,19 @@ struct RingOut {
   }
 };
 // Consumer end: wait for a batch, load it one entry per lane.  Returns the batch size.
-AVR_FI uint32_t ring_take(Shared* sh, int r, uint32_t tail, uint32_t* op_v) {
+AVR_FI uint32_t ring_take(Shared* sh, int r, uint32_t tail, uint32_t* op_v, uint64_t* waited) {
   uint32_t head;
+#ifdef AVR_PROFILE
+  const uint64_t tw = PROF_T();
+#endif
   for (;;) {
     head = ld_volatile(&sh->fifo_head[r]);
     if (head != tail) break;
     __builtin_amdgcn_s_sleep(1);
   }
+#ifdef AVR_PROFILE
+  *waited += PROF_T() - tw;
+#endif
   const uint32_t n = min(head - tail, 64u);
   const uint32_t lane = __lane_id();
   *op_v = lane < n ? sh->fifo[r][(tail + lane) & (kFifo - 1)] : 0u;
@@ -503,6 +522,7 @@ struct Walker {
       uint64_t sigmask = 0;
       int pos, end = max - 2;
       PROF_BEGIN(t3);
+      asm volatile("; MARK_MAP_BEGIN");
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
         if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
@@ -514,6 +534,7 @@ struct Walker {
           if (rdecide(16 + lc)) { end = pos; break; }
         }
       }
+      asm volatile("; MARK_MAP_END");
       if (pos == max - 1) cnt++;
       PROF_END(3, t3);
       // model: nnz first (recode.cpp:1208-1221), then the buffered map (1244-1255)
@@ -1197,6 +1218,9 @@ AVR_FI void walker_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uin
   profile_slice(w);
   w.rc_writeback();  // estimators persist across slices in the reference model
   w.push(OP_END);
+#ifdef AVR_PROFILE
+  if (__lane_id() == 0) atomicAdd(&avr_prof[16], (unsigned long long)w.ring0.wait_cycles);
+#endif
   w.publish();
   int status = w.err;
   if (!status && !w.finished) status = -9;
@@ -1232,9 +1256,14 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
   RingOut out;
   out.init(sh, 1);
   uint32_t tail = 0;
+  uint64_t waited = 0;
+#ifdef AVR_PROFILE
+  const uint64_t t_start = PROF_T();
+#endif
   for (bool done = false; !done;) {
     uint32_t op_v;
-    const uint32_t n = ring_take(sh, 0, tail, &op_v);
+    const uint32_t n = ring_take(sh, 0, tail, &op_v, &waited);
+    asm volatile("; MARK_MODEL_BEGIN");
     for (uint32_t j = 0; j < n; j++) {
       const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
       if (op & (OP_END | OP_FINISH)) {
@@ -1255,10 +1284,18 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
       }
       out.push(op_recode(b, e));
     }
+    asm volatile("; MARK_MODEL_END");
     tail += n;
     ring_retire(sh, 0, tail);
     out.publish();
   }
+#ifdef AVR_PROFILE
+  if (__lane_id() == 0) {
+    atomicAdd(&avr_prof[17], (unsigned long long)waited);
+    atomicAdd(&avr_prof[18], (unsigned long long)out.wait_cycles);
+    atomicAdd(&avr_prof[20], (unsigned long long)(PROF_T() - t_start));
+  }
+#endif
 }
 
 // The coder wave: compress retires ring 1 (arithmetic_code<uint64_t,uint8_t>::encoder::put /
@@ -1282,9 +1319,13 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
   }
   const int r = MODE == MODE_COMPRESS ? 1 : 0;
   uint32_t tail = 0;
+  uint64_t waited = 0;
+#ifdef AVR_PROFILE
+  const uint64_t t_start = PROF_T();
+#endif
   for (bool done = false; !done;) {
     uint32_t op_v;
-    const uint32_t n = ring_take(sh, r, tail, &op_v);
+    const uint32_t n = ring_take(sh, r, tail, &op_v, &waited);
     if (MODE == MODE_COMPRESS) {
       const uint32_t tot_v = (op_v >> 8) & 127;
       const uint64_t m_v = T->div[tot_v][0];
@@ -1312,6 +1353,12 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
     tail += n;
     ring_retire(sh, r, tail);
   }
+#ifdef AVR_PROFILE
+  if (__lane_id() == 0) {
+    atomicAdd(&avr_prof[19], (unsigned long long)waited);
+    atomicAdd(&avr_prof[21], (unsigned long long)(PROF_T() - t_start));
+  }
+#endif
   if (__lane_id() == 0) {
     sh->c_err = MODE == MODE_COMPRESS ? re.err : ce.err;
     sh->c_len = out_total(o);

@@ -32,7 +32,7 @@ def main():
     ps = avr.parse_stream(data)
     b = DeviceBatch(ctx, ps)
     L = avr.lib()
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 32)()
     L.avr_debug_profile(2, buf)   # clear the generator's counters
     out = {}
     for mode, name in ((0, "compress"), (1, "decompress")):
@@ -48,7 +48,11 @@ def main():
                      "cycles": {NAMES[i]: v[i] for i in range(8)},
                      "section_bins": {NAMES[i]: v[8 + i] for i in range(8)},
                      "cycles_per_slice_bin": {NAMES[i]: round(v[i] / bins, 1) for i in range(8)},
-                     "cycles_per_section_bin": {NAMES[i]: round(v[i] / max(1, v[8 + i]), 1) for i in range(8)}}
+                     "cycles_per_section_bin": {NAMES[i]: round(v[i] / max(1, v[8 + i]), 1) for i in range(8)},
+                     "waits_per_bin": {"walker_push": round(v[16] / bins, 1), "modeler_take": round(v[17] / bins, 1),
+                                       "modeler_push": round(v[18] / bins, 1), "coder_take": round(v[19] / bins, 1),
+                                       "modeler_total": round(v[20] / bins, 1), "coder_total": round(v[21] / bins, 1)},
+                     "ecache": {"lookups": v[22], "misses": v[23], "nz_lookups": v[24]}}
     print(json.dumps(out, indent=1))
 
 
