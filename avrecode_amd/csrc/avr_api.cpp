@@ -804,3 +804,302 @@ extern "C" int avr_debug_profile(int mode, unsigned long long* out16) {
                            : avr::profile_parallel_generate(out16);
   return e == hipSuccess ? AVR_OK : AVR_ERR_DEVICE;
 }
+
+// ==================================================================== libavcodec-hooks surface
+// The reference's hook objects (compressor::cabac_decoder recode.cpp:1134-1268,
+// decompressor::cabac_decoder 1411-1520) answer each bin request by running the model inline.
+// Here the device has already done the whole file; the session replays the device's decode-order
+// bin trace (MODE_TRACE kernel) to the caller and cross-checks the caller's parse against it.
+struct avr_hooks_session;
+
+struct avr_hooks_slice {
+  avr_hooks_session* sess = nullptr;
+  int index = 0;                 // slice index (decode order)
+  const uint8_t* trace = nullptr;
+  size_t nbins = 0, cur = 0;
+  bool sub_open = false;
+  int sub_args[5] = {0, 0, 0, 0, 0};
+  int coding_type = 0;
+};
+
+struct avr_hooks_session {
+  avr_ctx* c = nullptr;
+  bool decompress = false;
+  std::vector<uint8_t> original;   // the H.264 file
+  std::vector<uint8_t> result;     // compress: the container; decompress: the original file
+  std::vector<uint8_t> stream;     // decompress: read_packet's stream
+  ParsedFile pf;
+  std::vector<char> coded;
+  std::vector<uint8_t> traces;
+  std::vector<uint64_t> trace_off;
+  std::vector<uint32_t> trace_len;
+  std::vector<avr_hooks_slice> slices;
+  size_t next_slice = 0;
+  uint64_t next_marker = 1;
+  avr_hooks_slice* live = nullptr;  // the slice model hooks refer to (one live CABAC context, recode.cpp:199)
+  uint64_t mb_calls = 0;
+  std::string err;
+  void fail_once(const std::string& m) {
+    if (err.empty()) err = m;
+  }
+};
+
+namespace {
+
+// FFmpeg's state transition for one decoded bin (ff_h264_mlps_state, cabac_code.h:46-48)
+uint8_t next_state(uint8_t s, int bin) {
+  const int p = s >> 1, mps = s & 1;
+  if (bin == mps) return (uint8_t)(2 * (p < 62 ? p + 1 : p) + mps);
+  return (uint8_t)(p == 0 ? (s ^ 1) : 2 * avr::kTransIdxLPS[p] + mps);
+}
+
+// Device trace of every coded slice of hs->pf (decode order), MODE_TRACE kernel.
+int run_traces(avr_hooks_session* hs) {
+  avr_ctx* c = hs->c;
+  Plan plan;
+  std::vector<int> slice_of;
+  for (size_t i = 0; i < hs->pf.slices.size(); i++) {
+    if (!hs->coded[i]) continue;
+    const avr::SliceInfo& s = hs->pf.slices[i];
+    avr_slice_desc d = desc_from_header(s);
+    append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
+    d.payload_size = (uint32_t)s.size;
+    d.read_limit = (uint32_t)s.read_limit;
+    // 2 bytes per bin; H.264 bounds the bins of a slice by ~32/3 per payload byte plus a
+    // per-macroblock allowance (7.4.2.2), well inside this
+    d.out_capacity = (uint32_t)std::min<uint64_t>(0xfffffff0ull, 2ull * (16ull * s.size + 2048ull * d.mb_width * d.mb_height / 8 + 4096));
+    plan.max_w = std::max(plan.max_w, d.mb_width);
+    slice_of.push_back((int)i);
+    plan.descs.push_back(d);
+  }
+  hs->trace_off.assign(hs->pf.slices.size(), 0);
+  hs->trace_len.assign(hs->pf.slices.size(), 0);
+  if (plan.descs.empty()) return AVR_OK;
+  std::vector<avr_slice_result> res;
+  if (int r = run_plan(c, 3, false, plan, &res, &hs->traces)) return r;
+  for (size_t k = 0; k < plan.descs.size(); k++) {
+    if (res[k].status != 0)
+      return fail(c, AVR_ERR_FORMAT, "hooks: device trace of slice " + std::to_string(slice_of[k]) + " failed (" +
+                                         std::to_string(res[k].status) + ")");
+    hs->trace_off[slice_of[k]] = plan.descs[k].out_offset;
+    hs->trace_len[slice_of[k]] = res[k].out_len / 2;
+  }
+  return AVR_OK;
+}
+
+// which slices of the file a container re-codes: the i-th non-literal block is slice i's
+bool coded_from_container(const std::vector<avr::PbBlock>& blocks, size_t n_slices, std::vector<char>* coded) {
+  coded->assign(n_slices, 0);
+  size_t i = 0;
+  for (auto& b : blocks) {
+    if (b.has_literal) continue;
+    if (i >= n_slices) return false;
+    (*coded)[i++] = b.has_cabac ? 1 : 0;
+  }
+  return i == n_slices;
+}
+
+int hooks_finish_setup(avr_hooks_session* hs, const std::vector<avr::PbBlock>& blocks) {
+  if (int r = parse_file(hs->c, hs->original.data(), hs->original.size(), &hs->pf)) return r;
+  if (!coded_from_container(blocks, hs->pf.slices.size(), &hs->coded))
+    return fail(hs->c, AVR_ERR_FORMAT, "hooks: container blocks do not match the file's slices");
+  if (int r = run_traces(hs)) return r;
+  hs->slices.resize(hs->pf.slices.size());
+  return AVR_OK;
+}
+
+}  // namespace
+
+int avr_hooks_compress_begin(avr_ctx* c, const uint8_t* file, size_t n, int model, avr_hooks_session** out) {
+  if (!c || !file || !out) return AVR_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  std::unique_ptr<avr_hooks_session> hs(new avr_hooks_session);
+  hs->c = c;
+  hs->original.assign(file, file + n);
+  uint8_t* avrc = nullptr;
+  size_t avrc_len = 0;
+  if (int r = avr_compress_file(c, file, n, model, &avrc, &avrc_len)) return r;
+  hs->result.assign(avrc, avrc + avrc_len);
+  free(avrc);
+  std::vector<avr::PbBlock> blocks;
+  std::string version;
+  if (!avr::pb_parse(hs->result.data(), hs->result.size(), &blocks, &version))
+    return fail(c, AVR_ERR_FORMAT, "hooks: container does not parse");
+  if (int r = hooks_finish_setup(hs.get(), blocks)) return r;
+  *out = hs.release();
+  return AVR_OK;
+}
+
+int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_hooks_session** out,
+                               const uint8_t** stream, size_t* stream_len) {
+  if (!c || !avrc || !out) return AVR_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  std::unique_ptr<avr_hooks_session> hs(new avr_hooks_session);
+  hs->c = c;
+  hs->decompress = true;
+  uint8_t* orig = nullptr;
+  size_t orig_len = 0;
+  if (int r = avr_decompress_file(c, avrc, n, &orig, &orig_len)) return r;
+  hs->original.assign(orig, orig + orig_len);
+  hs->result = hs->original;
+  free(orig);
+  std::vector<avr::PbBlock> blocks;
+  std::string version;
+  if (!avr::pb_parse(avrc, n, &blocks, &version)) return fail(c, AVR_ERR_FORMAT, "hooks: container does not parse");
+  // read_packet (recode.cpp:1359-1409)
+  uint64_t seq = 1;
+  for (auto& b : blocks) {
+    if (b.has_literal) {
+      hs->stream.insert(hs->stream.end(), b.literal, b.literal + b.literal_len);
+    } else if (b.has_cabac) {
+      uint8_t mk[8];
+      avr::surrogate_marker(seq++, mk);
+      hs->stream.insert(hs->stream.end(), mk, mk + 8);
+      hs->stream.insert(hs->stream.end(), (size_t)b.size - 8, (uint8_t)'X');
+    }
+  }
+  if (int r = hooks_finish_setup(hs.get(), blocks)) return r;
+  if (stream) *stream = hs->stream.data();
+  if (stream_len) *stream_len = hs->stream.size();
+  *out = hs.release();
+  return AVR_OK;
+}
+
+void* avr_hook_init_decoder(void* opaque, void* /*cabac_context*/, const uint8_t* buf, int size) {
+  avr_hooks_session* hs = (avr_hooks_session*)opaque;
+  if (!hs) return nullptr;
+  if (hs->live && hs->live->cur != hs->live->nbins)
+    hs->fail_once("hooks: slice " + std::to_string(hs->live->index) + " ended after " +
+                  std::to_string(hs->live->cur) + " of " + std::to_string(hs->live->nbins) + " bins");
+  hs->live = nullptr;
+  if (hs->next_slice >= hs->pf.slices.size()) {
+    hs->fail_once("hooks: more slices than the file holds");
+    return nullptr;
+  }
+  const size_t i = hs->next_slice++;
+  const avr::SliceInfo& s = hs->pf.slices[i];
+  if (!buf || size < 0 || (size_t)size != s.size) {
+    hs->fail_once("hooks: slice " + std::to_string(i) + " size differs from the device's parse");
+    return nullptr;
+  }
+  if (!hs->coded[i]) return nullptr;  // not re-coded: decode natively (recode.cpp:1139-1145)
+  if (hs->decompress) {
+    // recognize_coded_block (recode.cpp:1546-1573)
+    uint8_t mk[8];
+    avr::surrogate_marker(hs->next_marker++, mk);
+    if (size < 8 || memcmp(buf, mk, 8) != 0) {
+      hs->fail_once("hooks: invalid surrogate marker in slice " + std::to_string(i));
+      return nullptr;
+    }
+  } else if (memcmp(buf, s.payload(), s.size) != 0) {
+    hs->fail_once("hooks: slice " + std::to_string(i) + " payload differs from the file's");
+    return nullptr;
+  }
+  avr_hooks_slice& h = hs->slices[i];
+  h.sess = hs;
+  h.index = (int)i;
+  h.trace = hs->traces.data() + hs->trace_off[i];
+  h.nbins = hs->trace_len[i];
+  h.cur = 0;
+  hs->live = &h;
+  return &h;
+}
+
+static int hook_bin(void* slice, int kind, uint8_t* state) {
+  avr_hooks_slice* h = (avr_hooks_slice*)slice;
+  if (!h || !h->sess) return 0;
+  if (h->cur >= h->nbins) {
+    h->sess->fail_once("hooks: slice " + std::to_string(h->index) + " asked for more bins than it holds");
+    return 0;
+  }
+  const uint8_t t = h->trace[2 * h->cur], pre = h->trace[2 * h->cur + 1];
+  h->cur++;
+  const int bin = t & 1;
+  if (((t >> 1) & 3) != kind) {
+    h->sess->fail_once("hooks: slice " + std::to_string(h->index) + " bin " + std::to_string(h->cur - 1) +
+                       ": bin kind differs from the device's parse");
+    return bin;
+  }
+  if (state) {
+    if (*state != pre)
+      h->sess->fail_once("hooks: slice " + std::to_string(h->index) + " bin " + std::to_string(h->cur - 1) +
+                         ": context state differs from the device's parse");
+    *state = next_state(*state, bin);
+  }
+  return bin;
+}
+
+int avr_hook_get(void* slice, uint8_t* state) {
+  if (!state) {
+    if (slice && ((avr_hooks_slice*)slice)->sess) ((avr_hooks_slice*)slice)->sess->fail_once("hooks: get without a state");
+    return 0;
+  }
+  return hook_bin(slice, 0, state);
+}
+int avr_hook_get_bypass(void* slice) { return hook_bin(slice, 1, nullptr); }
+int avr_hook_get_terminate(void* slice) { return hook_bin(slice, 2, nullptr); }
+
+const uint8_t* avr_hook_skip_bytes(void* slice, int /*n*/) {
+  avr_hooks_slice* h = (avr_hooks_slice*)slice;
+  if (h && h->sess) h->sess->fail_once("hooks: skip_bytes (I_PCM) is not supported");
+  return nullptr;
+}
+
+void avr_hook_frame_spec(void* /*opaque*/, int /*frame_num*/, int /*mb_width*/, int /*mb_height*/) {}
+
+void avr_hook_mb_xy(void* opaque, int /*x*/, int /*y*/) {
+  if (opaque) ((avr_hooks_session*)opaque)->mb_calls++;
+}
+
+void avr_hook_begin_sub_mb(void* opaque, int cat, int scan8index, int max_coeff, int is_dc, int chroma422) {
+  avr_hooks_session* hs = (avr_hooks_session*)opaque;
+  if (!hs || !hs->live) return;
+  avr_hooks_slice* h = hs->live;
+  if (h->sub_open) hs->fail_once("hooks: begin_sub_mb inside an open sub-macroblock");
+  h->sub_open = true;
+  const int a[5] = {cat, scan8index, max_coeff, is_dc, chroma422};
+  memcpy(h->sub_args, a, sizeof(a));
+}
+
+void avr_hook_end_sub_mb(void* opaque, int cat, int scan8index, int max_coeff, int is_dc, int chroma422) {
+  avr_hooks_session* hs = (avr_hooks_session*)opaque;
+  if (!hs || !hs->live) return;
+  avr_hooks_slice* h = hs->live;
+  const int a[5] = {cat, scan8index, max_coeff, is_dc, chroma422};
+  if (!h->sub_open || memcmp(h->sub_args, a, sizeof(a)) != 0)  // recode.cpp:185-189
+    hs->fail_once("hooks: end_sub_mb does not match begin_sub_mb");
+  h->sub_open = false;
+}
+
+void avr_hook_begin_coding_type(void* opaque, int coding_type, int /*zigzag_index*/, int /*param0*/, int /*param1*/) {
+  avr_hooks_session* hs = (avr_hooks_session*)opaque;
+  if (!hs || !hs->live) return;
+  if (hs->live->coding_type != AVR_PIP_UNKNOWN) hs->fail_once("hooks: nested begin_coding_type");
+  hs->live->coding_type = coding_type;
+}
+
+void avr_hook_end_coding_type(void* opaque, int coding_type) {
+  avr_hooks_session* hs = (avr_hooks_session*)opaque;
+  if (!hs || !hs->live) return;
+  if (hs->live->coding_type != coding_type) hs->fail_once("hooks: end_coding_type does not match begin_coding_type");
+  hs->live->coding_type = AVR_PIP_UNKNOWN;
+}
+
+int avr_hooks_end(avr_hooks_session* hs, uint8_t** out, size_t* out_len) {
+  if (!hs || !out || !out_len) return AVR_ERR_INVALID_ARGUMENT;
+  if (hs->live && hs->live->cur != hs->live->nbins)
+    hs->fail_once("hooks: slice " + std::to_string(hs->live->index) + " ended after " +
+                  std::to_string(hs->live->cur) + " of " + std::to_string(hs->live->nbins) + " bins");
+  hs->live = nullptr;
+  if (hs->next_slice != hs->pf.slices.size())
+    hs->fail_once("hooks: " + std::to_string(hs->next_slice) + " of " + std::to_string(hs->pf.slices.size()) +
+                  " slices were decoded");
+  if (!hs->err.empty()) return fail(hs->c, AVR_ERR_FORMAT, hs->err);
+  *out = (uint8_t*)malloc(hs->result.size() ? hs->result.size() : 1);
+  if (!*out) return AVR_ERR_OUT_OF_MEMORY;
+  memcpy(*out, hs->result.data(), hs->result.size());
+  *out_len = hs->result.size();
+  return AVR_OK;
+}
+
+void avr_hooks_destroy(avr_hooks_session* hs) { delete hs; }

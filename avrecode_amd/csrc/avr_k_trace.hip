@@ -1,0 +1,25 @@
+// parallel slice kernel, MODE_TRACE (decode-only bin trace for the hooks layer) (one translation unit per kernel: see avr_walker.h).
+#include "avr_walker.h"
+
+namespace avr {
+
+hipError_t launch_parallel_trace(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
+                    uint8_t* out, avr_slice_result* res, uint16_t* est, hipStream_t stream) {
+  hipLaunchKernelGGL(slices_parallel_kernel<MODE_TRACE>, dim3(n), dim3(slice_threads<MODE_TRACE>()), lds, stream, T, descs, n, in, out, res, est);
+  return hipGetLastError();
+}
+
+// AVR_PROFILE builds: read (and clear) this kernel's section cycle counters; zeros otherwise.
+hipError_t profile_parallel_trace(unsigned long long* out16) {
+#ifdef AVR_PROFILE
+  hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(avr_prof), sizeof(unsigned long long) * 32);
+  unsigned long long z[32] = {};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(avr_prof), z, sizeof(z));
+  return e;
+#else
+  for (int i = 0; i < 32; i++) out16[i] = 0;
+  return hipSuccess;
+#endif
+}
+
+}  // namespace avr

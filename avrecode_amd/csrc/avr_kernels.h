@@ -14,7 +14,7 @@ struct EngineTables;
 constexpr int kEstGlobal = 294016;
 
 size_t shared_bytes(int max_mb_width);
-// mode: 0 compress, 1 decompress, 2 generate.  sequential = reference model (single wavefront).
+// mode: 0 compress, 1 decompress, 2 generate, 3 trace (decode-only bin trace).  sequential = reference model (single wavefront).
 hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
                          int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                          uint8_t* frames, int* frame_meta, hipStream_t stream);
@@ -28,6 +28,9 @@ hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_des
 hipError_t launch_parallel_generate(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                     hipStream_t stream);
+hipError_t launch_parallel_trace(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
+                                 const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
+                                 hipStream_t stream);
 hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                       uint8_t* frames, int* frame_meta, hipStream_t stream);
@@ -38,6 +41,7 @@ hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_d
 hipError_t profile_parallel_compress(unsigned long long* out16);
 hipError_t profile_parallel_decompress(unsigned long long* out16);
 hipError_t profile_parallel_generate(unsigned long long* out16);
+hipError_t profile_parallel_trace(unsigned long long* out16);
 hipError_t profile_sequential_compress(unsigned long long* out16);
 hipError_t profile_sequential_decompress(unsigned long long* out16);
 hipError_t launch_derive_decompress(const avr_slice_desc* descs, const avr_slice_result* rc, int n,

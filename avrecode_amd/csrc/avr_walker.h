@@ -48,7 +48,10 @@ namespace avr {
 static __device__ unsigned long long avr_prof[32];
 #endif
 
-enum { MODE_COMPRESS = 0, MODE_DECOMPRESS = 1, MODE_GENERATE = 2 };
+// MODE_TRACE: the compress-side CABAC decode + parse alone, recording every bin in decode order
+// (2 bytes: bin | kind << 1, the context's state byte before the bin) -- the bin sequence the
+// libavcodec-hooks layer (avr_hook_*) serves to its caller.
+enum { MODE_COMPRESS = 0, MODE_DECOMPRESS = 1, MODE_GENERATE = 2, MODE_TRACE = 3 };
 enum { F_DEC = 1, F_SKIP = 2, F_INTRA = 4, F_I16 = 8, F_D16 = 16, F_T8 = 32, F_CPRED = 64 };
 enum { SE_OTHER = 0, SE_REF, SE_QPDELTA, SE_MVD_SUFFIX, SE_LEVEL_SUFFIX, SE_EOS, SE_PCM };
 
@@ -248,6 +251,7 @@ AVR_FI void est_store(Shared* sh, uint32_t idx, uint32_t slot, uint32_t e) {
 
 template <int MODE, bool RM>
 struct Walker {
+  static constexpr bool DEC = MODE == MODE_COMPRESS || MODE == MODE_TRACE;  // CABAC decoding side
   const HotTables* T;     // LDS copy
   const EngineTables* G;  // global (init-only tables)
   const avr_slice_desc* d;
@@ -311,13 +315,18 @@ struct Walker {
     uint32_t ns;
     const int b = cd_decide(cd, in, s, vtab_rec(vt, s), &ns);
     rc_v = wlane(rc_v, L, ns);
+    if (MODE == MODE_TRACE) trace(b, OPK_DECISION, s);
     return b;
+  }
+  AVR_FI void trace(int b, uint32_t kind, uint32_t s) {
+    out_byte(out, (uint32_t)b | kind << 1);
+    out_byte(out, s);
   }
   // a residual bin through the model on cached lane L; ctx = rc_addr(rc_cat, L)
   AVR_FI int rbin(uint32_t L, int ctx) {
-    if (MODE == MODE_COMPRESS) {
+    if (DEC) {
       const int b = rdecide(L);
-      push(op_model(b, 0, ctx));
+      if (MODE == MODE_COMPRESS) push(op_model(b, 0, ctx));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       bins++;
@@ -347,9 +356,13 @@ struct Walker {
   // ------------------------------------------------------------------ bins through the model
   AVR_FI int bin(int se, int k, int ctx) {
     bins++;
-    if (MODE == MODE_COMPRESS) {
-      const int b = cd_decision_v(cd, in, &sh->state[ctx], vt);
-      push(op_model(b, 0, ctx));
+    if (DEC) {
+      const uint32_t s = sh->state[ctx];
+      uint32_t ns;
+      const int b = cd_decide(cd, in, s, vtab_rec(vt, s), &ns);
+      sh->state[ctx] = (uint8_t)ns;
+      if (MODE == MODE_TRACE) trace(b, OPK_DECISION, s);
+      else push(op_model(b, 0, ctx));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[ctx];
@@ -365,9 +378,10 @@ struct Walker {
   }
   AVR_FI int bypass(int se, int k) {
     bins++;
-    if (MODE == MODE_COMPRESS) {
+    if (DEC) {
       const int b = cd_bypass(cd, in);
-      push(op_model(b, 0, 1024));
+      if (MODE == MODE_TRACE) trace(b, OPK_BYPASS, 0);
+      else push(op_model(b, 0, 1024));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1024];
@@ -384,10 +398,14 @@ struct Walker {
   AVR_FI int terminate(int se) {
     bins++;
     int b;
-    if (MODE == MODE_COMPRESS) {
+    if (DEC) {
       b = cd_terminate(cd, in);
-      push(op_model(b, 0, 1025));
-      if (b) push(OP_FINISH);
+      if (MODE == MODE_TRACE) {
+        trace(b, OPK_TERMINATE, 0);
+      } else {
+        push(op_model(b, 0, 1025));
+        if (b) push(OP_FINISH);
+      }
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1025];
       b = rd_get(rd, in, rc_p1(rd.range, e, T));
@@ -518,11 +536,10 @@ struct Walker {
     const int bits = max > 16 ? 6 : max > 4 ? 4 : 2;
     const int mask = (1 << bits) - 1;
     int cnt = 0;
-    if (MODE == MODE_COMPRESS) {
+    if (DEC) {
       uint64_t sigmask = 0;
       int pos, end = max - 2;
       PROF_BEGIN(t3);
-      asm volatile("; MARK_MAP_BEGIN");
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
         if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
@@ -534,23 +551,24 @@ struct Walker {
           if (rdecide(16 + lc)) { end = pos; break; }
         }
       }
-      asm volatile("; MARK_MAP_END");
       if (pos == max - 1) cnt++;
       PROF_END(3, t3);
-      // model: nnz first (recode.cpp:1208-1221), then the buffered map (1244-1255)
-      PROF_BEGIN(t4);
-      nz_bits(cat, n, max, is_dc, c422, cnt);
-      PROF_END(4, t4);
-      PROF_BEGIN(t5);
-      const int nnz_m = cnt & mask;
-      int obs = 0;
-      for (int zz = 0; zz <= end; zz++) {
-        int b = (int)((sigmask >> zz) & 1);
-        int idx = sig_est_index(cat, max, is_dc, c422, zz, nnz_m, obs);
-        push(op_model(b, OPM_CACHE | OPM_THR50, idx));
-        obs += b;
+      if (MODE == MODE_COMPRESS) {
+        // model: nnz first (recode.cpp:1208-1221), then the buffered map (1244-1255)
+        PROF_BEGIN(t4);
+        nz_bits(cat, n, max, is_dc, c422, cnt);
+        PROF_END(4, t4);
+        PROF_BEGIN(t5);
+        const int nnz_m = cnt & mask;
+        int obs = 0;
+        for (int zz = 0; zz <= end; zz++) {
+          int b = (int)((sigmask >> zz) & 1);
+          int idx = sig_est_index(cat, max, is_dc, c422, zz, nnz_m, obs);
+          push(op_model(b, OPM_CACHE | OPM_THR50, idx));
+          obs += b;
+        }
+        PROF_END(5, t5);
       }
-      PROF_END(5, t5);
     } else if (MODE == MODE_DECOMPRESS) {
       const int nnz_m = nz_bits(cat, n, max, is_dc, c422, 0);   // recode.cpp:1476-1486
       int pos;
@@ -1154,9 +1172,9 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
       wave_sync();
     }
     PROF_ENDW(7, t7);
-    if (MODE != MODE_GENERATE) w.publish();
+    if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) w.publish();
     if (w.terminate(SE_EOS)) break;
-    if (MODE == MODE_COMPRESS && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
+    if (Walker<MODE, RM>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
     addr++;
   }
 }
@@ -1177,7 +1195,7 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   vtab_load(w.vt, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
-  if (MODE == MODE_COMPRESS) {
+  if (MODE == MODE_COMPRESS || MODE == MODE_TRACE) {
     cd_init(w.cd, w.in);
   } else if (MODE == MODE_DECOMPRESS) {
     rd_init(w.rd, w.in);
@@ -1388,7 +1406,7 @@ AVR_FI void run_slice_inline(Walker<MODE, RM>& w, const avr_slice_desc* d, const
   w.rc_writeback();
   int status = w.err;
   if (!status && !w.finished) status = -9;
-  if (w.ce.err) status = -10;
+  if (MODE == MODE_GENERATE && w.ce.err) status = -10;
   if (out_overflow(w.out)) status = -12;
   if (__lane_id() == 0) {
     res->out_len = out_total(w.out);
@@ -1408,7 +1426,9 @@ AVR_FI void load_hot_tables(Shared* sh, const EngineTables* G) {
 
 // Threads per workgroup: two waves (walker + coder) for compress / decompress, one for generate.
 template <int MODE>
-constexpr int slice_threads() { return MODE == MODE_GENERATE ? 64 : MODE == MODE_COMPRESS ? 192 : 128; }
+constexpr int slice_threads() {
+  return MODE == MODE_GENERATE || MODE == MODE_TRACE ? 64 : MODE == MODE_COMPRESS ? 192 : 128;
+}
 
 template <int MODE>
 __global__ __launch_bounds__(192, 3) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
@@ -1437,14 +1457,14 @@ __global__ __launch_bounds__(192, 3) void slices_parallel_kernel(const EngineTab
     return;
   }
   // fresh model for this slice: clear the dense SIG/NZ estimators (16 B per thread per step)
-  if (MODE != MODE_GENERATE) {
+  if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) {
     uint4* e4 = (uint4*)w.est_g;
     for (int i = threadIdx.x; i < kEstGlobal / 8; i += blockDim.x) e4[i] = make_uint4(0, 0, 0, 0);
   }
   w.d = d;
   w.W = d->mb_width;
   init_slice_state(w, G);
-  if (MODE == MODE_GENERATE) {
+  if (MODE == MODE_GENERATE || MODE == MODE_TRACE) {
     run_slice_inline(w, d, in, out, &res[s]);
     return;
   }

@@ -14,8 +14,11 @@
  *                                                         arithmetic_code.h encoder 89-203)
  *   avr_decompress_slices decompressor::cabac_decoder x N recode.cpp:1411-1520 (+ cabac_code.h 27-80,
  *                                                         arithmetic_code.h decoder 211-298)
- * The per-bin libavcodec-hooks callback surface (AVCodecHooks, recode.cpp:137-228) is realised
- * inside the device kernels: the kernel owns the CABAC parse that drives those callbacks.
+ *   avr_hook_*           the libavcodec-hooks callback surface, AVCodecHooks    recode.cpp:137-228
+ *                        (cabac.init_decoder/get/get_bypass/get_terminate/skip_bytes, model.frame_spec/
+ *                        mb_xy/begin_sub_mb/end_sub_mb/begin_coding_type/end_coding_type)
+ * The device kernels own the CABAC parse; the hooks layer serves the bins the device decoded to a
+ * libavcodec-hooks caller, call by call, and checks the caller's parse against the device's.
  */
 #ifndef AVRECODE_AMD_H
 #define AVRECODE_AMD_H
@@ -148,6 +151,49 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
  * The result is byte-identical to avr_compress_file(..., AVR_MODEL_PARALLEL). */
 int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
                            const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len);
+
+/* ------------------------------------------------ libavcodec-hooks callback surface (AVCodecHooks) */
+/* For a caller that drives the recode path from its own H.264 decoder exactly as the reference's
+ * libavcodec-hooks fork does (recode.cpp:137-228).  A session runs the whole file on the device up
+ * front (compress: recoded container + the decode-order bin trace of every coded slice;
+ * decompress: the original file + the same traces), then serves the per-bin callbacks from the
+ * traces: get() returns the bin and advances *state the way ff_get_cabac / cabac::encoder::put
+ * would (recode.cpp:1176, 1443).  Every callback checks the caller's parse against the device's
+ * (state byte before each decision, bin kinds, sub-MB / coding-type pairing, recode.cpp:185-189,
+ * 933-947); a mismatch makes avr_hooks_end fail with AVR_ERR_FORMAT.  Not thread-safe. */
+typedef struct avr_hooks_session avr_hooks_session;
+
+/* CodingType (EACH_PIP_CODING_TYPE, recode.cpp:616) */
+typedef enum {
+  AVR_PIP_UNKNOWN = 0, AVR_PIP_UNREACHABLE, AVR_PIP_SIGNIFICANCE_MAP, AVR_PIP_SIGNIFICANCE_EOB,
+  AVR_PIP_SIGNIFICANCE_NZ, AVR_PIP_RESIDUALS
+} avr_pip_coding_type;
+
+/* compressor(input, out) (recode.cpp:1102-1113): file = the H.264 file the caller decodes. */
+int avr_hooks_compress_begin(avr_ctx* ctx, const uint8_t* file, size_t n, int model, avr_hooks_session** out);
+/* decompressor(input, out) (recode.cpp:1312-1336): avrc = a Recoded container.  *stream is what
+ * read_packet feeds the decoder (literals + surrogate blocks, recode.cpp:1359-1409), valid until
+ * avr_hooks_destroy. */
+int avr_hooks_decompress_begin(avr_ctx* ctx, const uint8_t* avrc, size_t n, avr_hooks_session** out,
+                               const uint8_t** stream, size_t* stream_len);
+/* AVCodecHooks.cabac: opaque = the session.  init_decoder returns the per-slice opaque, or NULL
+ * when the slice is not re-coded (the caller then decodes it natively, recode.cpp:1139-1145). */
+void* avr_hook_init_decoder(void* opaque, void* cabac_context, const uint8_t* buf, int size);
+int avr_hook_get(void* slice, uint8_t* state);
+int avr_hook_get_bypass(void* slice);
+int avr_hook_get_terminate(void* slice);
+/* I_PCM is unsupported, as in the reference (recode.cpp:161-163): records an error, returns NULL. */
+const uint8_t* avr_hook_skip_bytes(void* slice, int n);
+/* AVCodecHooks.model: opaque = the session */
+void avr_hook_frame_spec(void* opaque, int frame_num, int mb_width, int mb_height);
+void avr_hook_mb_xy(void* opaque, int x, int y);
+void avr_hook_begin_sub_mb(void* opaque, int cat, int scan8index, int max_coeff, int is_dc, int chroma422);
+void avr_hook_end_sub_mb(void* opaque, int cat, int scan8index, int max_coeff, int is_dc, int chroma422);
+void avr_hook_begin_coding_type(void* opaque, int coding_type, int zigzag_index, int param0, int param1);
+void avr_hook_end_coding_type(void* opaque, int coding_type);
+/* compress: *out = the Recoded container; decompress: *out = the original file (avr_free). */
+int avr_hooks_end(avr_hooks_session* s, uint8_t** out, size_t* out_len);
+void avr_hooks_destroy(avr_hooks_session* s);
 
 /* --------------------------------------------------------------- synthetic H.264 (benchmarks) */
 typedef struct {

@@ -1,0 +1,117 @@
+/*
+ * Test driver (TEST INFRASTRUCTURE): plays the libavcodec-hooks caller against the C-ABI hooks
+ * layer of libavrecode.so.  The oracle's slice_data() parser (oracle/oracle_walker.c) stands in for
+ * the fork's H.264 decoder: it walks every CABAC slice of the stream, pulling each bin through
+ * avr_hook_get / _bypass / _terminate and reporting the model events (mb_xy, begin/end_sub_mb,
+ * begin/end_coding_type) exactly where the fork would.  The parse is driven by the device's bins,
+ * so a wrong bin desynchronises it (and the layer checks the caller's context states).
+ *
+ * Built by tests/test_hooks.py into tests/native/_build/libhooks_driver.so.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/avrecode.h"
+#include "../../oracle/avr_oracle.h"
+
+static int fwd_get(void *o, uint8_t *state, int ctx_idx) { (void)ctx_idx; return avr_hook_get(o, state); }
+static int fwd_bypass(void *o) { return avr_hook_get_bypass(o); }
+static int fwd_terminate(void *o) { return avr_hook_get_terminate(o); }
+
+/* The model hooks go to the session (AVCodecHooks.opaque); the cabac hooks to the slice object. */
+static void *g_session;
+static void m_frame_spec(void *o, int f, int w, int h) { (void)o; avr_hook_frame_spec(g_session, f, w, h); }
+static void m_mb_xy(void *o, int x, int y) { (void)o; avr_hook_mb_xy(g_session, x, y); }
+static void m_begin_sub(void *o, int a, int b, int c, int d, int e) { (void)o; avr_hook_begin_sub_mb(g_session, a, b, c, d, e); }
+static void m_end_sub(void *o, int a, int b, int c, int d, int e) { (void)o; avr_hook_end_sub_mb(g_session, a, b, c, d, e); }
+static void m_begin_ct(void *o, avr_coding_type ct, int z, int p0, int p1) { (void)o; avr_hook_begin_coding_type(g_session, (int)ct, z, p0, p1); }
+static void m_end_ct(void *o, avr_coding_type ct) { (void)o; avr_hook_end_coding_type(g_session, (int)ct); }
+
+/* Decode every CABAC slice of `stream` through the hooks (the fork's av_decoder loop,
+ * recode.cpp:114-135).  Returns the number of slices walked, or < 0. */
+static long drive(const uint8_t *stream, size_t n) {
+  avr_nal_t *nals;
+  int nn = avr_demux(stream, n, &nals);
+  if (nn < 0) return -1;
+  avr_param_sets_t *ps = (avr_param_sets_t *)calloc(1, sizeof(avr_param_sets_t));
+  int x264_build = -1, have_prev = 0, picture_id = 0;
+  avr_slice_hdr_t prev;
+  long walked = 0;
+  memset(&prev, 0, sizeof(prev));
+  for (int i = 0; i < nn; i++) {
+    const uint8_t *nal = stream + nals[i].offset;
+    size_t len = nals[i].size;
+    if (len < 2) continue;
+    int type = nal[0] & 0x1f, ref_idc = (nal[0] >> 5) & 3;
+    if (type != 1 && type != 5 && type != 6 && type != 7 && type != 8) continue;
+    uint8_t *rbsp = (uint8_t *)malloc(len);
+    size_t rl = avr_nal_unescape(nal + 1, len - 1, rbsp);
+    if (type == 6) { int b = avr_parse_sei_x264_build(rbsp, rl); if (b > 0) x264_build = b; free(rbsp); continue; }
+    if (type == 7) { avr_parse_sps(ps, rbsp, rl); free(rbsp); continue; }
+    if (type == 8) { avr_parse_pps(ps, rbsp, rl); free(rbsp); continue; }
+    avr_slice_hdr_t h;
+    if (avr_parse_slice_header(ps, rbsp, rl, type, ref_idc, &h) != 0 || !ps->pps[h.pps_id].entropy_coding_mode) {
+      free(rbsp);
+      continue;
+    }
+    h.x264_build = x264_build;
+    int new_pic = !have_prev || h.first_mb == 0 || h.first_mb <= prev.first_mb || h.frame_num != prev.frame_num ||
+                  h.pps_id != prev.pps_id || h.poc_lsb != prev.poc_lsb ||
+                  (h.nal_unit_type == 5) != (prev.nal_unit_type == 5) || h.idr_pic_id != prev.idr_pic_id ||
+                  (h.nal_ref_idc == 0) != (prev.nal_ref_idc == 0);
+    if (new_pic) picture_id++;
+    prev = h;
+    have_prev = 1;
+    size_t bits = avr_rbsp_bit_length(rbsp, rl);
+    size_t end = (bits + 7) / 8;
+    size_t size = end > h.cabac_start ? end - h.cabac_start : 0;
+    m_frame_spec(NULL, picture_id, h.mb_width, h.mb_height);
+    void *slice = avr_hook_init_decoder(g_session, NULL, rbsp + h.cabac_start, (int)size);
+    if (slice) {
+      avr_hooks_t hk = {slice, fwd_get, fwd_bypass, fwd_terminate, m_frame_spec, m_mb_xy,
+                        m_begin_sub, m_end_sub, m_begin_ct, m_end_ct};
+      if (avr_walk_slice(&h, &hk, picture_id) != 0) { free(rbsp); walked = -2; break; }
+      walked++;
+    }
+    free(rbsp);
+  }
+  free(ps);
+  free(nals);
+  return walked;
+}
+
+/* compress `file` through the hooks; *out = the container.  Returns avr status (or -100 - x on a
+ * driver failure); *walked = slices walked through the hooks. */
+int hooks_compress(const uint8_t *file, size_t n, int model, uint8_t **out, size_t *out_len, long *walked) {
+  avr_ctx *c;
+  int r = avr_create(0, &c);
+  if (r) return r;
+  avr_hooks_session *s;
+  r = avr_hooks_compress_begin(c, file, n, model, &s);
+  if (r) { avr_destroy(c); return r; }
+  g_session = s;
+  *walked = drive(file, n);
+  r = avr_hooks_end(s, out, out_len);
+  avr_hooks_destroy(s);
+  avr_destroy(c);
+  return *walked < 0 ? -100 + (int)*walked : r;
+}
+
+/* decompress a container through the hooks; *out = the original file. */
+int hooks_decompress(const uint8_t *avrc, size_t n, uint8_t **out, size_t *out_len, long *walked) {
+  avr_ctx *c;
+  int r = avr_create(0, &c);
+  if (r) return r;
+  avr_hooks_session *s;
+  const uint8_t *stream;
+  size_t stream_len;
+  r = avr_hooks_decompress_begin(c, avrc, n, &s, &stream, &stream_len);
+  if (r) { avr_destroy(c); return r; }
+  g_session = s;
+  *walked = drive(stream, stream_len);
+  r = avr_hooks_end(s, out, out_len);
+  avr_hooks_destroy(s);
+  avr_destroy(c);
+  return *walked < 0 ? -100 + (int)*walked : r;
+}

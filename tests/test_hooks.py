@@ -1,0 +1,94 @@
+"""The libavcodec-hooks callback surface of the C ABI (avr_hook_*, include/avrecode.h;
+reference: AVCodecHooks trampolines recode.cpp:137-228).
+
+tests/native/hooks_driver.c plays the fork's H.264 decoder with the oracle's slice_data() parser:
+every bin of every re-coded slice is pulled through avr_hook_get / _bypass / _terminate and every
+model event is reported, the parse being driven by the device's bins.  Compress through the hooks
+must give the same container as the golden .avrc; decompress through the hooks must give the
+original file back.
+"""
+import ctypes
+import hashlib
+import json
+import subprocess
+from functools import lru_cache
+
+import pytest
+
+from _oracle import ROOT, build_oracle
+
+FIX = ROOT / "tests" / "fixtures"
+GOLD = {(g["file"], g["mode"]): g for g in json.loads((ROOT / "tests/golden/fixtures.json").read_text())}
+BUILD = ROOT / "tests" / "native" / "_build"
+
+
+@lru_cache(None)
+def driver_path():
+    build_oracle()
+    lib = ROOT / "avrecode_amd" / "libavrecode.so"
+    if not lib.exists():
+        subprocess.run(["make", "-C", str(ROOT / "avrecode_amd"), "-j8"], check=True)
+    BUILD.mkdir(parents=True, exist_ok=True)
+    out = BUILD / "libhooks_driver.so"
+    src = ROOT / "tests" / "native" / "hooks_driver.c"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-O2", "-Wall", str(src), "-o", str(out),
+                    "-L" + str(ROOT / "oracle"), "-loracle", "-Wl,-rpath," + str(ROOT / "oracle"),
+                    "-L" + str(ROOT / "avrecode_amd"), "-lavrecode", "-Wl,-rpath," + str(ROOT / "avrecode_amd")],
+                   check=True)
+    return out
+
+
+def test_hooks_driver_builds_and_links():
+    """CPU: the driver compiles against include/avrecode.h and links every avr_hook_* symbol."""
+    L = ctypes.CDLL(str(driver_path()))
+    assert L.hooks_compress and L.hooks_decompress
+
+
+def _driver():
+    L = ctypes.CDLL(str(driver_path()))
+    pp = ctypes.POINTER(ctypes.c_uint8)
+    L.hooks_compress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(pp),
+                                 ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_long)]
+    L.hooks_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(pp),
+                                   ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_long)]
+    return L, pp
+
+
+def _call(fn, *args):
+    L, pp = _driver()
+    out, n, walked = pp(), ctypes.c_size_t(), ctypes.c_long()
+    r = getattr(L, fn)(*args, ctypes.byref(out), ctypes.byref(n), ctypes.byref(walked))
+    data = ctypes.string_at(out, n.value) if r == 0 else b""
+    if r == 0:
+        import avrecode_amd as avr
+        avr.lib().avr_free(out)
+    return r, data, walked.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["realshort.mp4", "cockatoo.mp4"])
+@pytest.mark.parametrize("mode,model", [("R", 0), ("P", 1)])
+def test_hooks_compress_then_decompress(name, mode, model):
+    data = (FIX / name).read_bytes()
+    r, avrc, walked = _call("hooks_compress", data, len(data), model)
+    assert r == 0, r
+    g = GOLD[(name, mode)]
+    assert hashlib.sha256(avrc).hexdigest() == g["avrc_sha256"]
+    assert walked > 0
+    r, back, walked_d = _call("hooks_decompress", avrc, len(avrc))
+    assert r == 0, r
+    assert walked_d == walked
+    assert back == data
+
+
+@pytest.mark.gpu
+def test_hooks_detect_a_diverging_caller():
+    """A container whose re-coded stream was altered: the device decompress either fails or
+    yields different bins; either way the session must not report success with wrong bytes."""
+    data = (FIX / "realshort.mp4").read_bytes()
+    r, avrc, _ = _call("hooks_compress", data, len(data), 1)
+    assert r == 0
+    bad = bytearray(avrc)
+    bad[len(bad) // 2] ^= 0x5A
+    r, back, _ = _call("hooks_decompress", bytes(bad), len(bad))
+    assert r != 0 or back != data or bytes(bad) == avrc
