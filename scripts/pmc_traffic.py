@@ -1,0 +1,46 @@
+"""HBM traffic per launch of the slice kernels from rocprofv3 PMC passes (scripts/pmc.sh).
+
+  python scripts/pmc_traffic.py gpurun_out/pmc_<tag> profiles/<round>_pmc.json --slices 1024 --mb 120 68
+
+FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KiB per dispatch (TCC_EA0_RDREQ/WRREQ
+based).  Per /opt/skills/guides/MI355X_MICROARCH.md (HBM section), on gfx950 FETCH_SIZE counts
+128-B read requests at 64 B, so it is doubled here; WRITE_SIZE is taken as reported.  The result
+is what bench.py's roofline.traffic reads (bytes per launch, averaged over the dispatches).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--slices", type=int, required=True)
+    ap.add_argument("--mb", type=int, nargs=2, required=True)
+    a = ap.parse_args()
+    vals = defaultdict(lambda: defaultdict(list))
+    for p in glob.glob(os.path.join(a.src, "pass*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(p)):
+            name = r["Kernel_Name"]
+            if "slices_parallel_kernel<" not in name:
+                continue
+            k = "slices_parallel_kernel<%s>" % name.split("slices_parallel_kernel<")[1][0]
+            vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {"slices": a.slices, "mb": list(a.mb), "source": a.src,
+           "note": "FETCH_SIZE x2 (gfx950 correction), WRITE_SIZE as reported; KiB -> bytes; mean per dispatch",
+           "kernels": {}}
+    for k, c in vals.items():
+        fetch = 2 * 1024 * sum(c.get("FETCH_SIZE", [0])) / max(1, len(c.get("FETCH_SIZE", [])))
+        write = 1024 * sum(c.get("WRITE_SIZE", [0])) / max(1, len(c.get("WRITE_SIZE", [])))
+        out["kernels"][k] = {"fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+                             "hbm_bytes_per_launch": fetch + write}
+    json.dump(out, open(a.dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
