@@ -20,7 +20,8 @@ decompress the reverse) over its average launch time from HIP events on the laun
 traffic: HBM bytes per launch of that kernel from rocprofv3 FETCH_SIZE/WRITE_SIZE passes
 (profiles/<round>_pmc.json, written by scripts/pmc_traffic.py), or null.
 cpu_baseline: the oracle (CPU restatement of the reference algorithm, oracle/) compress +
-decompress of the first slices of the same batch on one host core, ~10-20 s.
+decompress of the first slices of the same batch on one host core (value), and on all host
+threads (all_cores), ~10-30 s.
 """
 import argparse
 import json
@@ -54,8 +55,19 @@ def make_input(ctx, n, rank, args):
     return b"".join(parts)
 
 
+def cpu_threads():
+    """Host threads the CPU baseline may use: the process's CPU affinity, capped by the job's
+    thread budget (OMP_NUM_THREADS is 16 on the GPU box, a one-GPU share of the node)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
+
+
 def cpu_baseline(ctx, args, n_bytes_hint):
-    """Oracle P-mode compress+decompress of the first slices of the same batch, one core."""
+    """Oracle (CPU restatement of the reference, fresh model per slice) compress+decompress of the
+    first slices of the same batch: on one core (the reference's own thread_count = 1,
+    recode.cpp:122), and on all host threads, one slice per task (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, str(ROOT / "tests"))
     import _oracle
     _oracle.build_oracle()
@@ -73,9 +85,23 @@ def cpu_baseline(ctx, args, n_bytes_hint):
         if dt >= t_budget * 0.5 or k >= 64:
             break
         k = max(k + 1, min(64, int(k * t_budget / max(dt, 1e-3))))
-    return {"value": total_bytes / total_t / 1e6, "unit": "MB/s", "cores": 1, "kind": "port",
+    line = {"value": total_bytes / total_t / 1e6, "unit": "MB/s", "cores": 1, "kind": "port",
             "sample": f"first {slices} slices of the batch ({k} per QP group, {total_bytes} input bytes), oracle "
                       f"fresh-model compress+decompress, {total_t:.1f} s"}
+    # all host threads: the same per-slice work over a sample of >= 2 slices per thread
+    nt = cpu_threads()
+    if nt > 1:
+        per = max(1, -(-2 * nt // 3))
+        big = b"".join(ctx.synthesize(synth_params(qp, args.seed + j, args), per) for j, qp in enumerate(QPS))
+        n = 3 * per
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(nt) as ex:
+            outs = list(ex.map(lambda i: _oracle.slices_p(big, i, i + 1, check_recodable=False)[1], range(n)))
+        dt = time.perf_counter() - t0
+        assert all(r["status_c"] == 0 and r["status_d"] == 0 for o in outs for r in o)
+        line["all_cores"] = {"value": len(big) / dt / 1e6, "unit": "MB/s", "cores": nt,
+                             "sample": f"{n} slices ({len(big)} input bytes), one slice per task, {dt:.1f} s"}
+    return line
 
 
 def load_traffic(args, kernel):
