@@ -1261,6 +1261,11 @@ AVR_FI void walker_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uin
   }
 }
 
+AVR_FI uint32_t vgpr_zero() {
+  uint32_t z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
 AVR_FI uint64_t readlane64(uint64_t v, uint32_t j) {
   const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j);
   const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
@@ -1330,8 +1335,15 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
   RecodedEncoder re;
   CabacEncoder ce;
   VTab vt;
-  if (MODE == MODE_COMPRESS) re_init(re);
-  else {
+  if (MODE == MODE_COMPRESS) {
+    re_init(re);
+    // Keep the coder's interval in VGPRs: every wave of the CU shares one scalar unit, and the
+    // walker wave (the critical path) is scalar-bound; 64-bit multiply-adds are also cheaper on
+    // the vector unit (v_mad_u64_u32).  A value the compiler cannot prove uniform stays vector.
+    const uint32_t z = vgpr_zero();
+    re.range += z;
+    re.low += z;
+  } else {
     ce_init(ce);
     vtab_load(vt, T);
   }
@@ -1348,6 +1360,7 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
       const uint32_t tot_v = (op_v >> 8) & 127;
       const uint64_t m_v = T->div[tot_v][0];
       const uint32_t s_v = (uint32_t)T->div[tot_v][1];
+      asm volatile("; MARK_CODER_BEGIN");
       for (uint32_t j = 0; j < n; j++) {
         const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
         if (op & OP_END) { done = true; break; }
@@ -1357,6 +1370,7 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
         const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
         re_put(re, o, op & 1, p1);
       }
+      asm volatile("; MARK_CODER_END");
     } else {
       for (uint32_t j = 0; j < n; j++) {
         const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
