@@ -366,6 +366,29 @@ __device__ __forceinline__ void ce_terminate(CabacEncoder& e, OutStream& o, int 
 __device__ __forceinline__ uint64_t rc_div(uint64_t range, uint32_t d, const HotTables* T) {
   return __umul64hi(range, T->div[d][0]) >> (uint32_t)T->div[d][1];
 }
+// The reciprocal table in six VGPRs (lane j: divisors j and 64 + j): a lookup with a uniform
+// divisor is three v_readlane pairs and scalar selects, no LDS round trip.
+struct VDiv {
+  uint32_t mlo0, mhi0, sh0, mlo1, mhi1, sh1;
+};
+__device__ __forceinline__ void vdiv_load(VDiv& v, const HotTables* T) {
+  const uint32_t j = __lane_id();
+  v.mlo0 = (uint32_t)T->div[j][0];
+  v.mhi0 = (uint32_t)(T->div[j][0] >> 32);
+  v.sh0 = (uint32_t)T->div[j][1];
+  v.mlo1 = (uint32_t)T->div[64 + j][0];
+  v.mhi1 = (uint32_t)(T->div[64 + j][0] >> 32);
+  v.sh1 = (uint32_t)T->div[64 + j][1];
+}
+__device__ __forceinline__ uint32_t sel32(uint32_t a, uint32_t b, uint32_t m) { return a ^ ((a ^ b) & m); }
+__device__ __forceinline__ uint64_t rc_p1v(uint64_t range, uint32_t est, const VDiv& v) {
+  const uint32_t pos = (est & 0xff) + 1, tot = pos + (est >> 8) + 1;
+  const uint32_t j = tot & 63, m = 0u - (tot >> 6);
+  const uint32_t mlo = sel32(__builtin_amdgcn_readlane(v.mlo0, j), __builtin_amdgcn_readlane(v.mlo1, j), m);
+  const uint32_t mhi = sel32(__builtin_amdgcn_readlane(v.mhi0, j), __builtin_amdgcn_readlane(v.mhi1, j), m);
+  const uint32_t sh = sel32(__builtin_amdgcn_readlane(v.sh0, j), __builtin_amdgcn_readlane(v.sh1, j), m);
+  return (__umul64hi(range, (uint64_t)mhi << 32 | mlo) >> sh) * pos;
+}
 // p1 = (range/(pos+neg))*pos  (recode.cpp:819); est = (pos-1) | (neg-1) << 8
 __device__ __forceinline__ uint64_t rc_p1(uint64_t range, uint32_t est, const HotTables* T) {
   const uint32_t pos = (est & 0xff) + 1, tot = pos + (est >> 8) + 1;
@@ -452,7 +475,9 @@ struct RecodedDecoder {
   uint32_t next;        // next byte index
 };
 __device__ __forceinline__ void rd_consume(RecodedDecoder& d, InStream& in) {
-  uint32_t b = in_byte(in, d.next++);
+  // the byte comes from LDS in a vector register: move it to a scalar one so that low stays a
+  // scalar register (otherwise every bin pays vector<->scalar transfers on low)
+  uint32_t b = __builtin_amdgcn_readfirstlane(in_byte(in, d.next++));
   uint32_t digit = ((d.next_digit & 1) << 7) | (b >> 1);
   d.next_digit = b;
   d.low = (d.low << 8) | digit;

@@ -277,6 +277,7 @@ struct Walker {
   int nref0, nref1, d8x8inf, x264_build, first_mb;
   RingOut ring0;          // walker -> modeler (compress) / coder (decompress)
   VTab vt;                // CABAC state records (compress / generate: the walker's engine)
+  VDiv vd;                // reciprocals (decompress: the walker's recoded decoder)
 
   // ------------------------------------------------------------------ residual context registers
   // The residual contexts of one ctxBlockCat (significant_coeff_flag lanes 0-15,
@@ -331,7 +332,7 @@ struct Walker {
     } else if (MODE == MODE_DECOMPRESS) {
       bins++;
       const uint32_t e = __builtin_amdgcn_readlane(rc_v, L);
-      const int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      const int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
       rc_v = wlane(rc_v, L, est_update(e, b, 0x60));
       push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
       return b;
@@ -366,7 +367,7 @@ struct Walker {
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[ctx];
-      const int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      const int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
       sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
       push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
       return b;
@@ -385,7 +386,7 @@ struct Walker {
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1024];
-      const int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      const int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
       sh->est[1024] = (uint16_t)est_update(e, b, 0x60);
       push((uint32_t)b | OPK_BYPASS << 1);
       return b;
@@ -408,7 +409,7 @@ struct Walker {
       }
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1025];
-      b = rd_get(rd, in, rc_p1(rd.range, e, T));
+      b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
       sh->est[1025] = (uint16_t)est_update(e, b, 0x60);
       push((uint32_t)b | OPK_TERMINATE << 1);
     } else {
@@ -515,7 +516,7 @@ struct Walker {
       } else {
         uint32_t slot;
         const uint32_t e = est_load(sh, est_g, idx, &slot);
-        b = rd_get(rd, in, rc_p1(rd.range, e, T));
+        b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
         est_store(sh, idx, slot, est_update(e, b, 0x60));
       }
       if (b) so_far |= cur_bit;
@@ -580,7 +581,7 @@ struct Walker {
         int idx = sig_est_index(cat, max, is_dc, c422, pos, nnz_m, cnt);
         uint32_t slot;
         uint32_t e = est_load(sh, est_g, idx, &slot);
-        int b = rd_get(rd, in, rc_p1(rd.range, e, T));
+        int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
         est_store(sh, idx, slot, est_update(e, b, 0x50));
         bins++;
         push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3);
@@ -1193,6 +1194,7 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   w.out.last = 0;
   w.ring0.init(w.sh, 0);
   vtab_load(w.vt, w.T);
+  if (MODE == MODE_DECOMPRESS) vdiv_load(w.vd, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
   if (MODE == MODE_COMPRESS || MODE == MODE_TRACE) {
