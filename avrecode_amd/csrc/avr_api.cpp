@@ -30,12 +30,15 @@ namespace {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  hipError_t reserve(size_t n) {
+  // zero: a fresh allocation starts zeroed (the estimator tables rely on it, see kEstDirty)
+  hipError_t reserve(size_t n, bool zero = false) {
     if (n <= cap) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
     hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess && zero) e = hipMemset(p, 0, n);
+    if (e == hipSuccess && zero) e = hipDeviceSynchronize();
     if (e == hipSuccess) cap = n;
     return e;
   }
@@ -240,7 +243,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
   HIP_TRY(c, hipMemcpyAsync(c->descs.p, plan.descs.data(), sizeof(avr_slice_desc) * n, hipMemcpyHostToDevice,
                             c->stream));
   if (sequential) {
-    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * avr::kEstGlobal));
+    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * avr::kEstGlobal, true));
     size_t fbytes = 0;
     for (auto& d : plan.descs) fbytes = std::max(fbytes, (size_t)2 * d.mb_width * d.mb_height * 52);
     HIP_TRY(c, c->frames.reserve(fbytes + 64));
@@ -250,7 +253,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
                                   c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), c->stream));
   } else {
     const int chunk = std::min(n, kMaxSlicesPerLaunch);
-    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk));
+    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk, true));
     for (int s0 = 0; s0 < n; s0 += chunk) {
       const int m = std::min(chunk, n - s0);
       HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>() + s0,
@@ -638,7 +641,7 @@ static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int 
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = (hipStream_t)stream;
   if (model == AVR_MODEL_REFERENCE) {
-    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * avr::kEstGlobal));
+    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * avr::kEstGlobal, true));
     HIP_TRY(c, c->frames.reserve((size_t)2 * max_w * max_h * 52 + 64));
     HIP_TRY(c, c->frame_meta.reserve(64));
     HIP_TRY(c, avr::launch_slices(mode, true, c->tables.as<avr::EngineTables>(), d_desc, n, max_w, d_in, d_out, d_res,
@@ -646,7 +649,7 @@ static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int 
     return AVR_OK;
   }
   const int chunk = std::max(1, std::min(n, kMaxSlicesPerLaunch));
-  HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk));
+  HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk, true));
   for (int s0 = 0; s0 < n; s0 += chunk) {
     const int m = std::min(chunk, n - s0);
     HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), d_desc + s0, m, max_w, d_in, d_out,

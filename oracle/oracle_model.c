@@ -9,6 +9,7 @@
  *      entries get_neighbor_sub_mb can reach are identical;
  *  (3) decompress side only: the nnz-bit key uses is_8x8 || size > 32 (see model_finished_queueing).
  */
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -93,7 +94,9 @@ static mbblock_t *model_block(avr_model_t *m, int x, int y) {
   return &f->image[x + y * f->width];
 }
 
+static FILE *keylog_file(void);
 avr_model_t *avr_model_new(void) {
+  if (keylog_file()) { model_key_t mark = ~(model_key_t)0; fwrite(&mark, sizeof(mark), 1, keylog_file()); }
   avr_model_t *m = (avr_model_t *)calloc(1, sizeof(avr_model_t));
   m->coding_type = PIP_UNKNOWN;
   m->sub_mb_cat = -1;
@@ -191,8 +194,23 @@ model_key_t model_get_key(avr_model_t *m, int ctx_kind) {
   }
 }
 
+/* Analysis aid (test infrastructure): AVR_ORACLE_KEYLOG=<file> appends every probability query's
+ * model key (u64) to <file>; used offline to size the device's estimator cache. */
+static FILE *keylog_file(void) {
+  static int init;
+  static FILE *f;
+  if (!init) {
+    init = 1;
+    const char *p = getenv("AVR_ORACLE_KEYLOG");
+    if (p && *p) f = fopen(p, "wb");
+  }
+  return f;
+}
+
 /* probability_for_model_key (816-820) */
 uint64_t model_p1(avr_model_t *m, uint64_t range, model_key_t key) {
+  FILE *kl = keylog_file();
+  if (kl) fwrite(&key, sizeof(key), 1, kl);
   estimator_t *e = estimator(m, key);
   return rc_p1(range, e->pos, e->neg);
 }
