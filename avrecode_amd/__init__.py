@@ -25,7 +25,8 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-library_path = os.path.join(_HERE, "libavrecode.so")
+# AVR_LIBRARY selects an instrumented build (e.g. prof/libavrecode.so, `make -C avrecode_amd prof`)
+library_path = os.environ.get("AVR_LIBRARY") or os.path.join(_HERE, "libavrecode.so")
 
 MODEL_REFERENCE = 0
 MODEL_PARALLEL = 1

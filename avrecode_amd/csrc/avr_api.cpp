@@ -30,7 +30,7 @@ namespace {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  // zero: a fresh allocation starts zeroed (the estimator tables rely on it, see kEstDirty)
+  // zero: a fresh allocation starts zeroed (the estimator tables rely on it, see kEstLogN)
   hipError_t reserve(size_t n, bool zero = false) {
     if (n <= cap) return hipSuccess;
     if (p) (void)hipFree(p);
@@ -801,6 +801,13 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
 
 // Debug only (not part of include/avrecode.h): section cycle counters (32 slots) of an AVR_PROFILE build of
 // the parallel kernels (mode 0 compress, 1 decompress, 2 generate), read and cleared.
+// Diagnostic (AVR_PROFILE builds): 8 u32 per slice of the last parallel compress (mode 0) or
+// decompress (1) launch: HW_ID of waves 0-2, XCC_ID, walker start/end cycle counters.
+extern "C" int avr_debug_placement(int mode, uint32_t* out8n, int n) {
+  hipError_t e = mode == 0 ? avr::placement_parallel_compress(out8n, n) : avr::placement_parallel_decompress(out8n, n);
+  return e == hipSuccess ? AVR_OK : AVR_ERR_DEVICE;
+}
+
 extern "C" int avr_debug_profile(int mode, unsigned long long* out16) {
   hipError_t e = mode == 0 ? avr::profile_parallel_compress(out16)
                : mode == 1 ? avr::profile_parallel_decompress(out16)

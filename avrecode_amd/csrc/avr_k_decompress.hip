@@ -22,4 +22,15 @@ hipError_t profile_parallel_decompress(unsigned long long* out16) {
 #endif
 }
 
+// AVR_PROFILE builds: per-slice wave placement (see avr_place); zeros otherwise.
+hipError_t placement_parallel_decompress(uint32_t* out, int n) {
+  if (n > 4096) n = 4096;
+#ifdef AVR_PROFILE
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(avr_place), sizeof(uint32_t) * 8 * n);
+#else
+  for (int i = 0; i < 8 * n; i++) out[i] = 0;
+  return hipSuccess;
+#endif
+}
+
 }  // namespace avr

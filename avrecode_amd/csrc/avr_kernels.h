@@ -10,8 +10,16 @@ namespace avr {
 
 struct EngineTables;
 
-// dense SIG + NZ estimator entries per model instance (u16 each), see avr_kernels.hip
-constexpr int kEstGlobal = 294016;
+// Per model instance (u16 units): the dense SIG + NZ estimator table (kEstTable entries), then
+// the write log that lets the next user clear only what was written (see avr_walker.h): a u32
+// count at kEstLogN (kEstLogOverflow: clear the whole table) and kEstLogCap u32 entry indices.
+constexpr int kEstTable = 294016;
+constexpr int kEstLogN = kEstTable;
+constexpr int kEstLog = kEstTable + 2;
+constexpr int kEstLogCap = 8191;
+constexpr uint32_t kEstLogOverflow = 0xffffffffu;
+constexpr int kEstGlobal = kEstLog + 2 * kEstLogCap;
+static_assert(kEstGlobal % 8 == 0 && kEstTable % 8 == 0, "16-byte clears");
 
 size_t shared_bytes(int max_mb_width);
 // mode: 0 compress, 1 decompress, 2 generate, 3 trace (decode-only bin trace).  sequential = reference model (single wavefront).
@@ -39,6 +47,8 @@ hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_d
                                         uint8_t* frames, int* frame_meta, hipStream_t stream);
 // section cycle counters of AVR_PROFILE builds (avr_walker.h); zeros otherwise
 hipError_t profile_parallel_compress(unsigned long long* out16);
+hipError_t placement_parallel_compress(uint32_t* out8n, int n);
+hipError_t placement_parallel_decompress(uint32_t* out8n, int n);
 hipError_t profile_parallel_decompress(unsigned long long* out16);
 hipError_t profile_parallel_generate(unsigned long long* out16);
 hipError_t profile_parallel_trace(unsigned long long* out16);

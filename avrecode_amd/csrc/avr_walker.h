@@ -46,6 +46,23 @@ namespace avr {
 
 #ifdef AVR_PROFILE
 static __device__ unsigned long long avr_prof[32];
+// wave placement per slice (AVR_PROFILE builds): HW_ID of waves 0..2, XCC_ID, walker start / end
+// (s_memtime low 32 bits), walker start / end (s_memrealtime, 100 MHz) -- scripts/placement.py
+constexpr int kPlaceSlices = 4096;
+static __device__ uint32_t avr_place[kPlaceSlices][8];
+AVR_FI void record_placement(int s, int wave) {
+  if (s < kPlaceSlices && __lane_id() == 0) {
+    avr_place[s][wave] = __builtin_amdgcn_s_getreg(4 | (31 << 11));        // HW_REG_HW_ID
+    if (wave == 0) avr_place[s][3] = __builtin_amdgcn_s_getreg(20 | (15 << 11));  // HW_REG_XCC_ID
+  }
+}
+#define AVR_PLACE(s, wave) record_placement(s, wave)
+#define AVR_PLACE_T(s, k) if ((s) < kPlaceSlices && __lane_id() == 0) { \
+    avr_place[s][4 + (k)] = (uint32_t)__builtin_readcyclecounter(); \
+    avr_place[s][6 + (k)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+#else
+#define AVR_PLACE(s, wave)
+#define AVR_PLACE_T(s, k)
 #endif
 
 // MODE_TRACE: the compress-side CABAC decode + parse alone, recording every bin in decode order
@@ -68,7 +85,7 @@ static __constant__ uint8_t c_b_pairs[9][2] = {{1, 1}, {2, 2}, {1, 2}, {2, 1}, {
 constexpr int kSigEst = 229376;
 constexpr int kNzEst = 63 * 2 * 3 * 3 * 57;
 constexpr int kEstDefault = 1026;
-static_assert(kEstGlobal >= kSigEst + kNzEst, "estimator table size");
+static_assert(kEstTable >= kSigEst + kNzEst, "estimator table size");
 
 struct MbRec {
   uint8_t flags, is8x8;
@@ -93,7 +110,7 @@ static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
 
 // LDS layout (per workgroup = one slice); the ring is sized by mb_width at launch.
 // SIG + NZ estimators: an LDS hash table (4096 slots, 16 KB) in front of the dense per-model
-// table in HBM (kEstGlobal u16 entries).  A slice touches ~3.5-5.5 K distinct SIG/NZ keys out of
+// table in HBM (kEstTable u16 entries).  A slice touches ~3.5-5.5 K distinct SIG/NZ keys out of
 // 294 K, so the first ones seen get an LDS slot for the rest of the model's life and only the
 // keys that find their probe window full live in HBM (0.4 % of lookups at QP 22, none at QP 30,
 // vs ~11 % misses for the direct-mapped write-back cache this replaces).  Keys never leave the
@@ -102,13 +119,15 @@ static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
 //   key p = idx * kEstKeyMul mod 2^19 (a bijection), home slot p >> 7, tag p & 127; one probe is
 //   one LDS read per lane over the 64 slots home .. home + 63; slot = (0x8000 | disp << 7 | tag)
 //   << 16 | estimator, 0 = free.
-// The HBM table is cleared lazily: kEstDirty is set when an estimator is written there and the
-// next model using that table clears it first.
+// The HBM table is cleared lazily and sparsely: an entry stored there carries bit 15 (estimators
+// use 15 bits: neg - 1 <= 0x60), so its first store is recognised and its index appended to the
+// table's write log; the next model using the table zeroes the logged entries (the whole table
+// only if the log overflowed) instead of clearing 588 KB per slice.
 constexpr int kEtabBits = 12;
 constexpr int kEtabSize = 1 << kEtabBits;
 constexpr uint32_t kEstKeyMul = 0x4F1BBu;   // odd: multiplication mod 2^19 is a bijection
-constexpr int kEstDirty = kEstGlobal - 1;
-static_assert(kEstGlobal < (1 << 19) && kEstDirty >= kSigEst + kNzEst, "estimator key space");
+constexpr uint32_t kEstWritten = 0x8000u;
+static_assert(kEstTable < (1 << 19), "estimator key space");
 
 // Producer -> consumer ring of coding operations (see "Two waves per slice" below).
 constexpr int kFifo = 512;
@@ -119,6 +138,9 @@ struct Shared {
   uint32_t fifo_head[2];     // operations published by the ring's producer (monotonic)
   uint32_t fifo_tail[2];     // operations retired by the ring's consumer (monotonic)
   int32_t p_status, p_stop_ok, c_err;  // slice results of the two waves
+  uint32_t elog_n;           // entries appended to the HBM table's write log by this model
+  uint32_t prio_max;         // largest input (payload) size of the batch
+  uint32_t prio;             // the slice's current wave priority (walker -> modeler / coder)
   uint32_t c_len, c_last;
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
   uint8_t state[1024];
@@ -181,6 +203,27 @@ AVR_FI void st_volatile(uint32_t* p, uint32_t v) {
 AVR_FI void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
+}
+
+// Wave priority (s_setprio): the SQ issues from higher-priority waves first, then the oldest.
+// A batch's time is its longest slice's, and the slices sharing a CU compete for the issue slots,
+// so every wave of a slice runs at a priority that grows with the slice's remaining input
+// (longest-remaining-first); the walker sets it once per macroblock and publishes it in LDS,
+// the modeler and coder follow it once per ring batch.
+AVR_FI void set_prio(uint32_t p) {
+  switch (p) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+}
+AVR_FI void follow_prio(Shared* sh, uint32_t* cur) {
+  const uint32_t p = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->prio);
+  if (p != *cur) {
+    *cur = p;
+    set_prio(p);
+  }
 }
 
 // Producer end of ring r: entries go to LDS at once, the head counter every 32 entries (and on
@@ -260,16 +303,42 @@ AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32
     *slot = (0x8000u | j << 7 | tag) << 16 | ((home + j) & (kEtabSize - 1));
     return 0;
   }
-  *slot = 0;
-  return __builtin_amdgcn_readfirstlane(est_g[idx]);
+  // HBM: slot 1 marks the entry's first store (to be logged), 0 a stored one
+  const uint32_t raw = __builtin_amdgcn_readfirstlane(est_g[idx]);
+  *slot = (raw & kEstWritten) ? 0u : 1u;
+  return raw & (kEstWritten - 1);
 }
 AVR_FI void est_store(Shared* sh, uint16_t* est_g, uint32_t idx, uint32_t slot, uint32_t e) {
-  if (slot) {
+  if (slot >> 31) {
     sh->etab[slot & (kEtabSize - 1)] = (slot & 0xffff0000u) | e;
   } else if (__lane_id() == 0) {
-    est_g[idx] = (uint16_t)e;
-    est_g[kEstDirty] = 1;
+    est_g[idx] = (uint16_t)(e | kEstWritten);
+    if (slot) {
+      const uint32_t n = sh->elog_n;
+      sh->elog_n = n + 1;
+      uint32_t* lg = (uint32_t*)(est_g + kEstLog);
+      if (n < (uint32_t)kEstLogCap) lg[n] = idx;
+      *(uint32_t*)(est_g + kEstLogN) = n < (uint32_t)kEstLogCap ? n + 1 : kEstLogOverflow;
+    }
   }
+}
+// A fresh model on a table the last model may have written: zero the logged entries (or the
+// whole table), reset the log.  Called by the whole workgroup; ends with a barrier.
+AVR_FI void est_table_reset(uint16_t* est_g, Shared* sh) {
+  const uint32_t n = *(volatile uint32_t*)(est_g + kEstLogN);
+  __syncthreads();   // every thread has read the count before it is reset
+  if (n == kEstLogOverflow) {
+    uint4* e4 = (uint4*)est_g;
+    for (int i = threadIdx.x; i < kEstTable / 8; i += blockDim.x) e4[i] = make_uint4(0, 0, 0, 0);
+  } else if (n) {
+    const uint32_t* lg = (const uint32_t*)(est_g + kEstLog);
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) est_g[lg[i]] = 0;
+  }
+  if (threadIdx.x == 0) {
+    *(uint32_t*)(est_g + kEstLogN) = 0;
+    sh->elog_n = 0;
+  }
+  __syncthreads();
 }
 
 template <int MODE, bool RM>
@@ -298,6 +367,18 @@ struct Walker {
   uint32_t bins;
   int target_mbs, mbs_done, last_mb;
   int nref0, nref1, d8x8inf, x264_build, first_mb;
+  uint32_t prio_t1, prio_t2, prio_t3, prio_cur;   // remaining-input thresholds (1/4, 1/2, 3/4 of the batch's largest)
+  AVR_FI void update_prio() {
+    const uint32_t pos = MODE == MODE_DECOMPRESS ? rd.next : cd.next;
+    const uint32_t size = d->payload_size;
+    const uint32_t rem = pos < size ? size - pos : 0u;
+    const uint32_t p = (rem > prio_t1 ? 1u : 0u) + (rem > prio_t2 ? 1u : 0u) + (rem > prio_t3 ? 1u : 0u);
+    if (p != prio_cur) {
+      prio_cur = p;
+      set_prio(p);
+      if (__lane_id() == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->prio = p;
+    }
+  }
   RingOut ring0;          // walker -> modeler (compress) / coder (decompress)
   VTab vt;                // CABAC state records (compress / generate: the walker's engine)
   VDiv vd;                // reciprocals (decompress: the walker's recoded decoder)
@@ -1200,7 +1281,10 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
       wave_sync();
     }
     PROF_ENDW(7, t7);
-    if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) w.publish();
+    if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) {
+      w.publish();
+      if (!RM) w.update_prio();
+    }
     if (w.terminate(SE_EOS)) break;
     if (Walker<MODE, RM>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
     addr++;
@@ -1224,6 +1308,13 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   if (MODE == MODE_DECOMPRESS) vdiv_load(w.vd, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
+  {
+    const uint32_t m = w.sh->prio_max;
+    w.prio_t1 = m >> 2;
+    w.prio_t2 = m >> 1;
+    w.prio_t3 = m - (m >> 2);
+    w.prio_cur = 0xffffffffu;   // set on the first macroblock
+  }
   if (MODE == MODE_COMPRESS || MODE == MODE_TRACE) {
     cd_init(w.cd, w.in);
   } else if (MODE == MODE_DECOMPRESS) {
@@ -1312,9 +1403,11 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
 #ifdef AVR_PROFILE
   const uint64_t t_start = PROF_T();
 #endif
+  uint32_t prio = 0;
   for (bool done = false; !done;) {
     uint32_t op_v;
     const uint32_t n = ring_take(sh, 0, tail, &op_v, &waited);
+    follow_prio(sh, &prio);
     asm volatile("; MARK_MODEL_BEGIN");
     for (uint32_t j = 0; j < n; j++) {
       const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
@@ -1382,9 +1475,11 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
 #ifdef AVR_PROFILE
   const uint64_t t_start = PROF_T();
 #endif
+  uint32_t prio = 0;
   for (bool done = false; !done;) {
     uint32_t op_v;
     const uint32_t n = ring_take(sh, r, tail, &op_v, &waited);
+    follow_prio(sh, &prio);
     if (MODE == MODE_COMPRESS) {
       const uint32_t tot_v = (op_v >> 8) & 127;
       const uint64_t m_v = T->div[tot_v][0];
@@ -1474,7 +1569,7 @@ constexpr int slice_threads() {
 }
 
 template <int MODE>
-__global__ __launch_bounds__(192, 3) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+__global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                 const uint8_t* in, uint8_t* out, avr_slice_result* res,
                                                                 uint16_t* est_scratch) {
   extern __shared__ __align__(16) uint8_t smem[];
@@ -1499,25 +1594,32 @@ __global__ __launch_bounds__(192, 3) void slices_parallel_kernel(const EngineTab
     }
     return;
   }
-  // fresh model for this slice: clear the dense SIG/NZ estimators if the last model that used
-  // this table wrote any (16 B per thread per step)
-  if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) {
-    const bool dirty = w.est_g[kEstDirty] != 0;
-    __syncthreads();   // every thread has read the flag before any clears it
-    if (dirty) {
-      uint4* e4 = (uint4*)w.est_g;
-      for (int i = threadIdx.x; i < kEstGlobal / 8; i += blockDim.x) e4[i] = make_uint4(0, 0, 0, 0);
-    }
-  }
+  // fresh model for this slice: undo the last model's stores to the HBM estimator table
+  if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) est_table_reset(w.est_g, w.sh);
   w.d = d;
   w.W = d->mb_width;
+  if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) {
+    if (threadIdx.x == 0) {
+      w.sh->prio_max = 0;
+      w.sh->prio = 0;
+    }
+    __syncthreads();
+    uint32_t m = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = max(m, descs[i].payload_size);
+    atomicMax(&w.sh->prio_max, m);   // visible after init_slice_state's barrier
+  }
   init_slice_state(w, G);
   if (MODE == MODE_GENERATE || MODE == MODE_TRACE) {
     run_slice_inline(w, d, in, out, &res[s]);
     return;
   }
   const int wave = threadIdx.x >> 6;
-  if (wave == 0) walker_slice(w, d, in, &res[s]);
+  AVR_PLACE(s, wave);
+  if (wave == 0) {
+    AVR_PLACE_T(s, 0);
+    walker_slice(w, d, in, &res[s]);
+    AVR_PLACE_T(s, 1);
+  }
   else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
   else coder_slice<MODE>(w.sh, w.T, d, out);
   __syncthreads();
@@ -1545,6 +1647,11 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
   {
     uint4* e4 = (uint4*)est_g;
     for (int i = tid; i < kEstGlobal / 8; i += nt) e4[i] = make_uint4(0, 0, 0, 0);
+    if (tid == 0) {
+      w.sh->elog_n = 0;
+      w.sh->prio = 0;
+      w.sh->prio_max = 0;
+    }
     for (int i = tid; i < kEstDefault + 2; i += nt) w.sh->est[i] = 0;
     for (int i = tid; i < kEtabSize; i += nt) w.sh->etab[i] = 0;
   }
