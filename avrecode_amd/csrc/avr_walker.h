@@ -148,7 +148,8 @@ struct Shared {
   uint8_t in_stage[kStage];
   MbRec cur, left;
   union {
-    uint32_t etab[kEtabSize];      // compress/decompress: LDS hash table of the SIG + NZ estimators
+    uint32_t etab[kEtabSize + 64]; // compress/decompress: LDS hash table of the SIG + NZ estimators
+                                   //   (home slots 0 .. kEtabSize - 1, probe windows do not wrap)
     uint16_t gen_p[1024];          // generator: P(bin = 1) in 1/65536 per context
   };
 };
@@ -262,6 +263,28 @@ struct RingOut {
     room--;
     if ((head & 31) == 0) publish();
   }
+  // n <= 64 ops at once, op k in lane k (one vector store)
+  AVR_FI void push_v(uint32_t op_v, uint32_t n) {
+    if (room < n) {
+      publish();
+#ifdef AVR_PROFILE
+      const uint64_t tw = PROF_T();
+#endif
+      for (;;) {
+        const uint32_t used = head - ld_volatile(&sh->fifo_tail[r]);
+        if (used + n <= (uint32_t)kFifo) { room = kFifo - used; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#ifdef AVR_PROFILE
+      wait_cycles += PROF_T() - tw;
+#endif
+    }
+    if (__lane_id() < n) sh->fifo[r][(head + __lane_id()) & (kFifo - 1)] = op_v;
+    const uint32_t h0 = head;
+    head += n;
+    room -= n;
+    if ((h0 ^ head) & ~31u) publish();
+  }
 };
 // Consumer end: wait for a batch, load it one entry per lane.  Returns the batch size.
 AVR_FI uint32_t ring_take(Shared* sh, int r, uint32_t tail, uint32_t* op_v, uint64_t* waited) {
@@ -290,17 +313,17 @@ AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32
   const uint32_t p = (idx * kEstKeyMul) & ((1u << 19) - 1);
   const uint32_t home = p >> 7, tag = p & 127;
   const uint32_t lane = __lane_id();
-  const uint32_t ent = sh->etab[(home + lane) & (kEtabSize - 1)];
+  const uint32_t ent = sh->etab[home + lane];
   const uint64_t hit = __ballot((ent >> 16) == (0x8000u | lane << 7 | tag));
   if (hit) {
     const uint32_t j = (uint32_t)__builtin_ctzll(hit);
-    *slot = (0x8000u | j << 7 | tag) << 16 | ((home + j) & (kEtabSize - 1));
+    *slot = (0x8000u | j << 7 | tag) << 16 | (home + j);
     return __builtin_amdgcn_readlane(ent, j) & 0xffff;
   }
   const uint64_t free_v = __ballot(ent == 0);
   if (free_v) {
     const uint32_t j = (uint32_t)__builtin_ctzll(free_v);
-    *slot = (0x8000u | j << 7 | tag) << 16 | ((home + j) & (kEtabSize - 1));
+    *slot = (0x8000u | j << 7 | tag) << 16 | (home + j);
     return 0;
   }
   // HBM: slot 1 marks the entry's first store (to be logged), 0 a stored one
@@ -310,7 +333,7 @@ AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32
 }
 AVR_FI void est_store(Shared* sh, uint16_t* est_g, uint32_t idx, uint32_t slot, uint32_t e) {
   if (slot >> 31) {
-    sh->etab[slot & (kEtabSize - 1)] = (slot & 0xffff0000u) | e;
+    sh->etab[slot & 0xffff] = (slot & 0xffff0000u) | e;
   } else if (__lane_id() == 0) {
     est_g[idx] = (uint16_t)(e | kEstWritten);
     if (slot) {
@@ -453,6 +476,7 @@ struct Walker {
 
   AVR_FI void publish() { ring0.publish(); }
   AVR_FI void push(uint32_t op) { ring0.push(op); }
+  AVR_FI void push_v(uint32_t op_v, uint32_t n) { ring0.push_v(op_v, n); }
 #ifdef AVR_PROFILE
   uint64_t prof[8];
   uint32_t profb[8];
@@ -606,6 +630,18 @@ struct Walker {
     }
     const int pv = mnnz_prev(n);
     const int t = ((sh->cur.is8x8 | (max > 32)) ? 1 : 0) + 2 * is_dc + c422 + 4 * cat;
+    if (MODE == MODE_COMPRESS) {
+      // all bits at once, bit i in lane i (so_far = the count's bits below i)
+      const int i = (int)__lane_id();
+      const int cur_bit = 1 << (i & 7);
+      const int so_far = count & (cur_bit - 1);
+      const int lb = has_left ? (lv >= cur_bit) : 2;
+      const int ab = av ? (av >= cur_bit) : 2;
+      const int pb = pv >= cur_bit;
+      const int idx = kSigEst + (((((cur_bit - 1 + so_far) * 2 + pb) * 3 + lb) * 3 + ab) * 57 + t);
+      push_v(op_model((count >> (i & 7)) & 1, OPM_CACHE, idx), (uint32_t)bits);
+      return count & ((1 << bits) - 1);
+    }
     int so_far = 0;
     for (int i = 0; i < bits; i++) {
       const int cur_bit = 1 << i;
@@ -665,13 +701,12 @@ struct Walker {
         PROF_END(4, t4);
         PROF_BEGIN(t5);
         const int nnz_m = cnt & mask;
-        int obs = 0;
-        for (int zz = 0; zz <= end; zz++) {
-          int b = (int)((sigmask >> zz) & 1);
-          int idx = sig_est_index(cat, max, is_dc, c422, zz, nnz_m, obs);
-          push(op_model(b, OPM_CACHE | OPM_THR50, idx));
-          obs += b;
-        }
+        // positions 0..end at once, position zz in lane zz (obs = significant positions before it)
+        const int zz = (int)__lane_id();
+        const int b = (int)((sigmask >> zz) & 1);
+        const int obs = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sigmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sigmask, 0u));
+        const int idx = sig_est_index(cat, max, is_dc, c422, zz, nnz_m, obs);
+        push_v(op_model(b, OPM_CACHE | OPM_THR50, idx), (uint32_t)end + 1);
         PROF_END(5, t5);
       }
     } else if (MODE == MODE_DECOMPRESS) {
@@ -1194,7 +1229,7 @@ AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
   if (!RM) {
     for (int i = lane; i < kEstDefault + 2; i += nt) w.sh->est[i] = 0;
     if (MODE != MODE_GENERATE)
-      for (int i = lane; i < kEtabSize; i += nt) w.sh->etab[i] = 0;
+      for (int i = lane; i < kEtabSize + 64; i += nt) w.sh->etab[i] = 0;
   }
   uint32_t* ring32 = (uint32_t*)w.ring;
   for (int i = lane; i < w.W * (int)sizeof(EdgeRec) / 4; i += nt) ring32[i] = 0;
@@ -1392,52 +1427,141 @@ AVR_FI uint64_t readlane64(uint64_t v, uint32_t j) {
   return (uint64_t)hi << 32 | lo;
 }
 
-// The modeler wave (compress): the estimator recurrences.  Per-context estimators live in LDS
-// (Shared::est), the SIG/NZ ones in the LDS cache over HBM; each op's estimator before the update
-// goes to the coder as (pos, pos + neg).
+// The modeler wave (compress): the estimator recurrences (recode.cpp:816-820, 1030-1047),
+// lane-parallel over each batch of ring-0 ops (lane j = op j):
+//  1. every lane loads its op's estimator at once: per-context ones from Shared::est, SIG/NZ
+//     ones by probing the first four slots of the key's window in the LDS hash table; keys not
+//     resolved there (new keys, deep or HBM-resident ones) go through est_load one key at a time,
+//     a new key claiming its slot immediately;
+//  2. a scalar loop walks the batch key by key (ballot of equal keys) and, within a key, op by op
+//     in order: the recurrence runs in a scalar register and each op's estimator before its update
+//     goes into its lane of the output vector -- no memory access on this chain;
+//  3. the last op of each key writes the estimator back (lane-parallel), and the whole batch
+//     goes to ring 1 as one vector store.
+// Ops of one key stay in order, different keys are independent, so this equals processing the
+// ops one by one.
+// lane L of v := x (x, L wave-uniform)
+AVR_FI uint32_t writelane(uint32_t v, uint32_t L, uint32_t x) { return __lane_id() == L ? x : v; }
 AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
-  RingOut out;
-  out.init(sh, 1);
-  uint32_t tail = 0;
+  uint32_t tail = 0, head1 = 0, tail1 = 0;
   uint64_t waited = 0;
+  uint32_t prio = 0;
+  const uint32_t lane = __lane_id();
 #ifdef AVR_PROFILE
+  uint64_t out_wait = 0;
   const uint64_t t_start = PROF_T();
 #endif
-  uint32_t prio = 0;
   for (bool done = false; !done;) {
     uint32_t op_v;
     const uint32_t n = ring_take(sh, 0, tail, &op_v, &waited);
     follow_prio(sh, &prio);
     asm volatile("; MARK_MODEL_BEGIN");
-    for (uint32_t j = 0; j < n; j++) {
-      const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
-      if (op & (OP_END | OP_FINISH)) {
-        out.push(op);
-        if (op & OP_END) { done = true; break; }
-        continue;
+    const bool live = lane < n;
+    const bool ctrl = (op_v & (OP_END | OP_FINISH)) != 0;
+    const bool est_op = live && !ctrl;
+    if (__ballot(live && (op_v & OP_END))) done = true;
+    const uint32_t idx = (op_v >> 3) & 0x7ffffu;
+    const bool cache = (op_v & OPM_CACHE) != 0;
+    // ---- 1. loads
+    uint32_t e_v = 0, slot_v = 0;
+    bool resolved = true;
+    if (est_op && !cache) e_v = sh->est[idx];
+    if (est_op && cache) {
+      const uint32_t p = (idx * kEstKeyMul) & ((1u << 19) - 1);
+      const uint32_t home = p >> 7, tag = p & 127;
+      const uint32_t t0 = 0x8000u | tag;
+      const uint32_t s0 = sh->etab[home], s1 = sh->etab[home + 1], s2 = sh->etab[home + 2], s3 = sh->etab[home + 3];
+      resolved = false;
+      if ((s0 >> 16) == t0) { resolved = true; e_v = s0 & 0xffff; slot_v = t0 << 16 | home; }
+      else if (s0 != 0 && (s1 >> 16) == (t0 | 1u << 7)) { resolved = true; e_v = s1 & 0xffff; slot_v = (t0 | 1u << 7) << 16 | (home + 1); }
+      else if (s0 != 0 && s1 != 0 && (s2 >> 16) == (t0 | 2u << 7)) { resolved = true; e_v = s2 & 0xffff; slot_v = (t0 | 2u << 7) << 16 | (home + 2); }
+      else if (s0 != 0 && s1 != 0 && s2 != 0 && (s3 >> 16) == (t0 | 3u << 7)) { resolved = true; e_v = s3 & 0xffff; slot_v = (t0 | 3u << 7) << 16 | (home + 3); }
+    }
+    // keys the short probe did not find: one at a time through the wave-wide probe
+    uint64_t slow = __ballot(est_op && !resolved);
+    while (slow) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(slow);
+      const uint32_t idx_l = __builtin_amdgcn_readlane(idx, l);
+      uint32_t slot;
+      const uint32_t e = est_load(sh, est_g, idx_l, &slot);
+      if (slot >> 31) {
+        if (lane == 0) sh->etab[slot & 0xffff] = (slot & 0xffff0000u) | e;   // claim / keep the slot
+        wave_sync();
       }
-      const int b = op & 1;
-      const uint32_t idx = (op >> 3) & 0x7ffff;
-      uint32_t e;
-      if (op & OPM_CACHE) {
-        uint32_t slot;
-        e = est_load(sh, est_g, idx, &slot);
-        est_store(sh, est_g, idx, slot, est_update(e, b, (op & OPM_THR50) ? 0x50 : 0x60));
-      } else {
-        e = sh->est[idx];
-        sh->est[idx] = (uint16_t)est_update(e, b, 0x60);
+      const uint64_t same = __ballot(est_op && cache && idx == idx_l);
+      if ((same >> lane) & 1) { e_v = e; slot_v = slot; }
+      slow &= ~same;
+    }
+    // ---- 2. the recurrences, key by key, ops in order
+    const uint32_t key_v = (op_v >> 1) & 0xfffffdu;            // cache bit + index (bin, threshold excluded)
+    const uint64_t bins_m = __ballot(op_v & 1), thr_m = __ballot(op_v & OPM_THR50);
+    uint32_t out_v = op_v;                                     // control ops pass through
+    uint32_t fin_v = 0;
+    uint64_t last_m = 0;
+    uint64_t todo = __ballot(est_op);
+    while (todo) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(todo);
+      const uint32_t k = __builtin_amdgcn_readlane(key_v, l);
+      uint64_t m = __ballot(key_v == k) & todo;
+      todo &= ~m;
+      uint32_t e = __builtin_amdgcn_readlane(e_v, l);
+      uint32_t j = l;
+      for (;;) {
+        const uint32_t b = (uint32_t)(bins_m >> j) & 1u;
+        out_v = writelane(out_v, j, op_recode((int)b, e));
+        e = est_update(e, (int)b, ((thr_m >> j) & 1) ? 0x50u : 0x60u);
+        m &= m - 1;
+        if (!m) break;
+        j = (uint32_t)__builtin_ctzll(m);
       }
-      out.push(op_recode(b, e));
+      fin_v = writelane(fin_v, j, e);
+      last_m |= 1ull << j;
+    }
+    // ---- 3. write-back by the last op of each key
+    const bool is_last = (last_m >> lane) & 1;
+    if (is_last && !cache) sh->est[idx] = (uint16_t)fin_v;
+    if (is_last && cache && (slot_v >> 31)) sh->etab[slot_v & 0xffff] = (slot_v & 0xffff0000u) | fin_v;
+    const bool hbm = is_last && cache && !(slot_v >> 31);
+    if (__ballot(hbm)) {
+      if (hbm) est_g[idx] = (uint16_t)(fin_v | kEstWritten);
+      const uint64_t first = __ballot(hbm && slot_v == 1);
+      if (first) {   // append first stores to the table's write log (est_store)
+        const uint32_t base = __builtin_amdgcn_readfirstlane(sh->elog_n);
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(first);
+        const uint32_t pos = base + (uint32_t)__builtin_popcountll(first & ((1ull << lane) - 1));
+        uint32_t* lg = (uint32_t*)(est_g + kEstLog);
+        if (((first >> lane) & 1) && pos < (uint32_t)kEstLogCap) lg[pos] = idx;
+        if (lane == 0) {
+          sh->elog_n = base + cnt;
+          *(uint32_t*)(est_g + kEstLogN) = base + cnt <= (uint32_t)kEstLogCap ? base + cnt : kEstLogOverflow;
+        }
+      }
     }
     asm volatile("; MARK_MODEL_END");
+    // ---- the batch to ring 1 (room for n entries), then retire it from ring 0
+    if (head1 + n - tail1 > (uint32_t)kFifo) {
+#ifdef AVR_PROFILE
+      const uint64_t tw = PROF_T();
+#endif
+      for (;;) {
+        tail1 = ld_volatile(&sh->fifo_tail[1]);
+        if (head1 + n - tail1 <= (uint32_t)kFifo) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+#ifdef AVR_PROFILE
+      out_wait += PROF_T() - tw;
+#endif
+    }
+    if (live) sh->fifo[1][(head1 + lane) & (kFifo - 1)] = out_v;
+    head1 += n;
+    st_volatile(&sh->fifo_head[1], head1);
     tail += n;
     ring_retire(sh, 0, tail);
-    out.publish();
   }
 #ifdef AVR_PROFILE
   if (__lane_id() == 0) {
     atomicAdd(&avr_prof[17], (unsigned long long)waited);
-    atomicAdd(&avr_prof[18], (unsigned long long)out.wait_cycles);
+    atomicAdd(&avr_prof[18], (unsigned long long)out_wait);
     atomicAdd(&avr_prof[20], (unsigned long long)(PROF_T() - t_start));
   }
 #endif
@@ -1653,7 +1777,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
       w.sh->prio_max = 0;
     }
     for (int i = tid; i < kEstDefault + 2; i += nt) w.sh->est[i] = 0;
-    for (int i = tid; i < kEtabSize; i += nt) w.sh->etab[i] = 0;
+    for (int i = tid; i < kEtabSize + 64; i += nt) w.sh->etab[i] = 0;
   }
   // frame_meta: [0] cur_frame.  Frame ids / sizes of the two frames, as scalars (no private arrays).
   int cur = 0, fid0 = 0, fid1 = 0, fw0 = 0, fw1 = 0, fh0 = 0, fh1 = 0;
