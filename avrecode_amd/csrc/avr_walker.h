@@ -1586,9 +1586,11 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
     // Keep the coder's interval in VGPRs: every wave of the CU shares one scalar unit, and the
     // walker wave (the critical path) is scalar-bound; 64-bit multiply-adds are also cheaper on
     // the vector unit (v_mad_u64_u32).  A value the compiler cannot prove uniform stays vector.
+#ifndef AVR_CODER_SALU
     const uint32_t z = vgpr_zero();
     re.range += z;
     re.low += z;
+#endif
   } else {
     ce_init(ce);
     vtab_load(vt, T);
@@ -1609,14 +1611,23 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
       const uint64_t m_v = T->div[tot_v][0];
       const uint32_t s_v = (uint32_t)T->div[tot_v][1];
       asm volatile("; MARK_CODER_BEGIN");
-      for (uint32_t j = 0; j < n; j++) {
+      // control ops (FINISH, END: once per slice) located up front, so the put loop has no checks
+      uint64_t ctrl = __ballot(__lane_id() < n && (op_v & (OP_END | OP_FINISH)));
+      for (uint32_t j = 0;;) {
+        const uint32_t stop = ctrl ? (uint32_t)__builtin_ctzll(ctrl) : n;
+        for (; j < stop; j++) {
+          const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
+          const uint64_t m = readlane64(m_v, j);
+          const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
+          const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
+          re_put(re, o, op & 1, p1);
+        }
+        if (j >= n) break;
         const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
         if (op & OP_END) { done = true; break; }
-        if (op & OP_FINISH) { re_finish(re, o); continue; }
-        const uint64_t m = readlane64(m_v, j);
-        const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
-        const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
-        re_put(re, o, op & 1, p1);
+        re_finish(re, o);
+        ctrl &= ctrl - 1;
+        j++;
       }
       asm volatile("; MARK_CODER_END");
     } else {
