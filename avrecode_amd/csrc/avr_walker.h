@@ -345,6 +345,22 @@ AVR_FI void est_store(Shared* sh, uint16_t* est_g, uint32_t idx, uint32_t slot, 
     }
   }
 }
+// Lane-parallel lookup of each lane's key in the first four slots of its window: true (with the
+// estimator and its slot) when found there.  A key found stays where it is, so a hit is final;
+// a miss (new key, deeper or HBM-resident one) goes through est_load.
+AVR_FI bool est_probe4(const Shared* sh, uint32_t idx, uint32_t* e, uint32_t* slot) {
+  const uint32_t p = (idx * kEstKeyMul) & ((1u << 19) - 1);
+  const uint32_t home = p >> 7, t0 = 0x8000u | (p & 127);
+  const uint32_t s0 = sh->etab[home], s1 = sh->etab[home + 1], s2 = sh->etab[home + 2], s3 = sh->etab[home + 3];
+  // branch-free (selects): callers run it on every lane
+  const bool h0 = (s0 >> 16) == t0, h1 = (s1 >> 16) == (t0 | 1u << 7);
+  const bool h2 = (s2 >> 16) == (t0 | 2u << 7), h3 = (s3 >> 16) == (t0 | 3u << 7);
+  const uint32_t d = h0 ? 0u : h1 ? 1u : h2 ? 2u : 3u;
+  *e = (h0 ? s0 : h1 ? s1 : h2 ? s2 : s3) & 0xffff;
+  *slot = (t0 | d << 7) << 16 | (home + d);
+  return h0 | h1 | h2 | h3;
+}
+
 // A fresh model on a table the last model may have written: zero the logged entries (or the
 // whole table), reset the log.  Called by the whole workgroup; ends with a barrier.
 AVR_FI void est_table_reset(uint16_t* est_g, Shared* sh) {
@@ -641,6 +657,36 @@ struct Walker {
       const int idx = kSigEst + (((((cur_bit - 1 + so_far) * 2 + pb) * 3 + lb) * 3 + ab) * 57 + t);
       push_v(op_model((count >> (i & 7)) & 1, OPM_CACHE, idx), (uint32_t)bits);
       return count & ((1 << bits) - 1);
+    }
+    if (MODE == MODE_DECOMPRESS) {
+      // every key of the bit tree at once (lane (1 << i) - 1 + so_far: bit i after so_far; the
+      // keys are distinct), then the bits in order with the estimators already in registers
+      const uint32_t L = __lane_id();
+      const int i = 31 - __clz((int)L + 1);
+      const int cur_bit = 1 << i;
+      const int lb = has_left ? (lv >= cur_bit) : 2;
+      const int ab = av ? (av >= cur_bit) : 2;
+      const int pb = pv >= cur_bit;
+      const uint32_t idx_v = kSigEst + ((((L * 2 + pb) * 3 + lb) * 3 + ab) * 57 + t);
+      uint32_t e_v = 0, slot_v = 0;
+      const bool hit = est_probe4(sh, idx_v, &e_v, &slot_v);   // lanes past the tree are never read
+      const uint64_t hit_m = __ballot(hit);
+      int so_far = 0;
+      for (int k = 0; k < bits; k++) {
+        const uint32_t j = (1u << k) - 1 + (uint32_t)so_far;
+        const uint32_t idx = __builtin_amdgcn_readlane(idx_v, j);
+        uint32_t e, slot;
+        if ((hit_m >> j) & 1) {
+          e = __builtin_amdgcn_readlane(e_v, j);
+          slot = __builtin_amdgcn_readlane(slot_v, j);
+        } else {
+          e = est_load(sh, est_g, idx, &slot);
+        }
+        const int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
+        est_store(sh, est_g, idx, slot, est_update(e, b, 0x60));
+        so_far |= b << k;
+      }
+      return so_far;
     }
     int so_far = 0;
     for (int i = 0; i < bits; i++) {
@@ -1466,17 +1512,7 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
     uint32_t e_v = 0, slot_v = 0;
     bool resolved = true;
     if (est_op && !cache) e_v = sh->est[idx];
-    if (est_op && cache) {
-      const uint32_t p = (idx * kEstKeyMul) & ((1u << 19) - 1);
-      const uint32_t home = p >> 7, tag = p & 127;
-      const uint32_t t0 = 0x8000u | tag;
-      const uint32_t s0 = sh->etab[home], s1 = sh->etab[home + 1], s2 = sh->etab[home + 2], s3 = sh->etab[home + 3];
-      resolved = false;
-      if ((s0 >> 16) == t0) { resolved = true; e_v = s0 & 0xffff; slot_v = t0 << 16 | home; }
-      else if (s0 != 0 && (s1 >> 16) == (t0 | 1u << 7)) { resolved = true; e_v = s1 & 0xffff; slot_v = (t0 | 1u << 7) << 16 | (home + 1); }
-      else if (s0 != 0 && s1 != 0 && (s2 >> 16) == (t0 | 2u << 7)) { resolved = true; e_v = s2 & 0xffff; slot_v = (t0 | 2u << 7) << 16 | (home + 2); }
-      else if (s0 != 0 && s1 != 0 && s2 != 0 && (s3 >> 16) == (t0 | 3u << 7)) { resolved = true; e_v = s3 & 0xffff; slot_v = (t0 | 3u << 7) << 16 | (home + 3); }
-    }
+    if (est_op && cache) resolved = est_probe4(sh, idx, &e_v, &slot_v);
     // keys the short probe did not find: one at a time through the wave-wide probe
     uint64_t slow = __ballot(est_op && !resolved);
     while (slow) {
