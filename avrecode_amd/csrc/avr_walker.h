@@ -139,7 +139,6 @@ struct Shared {
   uint32_t fifo_tail[2];     // operations retired by the ring's consumer (monotonic)
   int32_t p_status, p_stop_ok, c_err;  // slice results of the two waves
   uint32_t elog_n;           // entries appended to the HBM table's write log by this model
-  uint32_t prio_max;         // largest input (payload) size of the batch
   uint32_t prio;             // the slice's current wave priority (walker -> modeler / coder)
   uint32_t c_len, c_last;
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
@@ -219,6 +218,33 @@ AVR_FI void set_prio(uint32_t p) {
     default: __builtin_amdgcn_s_setprio(3); break;
   }
 }
+// The slices that share a CU (up to 4 resident workgroups) rank themselves by remaining input on
+// a per-CU board in global memory (one copy per kernel): each walker registers a cell of its CU
+// (HW_ID / XCC_ID registers), posts its remaining bytes there once per macroblock and takes
+// priority 3 - (number of CU neighbours with more input left), so the CU's issue slots go to the
+// longest remaining slice first and the co-resident slices tend to finish together.
+constexpr int kCuIds = 2048;   // XCC (3 bits) x SE (3) x SH (1) x CU (4)
+static __device__ uint32_t avr_cu_count[kCuIds];
+static __device__ uint32_t avr_cu_rem[kCuIds * 4];
+AVR_FI uint32_t cu_cell() {
+  const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+  const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11));  // HW_REG_XCC_ID
+  const uint32_t cu = (((xcc & 7) * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 16 + ((hw >> 8) & 15);
+  uint32_t slot = 0;
+  if (__lane_id() == 0) slot = atomicAdd(&avr_cu_count[cu], 1u);
+  return cu * 4 + (__builtin_amdgcn_readfirstlane(slot) & 3);
+}
+AVR_FI void cu_post(uint32_t cell, uint32_t rem) {
+  if (__lane_id() == 0) __hip_atomic_store(&avr_cu_rem[cell], rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+AVR_FI uint32_t cu_rank_prio(uint32_t cell, uint32_t rem) {
+  const uint32_t lane = __lane_id(), me = cell & 3;
+  uint32_t v = 0;
+  if (lane < 4) v = __hip_atomic_load(&avr_cu_rem[(cell & ~3u) + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t ahead = __ballot(lane < 4 && lane != me && (v > rem || (v == rem && lane < me)));
+  return 3u - (uint32_t)__builtin_popcountll(ahead);
+}
+
 AVR_FI void follow_prio(Shared* sh, uint32_t* cur) {
   const uint32_t p = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->prio);
   if (p != *cur) {
@@ -406,12 +432,13 @@ struct Walker {
   uint32_t bins;
   int target_mbs, mbs_done, last_mb;
   int nref0, nref1, d8x8inf, x264_build, first_mb;
-  uint32_t prio_t1, prio_t2, prio_t3, prio_cur;   // remaining-input thresholds (1/4, 1/2, 3/4 of the batch's largest)
+  uint32_t prio_cell, prio_cur;   // this slice's cell on the CU board, current priority
   AVR_FI void update_prio() {
     const uint32_t pos = MODE == MODE_DECOMPRESS ? rd.next : cd.next;
     const uint32_t size = d->payload_size;
     const uint32_t rem = pos < size ? size - pos : 0u;
-    const uint32_t p = (rem > prio_t1 ? 1u : 0u) + (rem > prio_t2 ? 1u : 0u) + (rem > prio_t3 ? 1u : 0u);
+    cu_post(prio_cell, rem);
+    const uint32_t p = cu_rank_prio(prio_cell, rem);
     if (p != prio_cur) {
       prio_cur = p;
       set_prio(p);
@@ -1389,11 +1416,8 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   if (MODE == MODE_DECOMPRESS) vdiv_load(w.vd, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
-  {
-    const uint32_t m = w.sh->prio_max;
-    w.prio_t1 = m >> 2;
-    w.prio_t2 = m >> 1;
-    w.prio_t3 = m - (m >> 2);
+  if (!RM && (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS)) {
+    w.prio_cell = cu_cell();
     w.prio_cur = 0xffffffffu;   // set on the first macroblock
   }
   if (MODE == MODE_COMPRESS || MODE == MODE_TRACE) {
@@ -1435,6 +1459,7 @@ template <int MODE, bool RM>
 AVR_FI void walker_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
   begin_slice(w, d, in, nullptr);
   profile_slice(w);
+  if (!RM) cu_post(w.prio_cell, 0);   // leave the CU board
   w.rc_writeback();  // estimators persist across slices in the reference model
   w.push(OP_END);
 #ifdef AVR_PROFILE
@@ -1769,16 +1794,7 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) est_table_reset(w.est_g, w.sh);
   w.d = d;
   w.W = d->mb_width;
-  if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) {
-    if (threadIdx.x == 0) {
-      w.sh->prio_max = 0;
-      w.sh->prio = 0;
-    }
-    __syncthreads();
-    uint32_t m = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) m = max(m, descs[i].payload_size);
-    atomicMax(&w.sh->prio_max, m);   // visible after init_slice_state's barrier
-  }
+  if ((MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x == 0) w.sh->prio = 0;   // before init_slice_state's barrier
   init_slice_state(w, G);
   if (MODE == MODE_GENERATE || MODE == MODE_TRACE) {
     run_slice_inline(w, d, in, out, &res[s]);
@@ -1821,7 +1837,6 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
     if (tid == 0) {
       w.sh->elog_n = 0;
       w.sh->prio = 0;
-      w.sh->prio_max = 0;
     }
     for (int i = tid; i < kEstDefault + 2; i += nt) w.sh->est[i] = 0;
     for (int i = tid; i < kEtabSize + 64; i += nt) w.sh->etab[i] = 0;
