@@ -447,7 +447,6 @@ struct Walker {
   }
   RingOut ring0;          // walker -> modeler (compress) / coder (decompress)
   VTab vt;                // CABAC state records (compress / generate: the walker's engine)
-  VDiv vd;                // reciprocals (decompress: the walker's recoded decoder)
 
   // ------------------------------------------------------------------ residual context registers
   // The residual contexts of one ctxBlockCat (significant_coeff_flag lanes 0-15,
@@ -484,7 +483,7 @@ struct Walker {
     bins++;
     const uint32_t s = __builtin_amdgcn_readlane(rc_v, L);
     uint32_t ns;
-    const int b = cd_decide(cd, in, s, vtab_rec(vt, s), &ns);
+    const int b = cd_decide(cd, in, s, crec(s), &ns);
     rc_v = wlane(rc_v, L, ns);
     if (MODE == MODE_TRACE) trace(b, OPK_DECISION, s);
     return b;
@@ -502,7 +501,7 @@ struct Walker {
     } else if (MODE == MODE_DECOMPRESS) {
       bins++;
       const uint32_t e = __builtin_amdgcn_readlane(rc_v, L);
-      const int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
+      const int b = rd_get(rd, in, p1(e));
       rc_v = wlane(rc_v, L, est_update(e, b, 0x60));
       push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
       return b;
@@ -517,6 +516,24 @@ struct Walker {
     }
   }
 
+  // recoded-decoder probability (recode.cpp:816-820).  The reciprocal comes by a scalar load
+  // from the constant table (s_load_dwordx4 into SGPRs, scalar-cache hit): fewer instructions on
+  // the walker than three v_readlane pairs and selects (VDiv), which measured 10 % slower.
+  typedef const __attribute__((address_space(4))) uint64_t cu64;
+  AVR_FI uint64_t p1(uint32_t e) const {
+    const uint32_t pos = (e & 0xff) + 1, tot = pos + (e >> 8) + 1;
+    cu64* dv = (cu64*)&G->hot.div[tot][0];
+    return (__umul64hi(rd.range, dv[0]) >> (uint32_t)dv[1]) * pos;
+  }
+  // CABAC state record of state byte s: VGPR table (two v_readlane) or, with AVR_CABAC_SMEM, a
+  // scalar load
+  AVR_FI CabacRec crec(uint32_t s) const {
+#ifdef AVR_CABAC_SMEM
+    return rec_of(((cu64*)G->hot.cabac)[s]);
+#else
+    return vtab_rec(vt, s);
+#endif
+  }
   AVR_FI void publish() { ring0.publish(); }
   AVR_FI void push(uint32_t op) { ring0.push(op); }
   AVR_FI void push_v(uint32_t op_v, uint32_t n) { ring0.push_v(op_v, n); }
@@ -531,14 +548,14 @@ struct Walker {
     if (DEC) {
       const uint32_t s = sh->state[ctx];
       uint32_t ns;
-      const int b = cd_decide(cd, in, s, vtab_rec(vt, s), &ns);
+      const int b = cd_decide(cd, in, s, crec(s), &ns);
       sh->state[ctx] = (uint8_t)ns;
       if (MODE == MODE_TRACE) trace(b, OPK_DECISION, s);
       else push(op_model(b, 0, ctx));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[ctx];
-      const int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
+      const int b = rd_get(rd, in, p1(e));
       sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
       push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
       return b;
@@ -557,7 +574,7 @@ struct Walker {
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1024];
-      const int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
+      const int b = rd_get(rd, in, p1(e));
       sh->est[1024] = (uint16_t)est_update(e, b, 0x60);
       push((uint32_t)b | OPK_BYPASS << 1);
       return b;
@@ -580,7 +597,7 @@ struct Walker {
       }
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1025];
-      b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
+      b = rd_get(rd, in, p1(e));
       sh->est[1025] = (uint16_t)est_update(e, b, 0x60);
       push((uint32_t)b | OPK_TERMINATE << 1);
     } else {
@@ -709,7 +726,7 @@ struct Walker {
         } else {
           e = est_load(sh, est_g, idx, &slot);
         }
-        const int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
+        const int b = rd_get(rd, in, p1(e));
         est_store(sh, est_g, idx, slot, est_update(e, b, 0x60));
         so_far |= b << k;
       }
@@ -729,7 +746,7 @@ struct Walker {
       } else {
         uint32_t slot;
         const uint32_t e = est_load(sh, est_g, idx, &slot);
-        b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
+        b = rd_get(rd, in, p1(e));
         est_store(sh, est_g, idx, slot, est_update(e, b, 0x60));
       }
       if (b) so_far |= cur_bit;
@@ -796,7 +813,7 @@ struct Walker {
         int idx = sig_est_index(cat, max, is_dc, c422, pos, nnz_m, cnt);
         uint32_t slot;
         uint32_t e = est_load(sh, est_g, idx, &slot);
-        int b = rd_get(rd, in, rc_p1v(rd.range, e, vd));
+        int b = rd_get(rd, in, p1(e));
         est_store(sh, est_g, idx, slot, est_update(e, b, 0x50));
         bins++;
         push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3);
@@ -1413,7 +1430,6 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   w.out.last = 0;
   w.ring0.init(w.sh, 0);
   vtab_load(w.vt, w.T);
-  if (MODE == MODE_DECOMPRESS) vdiv_load(w.vd, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
   if (!RM && (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS)) {
@@ -1697,9 +1713,13 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
         if (op & OP_END) { done = true; break; }
         const int b = op & 1;
         const uint32_t kind = (op >> 1) & 3;
+#ifndef AVR_EXP_NOCODER
         if (kind == OPK_DECISION) ce_decision_v(ce, o, b, &sh->state[(op >> 3) & 1023], vt);
         else if (kind == OPK_BYPASS) ce_bypass(ce, o, b);
         else ce_terminate(ce, o, b);
+#else
+        (void)b; (void)kind;   // experiment: the walker alone (output invalid)
+#endif
       }
     }
     tail += n;
