@@ -450,16 +450,22 @@ struct Walker {
 
   // ------------------------------------------------------------------ residual context registers
   // The residual contexts of one ctxBlockCat (significant_coeff_flag lanes 0-15,
-  // last_significant lanes 16-31, coeff_abs_level_minus1 lanes 32-41) live in one VGPR, lane j
+  // last_significant lanes 16-31, coeff_abs_level_minus1 lanes 32-41, coded_block_flag lanes
+  // 42-45) live in one VGPR, lane j
   // holding the walker's per-context value for ctx rc_addr(j): the CABAC state byte (compress,
   // generate) or the estimator (decompress).  A residual bin then costs a v_readlane /
   // v_writelane instead of an LDS round trip.  Switching category writes the lanes back.
   uint32_t rc_v;
   int rc_cat;
+  uint32_t byp_e;         // decompress: the estimator of &bypass_context (recode.cpp:1049), Shared::est[1024] while walking
   AVR_FI static uint32_t wlane(uint32_t v, uint32_t L, uint32_t x) { return __lane_id() == L ? x : v; }
   AVR_FI int rc_addr(int cat, uint32_t j) const {
+    // 8x8 categories (5, 9, 13) use sig ctxIdxInc 0-14 and last 0-8 only: the other lanes would
+    // alias the next syntax element's contexts, so they hold nothing
+    const bool c8 = cat == 5 || cat == 9 || cat == 13;
+    if (c8 && (j == 15 || (j >= 25 && j < 32))) return -1;
     return j < 16 ? T->sig_base[cat] + (int)j : j < 32 ? T->last_base[cat] + (int)j - 16
-         : j < 42 ? T->abs_base[cat] + (int)j - 32 : -1;
+         : j < 42 ? T->abs_base[cat] + (int)j - 32 : j < 46 ? T->cbf_base[cat] + (int)j - 42 : -1;
   }
   AVR_FI void rc_writeback() {
     if (rc_cat < 0) return;
@@ -573,9 +579,9 @@ struct Walker {
       else push(op_model(b, 0, 1024));
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
-      const uint32_t e = sh->est[1024];
+      const uint32_t e = byp_e;   // the bypass estimator lives in a scalar register
       const int b = rd_get(rd, in, p1(e));
-      sh->est[1024] = (uint16_t)est_update(e, b, 0x60);
+      byp_e = est_update(e, b, 0x60);
       push((uint32_t)b | OPK_BYPASS << 1);
       return b;
     } else {
@@ -859,7 +865,8 @@ struct Walker {
         nza = nnz_left(p, pw, x4, y4) > 0;
         nzb = nnz_top(p, x4, y4) > 0;
       }
-      coded = bin(SE_OTHER, 0, T->cbf_base[cat] + nza + 2 * nzb);
+      rc_select(cat);
+      coded = rbin(42 + nza + 2 * nzb, T->cbf_base[cat] + nza + 2 * nzb);
     }
     int cnt = 0;
     if (coded) {
@@ -1432,6 +1439,7 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   vtab_load(w.vt, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
+  if (MODE == MODE_DECOMPRESS) w.byp_e = w.sh->est[1024];
   if (!RM && (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS)) {
     w.prio_cell = cu_cell();
     w.prio_cur = 0xffffffffu;   // set on the first macroblock
@@ -1477,6 +1485,7 @@ AVR_FI void walker_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uin
   profile_slice(w);
   if (!RM) cu_post(w.prio_cell, 0);   // leave the CU board
   w.rc_writeback();  // estimators persist across slices in the reference model
+  if (MODE == MODE_DECOMPRESS && __lane_id() == 0) w.sh->est[1024] = (uint16_t)w.byp_e;
   w.push(OP_END);
 #ifdef AVR_PROFILE
   if (__lane_id() == 0) atomicAdd(&avr_prof[16], (unsigned long long)w.ring0.wait_cycles);
