@@ -549,7 +549,49 @@ struct Walker {
 #endif
 
   // ------------------------------------------------------------------ bins through the model
+  // Macroblock-layer contexts kMcBase .. kMcBase + 63 (sub_mb_type, B mb_type, mvd, ref_idx,
+  // mb_qp_delta, intra_chroma_pred_mode, prev/rem_intra_pred_mode, coded_block_pattern) stay in
+  // one VGPR for the whole slice, lane ctx - kMcBase, like the residual contexts.
+  static constexpr int kMcBase = 21;
+  uint32_t mc_v;
+  AVR_FI void mc_load() {
+    const int a = kMcBase + (int)__lane_id();
+    mc_v = MODE == MODE_DECOMPRESS ? (uint32_t)sh->est[a] : (uint32_t)sh->state[a];
+  }
+  AVR_FI void mc_store() {
+    const int a = kMcBase + (int)__lane_id();
+    if (MODE == MODE_DECOMPRESS) sh->est[a] = (uint16_t)mc_v;
+    else sh->state[a] = (uint8_t)mc_v;
+    wave_sync();
+  }
+  AVR_FI int mbin(int se, int k, int ctx) {
+    bins++;
+    const uint32_t L = (uint32_t)(ctx - kMcBase);
+    if (DEC) {
+      const uint32_t s = __builtin_amdgcn_readlane(mc_v, L);
+      uint32_t ns;
+      const int b = cd_decide(cd, in, s, crec(s), &ns);
+      mc_v = wlane(mc_v, L, ns);
+      if (MODE == MODE_TRACE) trace(b, OPK_DECISION, s);
+      else push(op_model(b, 0, ctx));
+      return b;
+    } else if (MODE == MODE_DECOMPRESS) {
+      const uint32_t e = __builtin_amdgcn_readlane(mc_v, L);
+      const int b = rd_get(rd, in, p1(e));
+      mc_v = wlane(mc_v, L, est_update(e, b, 0x60));
+      push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
+      return b;
+    } else {
+      const uint32_t s = __builtin_amdgcn_readlane(mc_v, L);
+      const int b = gen_bin(se, k, ctx);
+      uint32_t ns;
+      ce_encode(ce, out, b, s, vtab_rec(vt, s), &ns);
+      mc_v = wlane(mc_v, L, ns);
+      return b;
+    }
+  }
   AVR_FI int bin(int se, int k, int ctx) {
+    if ((uint32_t)(ctx - kMcBase) < 64u) return mbin(se, k, ctx);
     bins++;
     if (DEC) {
       const uint32_t s = sh->state[ctx];
@@ -1440,6 +1482,7 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   w.rc_cat = -1;
   w.rc_v = 0;
   if (MODE == MODE_DECOMPRESS) w.byp_e = w.sh->est[1024];
+  w.mc_load();
   if (!RM && (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS)) {
     w.prio_cell = cu_cell();
     w.prio_cur = 0xffffffffu;   // set on the first macroblock
@@ -1485,6 +1528,7 @@ AVR_FI void walker_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uin
   profile_slice(w);
   if (!RM) cu_post(w.prio_cell, 0);   // leave the CU board
   w.rc_writeback();  // estimators persist across slices in the reference model
+  w.mc_store();
   if (MODE == MODE_DECOMPRESS && __lane_id() == 0) w.sh->est[1024] = (uint16_t)w.byp_e;
   w.push(OP_END);
 #ifdef AVR_PROFILE
@@ -1767,6 +1811,7 @@ AVR_FI void run_slice_inline(Walker<MODE, RM>& w, const avr_slice_desc* d, const
   begin_slice(w, d, in, out);
   profile_slice(w);
   w.rc_writeback();
+  w.mc_store();
   int status = w.err;
   if (!status && !w.finished) status = -9;
   if (MODE == MODE_GENERATE && w.ce.err) status = -10;
