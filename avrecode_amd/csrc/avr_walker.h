@@ -222,7 +222,10 @@ AVR_FI void set_prio(uint32_t p) {
 // a per-CU board in global memory (one copy per kernel): each walker registers a cell of its CU
 // (HW_ID / XCC_ID registers), posts its remaining bytes there once per macroblock and takes
 // priority 3 - (number of CU neighbours with more input left), so the CU's issue slots go to the
-// longest remaining slice first and the co-resident slices tend to finish together.
+// longest remaining slice first and the co-resident slices tend to finish together.  The board
+// is shared by waves of one CU only, so workgroup-scope accesses (through the CU's own vector
+// cache and the XCD's L2) suffice; agent scope would send every post to memory.  A stale read
+// only delays a priority change.
 constexpr int kCuIds = 2048;   // XCC (3 bits) x SE (3) x SH (1) x CU (4)
 static __device__ uint32_t avr_cu_count[kCuIds];
 static __device__ uint32_t avr_cu_rem[kCuIds * 4];
@@ -235,12 +238,12 @@ AVR_FI uint32_t cu_cell() {
   return cu * 4 + (__builtin_amdgcn_readfirstlane(slot) & 3);
 }
 AVR_FI void cu_post(uint32_t cell, uint32_t rem) {
-  if (__lane_id() == 0) __hip_atomic_store(&avr_cu_rem[cell], rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__lane_id() == 0) __hip_atomic_store(&avr_cu_rem[cell], rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 AVR_FI uint32_t cu_rank_prio(uint32_t cell, uint32_t rem) {
   const uint32_t lane = __lane_id(), me = cell & 3;
   uint32_t v = 0;
-  if (lane < 4) v = __hip_atomic_load(&avr_cu_rem[(cell & ~3u) + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane < 4) v = __hip_atomic_load(&avr_cu_rem[(cell & ~3u) + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   const uint64_t ahead = __ballot(lane < 4 && lane != me && (v > rem || (v == rem && lane < me)));
   return 3u - (uint32_t)__builtin_popcountll(ahead);
 }
