@@ -63,7 +63,7 @@ struct avr_ctx {
   int device = 0;
   std::string err;
   hipStream_t stream = nullptr;
-  DevBuf tables, est, frames, frame_meta, in, out, descs, res, packed, offsets;
+  DevBuf tables, est, frames, frame_meta, in, out, descs, res, packed, offsets, order;
 };
 
 namespace {
@@ -250,16 +250,18 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
     HIP_TRY(c, c->frame_meta.reserve(64));
     HIP_TRY(c, avr::launch_slices(mode, true, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n,
                                   plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(), c->res.as<avr_slice_result>(),
-                                  c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), c->stream));
+                                  c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), nullptr,
+                                  c->stream));
   } else {
     const int chunk = std::min(n, kMaxSlicesPerLaunch);
     HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk, true));
+    HIP_TRY(c, c->order.reserve(sizeof(int) * (size_t)chunk));
     for (int s0 = 0; s0 < n; s0 += chunk) {
       const int m = std::min(chunk, n - s0);
       HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>() + s0,
                                     m, plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(),
                                     c->res.as<avr_slice_result>() + s0, c->est.as<uint16_t>(), nullptr, nullptr,
-                                    c->stream));
+                                    c->order.as<int>(), c->stream));
     }
   }
   HIP_TRY(c, hipMemcpyAsync(res->data(), c->res.p, sizeof(avr_slice_result) * n, hipMemcpyDeviceToHost, c->stream));
@@ -645,15 +647,16 @@ static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int 
     HIP_TRY(c, c->frames.reserve((size_t)2 * max_w * max_h * 52 + 64));
     HIP_TRY(c, c->frame_meta.reserve(64));
     HIP_TRY(c, avr::launch_slices(mode, true, c->tables.as<avr::EngineTables>(), d_desc, n, max_w, d_in, d_out, d_res,
-                                  c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), s));
+                                  c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), nullptr, s));
     return AVR_OK;
   }
   const int chunk = std::max(1, std::min(n, kMaxSlicesPerLaunch));
   HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk, true));
+  HIP_TRY(c, c->order.reserve(sizeof(int) * (size_t)chunk));
   for (int s0 = 0; s0 < n; s0 += chunk) {
     const int m = std::min(chunk, n - s0);
     HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), d_desc + s0, m, max_w, d_in, d_out,
-                                  d_res + s0, c->est.as<uint16_t>(), nullptr, nullptr, s));
+                                  d_res + s0, c->est.as<uint16_t>(), nullptr, nullptr, c->order.as<int>(), s));
   }
   return AVR_OK;
 }

@@ -25,20 +25,20 @@ size_t shared_bytes(int max_mb_width);
 // mode: 0 compress, 1 decompress, 2 generate, 3 trace (decode-only bin trace).  sequential = reference model (single wavefront).
 hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
                          int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                         uint8_t* frames, int* frame_meta, hipStream_t stream);
+                         uint8_t* frames, int* frame_meta, int* order, hipStream_t stream);
 // one per kernel translation unit (avr_k_*.hip); lds = shared_bytes(max_mb_width)
 hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                    hipStream_t stream);
+                                    const int* order, hipStream_t stream);
 hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                      hipStream_t stream);
+                                      const int* order, hipStream_t stream);
 hipError_t launch_parallel_generate(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                    hipStream_t stream);
+                                    const int* order, hipStream_t stream);
 hipError_t launch_parallel_trace(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                  const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                 hipStream_t stream);
+                                 const int* order, hipStream_t stream);
 hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                       uint8_t* frames, int* frame_meta, hipStream_t stream);

@@ -1844,10 +1844,10 @@ constexpr int slice_threads() {
 template <int MODE>
 __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                 const uint8_t* in, uint8_t* out, avr_slice_result* res,
-                                                                uint16_t* est_scratch) {
+                                                                uint16_t* est_scratch, const int* order) {
   extern __shared__ __align__(16) uint8_t smem[];
-  const int s = blockIdx.x;
-  if (s >= n) return;
+  if ((int)blockIdx.x >= n) return;
+  const int s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
   const avr_slice_desc* d = &descs[s];
   Walker<MODE, false> w;
   w.sh = (Shared*)smem;
