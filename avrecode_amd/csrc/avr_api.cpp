@@ -64,6 +64,7 @@ struct avr_ctx {
   std::string err;
   hipStream_t stream = nullptr;
   DevBuf tables, est, frames, frame_meta, in, out, descs, res, packed, offsets, order;
+  DevBuf rm_goff, rm_counts, rm_stop, rm_off, rm_ops;   // parallel reference-model compress
 };
 
 namespace {
@@ -223,6 +224,87 @@ avr_slice_desc desc_from_header(const avr::SliceInfo& s) {
   return d;
 }
 
+constexpr int kRModeFallback = 1;
+
+// Reference-model compress of a plan (file order) in parallel over slices (avr_k_rmode.hip).
+// Frame metadata generations mirror update_frame_spec (recode.cpp:824-843) as
+// slices_sequential_kernel implements it; a stream whose frame size changes with a stale other
+// frame is left to the sequential kernel (kRModeFallback), as is a plan too large for one pass.
+int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total) {
+  const int n = (int)plan.descs.size();
+  struct Fb { int gen = -1, w = 0, h = 0, fid = 0; } fb[2];
+  int cur = 0;
+  std::vector<int64_t> gen_off, goff(2 * (size_t)n);
+  int64_t fbytes = 0;
+  for (int k = 0; k < n; k++) {
+    const avr_slice_desc& d = plan.descs[k];
+    const int W = d.mb_width, H = d.mb_height;
+    if (fb[cur].w != W || fb[cur].h != H || !(fb[cur].fid == d.picture_id && fb[cur].w && fb[cur].h)) {
+      cur = 1 - cur;
+      Fb& nw = fb[cur];
+      Fb& ot = fb[1 - cur];
+      const bool reinit_other = (nw.w != W || nw.h != H) && (ot.w != W || ot.h != H);
+      nw.gen = (int)gen_off.size();
+      gen_off.push_back(fbytes);
+      fbytes += (int64_t)W * H * 52;
+      if (reinit_other) {
+        ot.gen = -1;
+        ot.w = W;
+        ot.h = H;
+      }
+      nw.w = W;
+      nw.h = H;
+      nw.fid = d.picture_id;
+    }
+    const Fb& ot = fb[1 - cur];
+    if (ot.gen >= 0 && (ot.w != W || ot.h != H)) return kRModeFallback;
+    goff[2 * k] = gen_off[fb[cur].gen];
+    goff[2 * k + 1] = ot.gen < 0 ? -1 : gen_off[ot.gen];
+  }
+  if (fbytes > ((int64_t)4 << 30)) return kRModeFallback;
+  const size_t lds = avr::shared_bytes(plan.max_w);
+  HIP_TRY(c, c->frames.reserve((size_t)fbytes + 64));
+  HIP_TRY(c, hipMemsetAsync(c->frames.p, 0, (size_t)fbytes + 64, c->stream));
+  HIP_TRY(c, c->rm_goff.reserve(sizeof(int64_t) * goff.size()));
+  HIP_TRY(c, hipMemcpyAsync(c->rm_goff.p, goff.data(), sizeof(int64_t) * goff.size(), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, c->rm_counts.reserve(sizeof(uint32_t) * n));
+  HIP_TRY(c, c->rm_stop.reserve(sizeof(int32_t) * n));
+  HIP_TRY(c, c->rm_off.reserve(sizeof(uint64_t) * (n + 1)));
+  // 1) count the model ops (and fill the frame metadata)
+  HIP_TRY(c, avr::launch_rscan(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, lds,
+                               c->in.as<uint8_t>(), c->frames.as<uint8_t>(), c->rm_goff.as<int64_t>(),
+                               c->rm_counts.as<uint32_t>(), nullptr, nullptr, c->res.as<avr_slice_result>(),
+                               c->rm_stop.as<int32_t>(), c->stream));
+  std::vector<uint32_t> counts(n);
+  HIP_TRY(c, hipMemcpyAsync(counts.data(), c->rm_counts.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  std::vector<uint64_t> off(n + 1, 0);
+  for (int k = 0; k < n; k++) off[k + 1] = off[k] + counts[k];
+  const uint64_t N = off[n];
+  if (N >= (1ull << 30)) return kRModeFallback;
+  HIP_TRY(c, hipMemcpyAsync(c->rm_off.p, off.data(), sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, c->stream));
+  const size_t tb = avr::rmode_sort_temp_bytes(N);
+  HIP_TRY(c, c->rm_ops.reserve(sizeof(uint32_t) * (N + 1) * 6 + tb + 256));
+  uint32_t* ops = c->rm_ops.as<uint32_t>();
+  uint32_t* keys = ops + (N + 1);
+  uint32_t* vals = keys + (N + 1);
+  uint32_t* skeys = vals + (N + 1);
+  uint32_t* svals = skeys + (N + 1);
+  uint32_t* rops = svals + (N + 1);
+  void* temp = (void*)(((uintptr_t)(rops + (N + 1)) + 255) & ~(uintptr_t)255);
+  // 2) write the ops, 3) estimator chains, 4) per-slice coder
+  HIP_TRY(c, avr::launch_rscan(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, lds,
+                               c->in.as<uint8_t>(), c->frames.as<uint8_t>(), c->rm_goff.as<int64_t>(),
+                               c->rm_counts.as<uint32_t>(), ops, c->rm_off.as<uint64_t>(),
+                               c->res.as<avr_slice_result>(), c->rm_stop.as<int32_t>(), c->stream));
+  HIP_TRY(c, avr::launch_rmode_estimators(ops, N, keys, vals, skeys, svals, temp, tb, rops, c->stream));
+  HIP_TRY(c, avr::launch_rcode(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, rops,
+                               c->rm_off.as<uint64_t>(), c->rm_counts.as<uint32_t>(), c->out.as<uint8_t>(),
+                               c->res.as<avr_slice_result>(), c->rm_stop.as<int32_t>(), c->stream));
+  (void)out_total;
+  return AVR_OK;
+}
+
 // Upload plan, run the slice kernel over it (in chunks), download results and outputs.
 int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_slice_result>* res,
              std::vector<uint8_t>* out_host) {
@@ -242,7 +324,14 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
   HIP_TRY(c, c->res.reserve(sizeof(avr_slice_result) * n));
   HIP_TRY(c, hipMemcpyAsync(c->descs.p, plan.descs.data(), sizeof(avr_slice_desc) * n, hipMemcpyHostToDevice,
                             c->stream));
-  if (sequential) {
+  int rm = kRModeFallback;
+  if (sequential && mode == 0 && !getenv("AVR_RMODE_SEQUENTIAL")) {
+    rm = run_rmode_compress(c, plan, out_total);
+    if (rm < 0) return rm;
+  }
+  if (sequential && rm == AVR_OK) {
+    // done: the parallel reference-model compress
+  } else if (sequential) {
     HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * avr::kEstGlobal, true));
     size_t fbytes = 0;
     for (auto& d : plan.descs) fbytes = std::max(fbytes, (size_t)2 * d.mb_width * d.mb_height * 52);

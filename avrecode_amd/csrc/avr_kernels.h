@@ -45,6 +45,17 @@ hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_des
 hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                         const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                         uint8_t* frames, int* frame_meta, hipStream_t stream);
+// reference-model compress in parallel (avr_k_rmode.hip): scan (count: ops == nullptr; write),
+// estimator chains over the op stream, per-slice coder
+hipError_t launch_rscan(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
+                        uint8_t* frames, const int64_t* goff, uint32_t* counts, uint32_t* ops,
+                        const uint64_t* op_off, avr_slice_result* res, int32_t* stop_ok, hipStream_t stream);
+size_t rmode_sort_temp_bytes(uint64_t N);
+hipError_t launch_rmode_estimators(const uint32_t* ops, uint64_t N, uint32_t* keys, uint32_t* vals, uint32_t* skeys,
+                                   uint32_t* svals, void* temp, size_t temp_bytes, uint32_t* rops, hipStream_t stream);
+hipError_t launch_rcode(const EngineTables* T, const avr_slice_desc* descs, int n, const uint32_t* rops,
+                        const uint64_t* op_off, const uint32_t* counts, uint8_t* out, avr_slice_result* res,
+                        const int32_t* stop_ok, hipStream_t stream);
 // section cycle counters of AVR_PROFILE builds (avr_walker.h); zeros otherwise
 hipError_t profile_parallel_compress(unsigned long long* out16);
 hipError_t placement_parallel_compress(uint32_t* out8n, int n);

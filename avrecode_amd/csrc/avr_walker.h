@@ -419,7 +419,11 @@ struct Walker {
   EdgeRec* ring;
   uint16_t* est_g;        // SIG + NZ estimators (global)
   uint8_t* frames;        // RM: 2 frames of W*H*52 model bytes
-  int cur_frame;
+  int64_t cur_off, prev_off;   // RM: byte offsets of the current / previous frame's model bytes (prev < 0: zeros)
+  // RM scan (rscan_kernel): model ops go to global memory instead of the modeler's ring
+  bool gmode;
+  uint32_t* gsink;        // nullptr: count only
+  uint32_t gcount;
   // engines
   InStream in;
   OutStream out;
@@ -543,9 +547,26 @@ struct Walker {
     return vtab_rec(vt, s);
 #endif
   }
-  AVR_FI void publish() { ring0.publish(); }
-  AVR_FI void push(uint32_t op) { ring0.push(op); }
-  AVR_FI void push_v(uint32_t op_v, uint32_t n) { ring0.push_v(op_v, n); }
+  AVR_FI void publish() {
+    if (RM && gmode) return;
+    ring0.publish();
+  }
+  AVR_FI void push(uint32_t op) {
+    if (RM && gmode) {
+      if (gsink && __lane_id() == 0) gsink[gcount] = op;
+      gcount++;
+      return;
+    }
+    ring0.push(op);
+  }
+  AVR_FI void push_v(uint32_t op_v, uint32_t n) {
+    if (RM && gmode) {
+      if (gsink && __lane_id() < n) gsink[gcount + __lane_id()] = op_v;
+      gcount += n;
+      return;
+    }
+    ring0.push_v(op_v, n);
+  }
 #ifdef AVR_PROFILE
   uint64_t prof[8];
   uint32_t profb[8];
@@ -709,15 +730,15 @@ struct Walker {
   // ------------------------------------------------------------------ model neighbours
   // model num_nonzeros of a neighbouring macroblock (get_neighbor_sub_mb, recode.cpp:419-471)
   AVR_FI int mnnz_left(int idx) const {
-    if (RM) return frames[(size_t)cur_frame * W * H * 52 + ((size_t)mb_y * W + mb_x - 1) * 52 + idx];
+    if (RM) return frames[cur_off + ((int64_t)mb_y * W + mb_x - 1) * 52 + idx];
     return left_ok ? sh->left.mnnz[idx] : 0;
   }
   AVR_FI int mnnz_top(int idx) const {
-    if (RM) return frames[(size_t)cur_frame * W * H * 52 + ((size_t)(mb_y - 1) * W + mb_x) * 52 + idx];
+    if (RM) return frames[cur_off + ((int64_t)(mb_y - 1) * W + mb_x) * 52 + idx];
     return top_ok ? ring[mb_x].mnnz[idx] : 0;
   }
   AVR_FI int mnnz_prev(int idx) const {
-    if (RM) return frames[(size_t)(1 - cur_frame) * W * H * 52 + ((size_t)mb_y * W + mb_x) * 52 + idx];
+    if (RM) return prev_off < 0 ? 0 : frames[prev_off + ((int64_t)mb_y * W + mb_x) * 52 + idx];
     return 0;
   }
 
@@ -1448,7 +1469,7 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
         e.cbp = c.cbp;
       }
       if (RM) {
-        uint8_t* f = w.frames + (size_t)w.cur_frame * w.W * w.H * 52 + ((size_t)w.mb_y * w.W + w.mb_x) * 52;
+        uint8_t* f = w.frames + w.cur_off + ((int64_t)w.mb_y * w.W + w.mb_x) * 52;
         if (lane < 52) f[lane] = c.mnnz[lane];
       }
       wave_sync();
@@ -1856,7 +1877,11 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   w.T = &w.sh->tab;
   w.G = G;
   w.frames = nullptr;
-  w.cur_frame = 0;
+  w.cur_off = 0;
+  w.prev_off = -1;
+  w.gmode = false;
+  w.gsink = nullptr;
+  w.gcount = 0;
   w.est_g = est_scratch + (size_t)s * kEstGlobal;
   if (!d->coded) {
     if (threadIdx.x == 0) {
@@ -1952,7 +1977,11 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
       }
       continue;
     }
-    w.cur_frame = cur;
+    w.cur_off = (int64_t)cur * W * H * 52;
+    w.prev_off = (int64_t)(1 - cur) * W * H * 52;
+    w.gmode = false;
+    w.gsink = nullptr;
+    w.gcount = 0;
     w.d = d;
     w.W = W;
     init_slice_state(w, G);
