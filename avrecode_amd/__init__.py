@@ -76,7 +76,8 @@ class _FileStats(ctypes.Structure):
 class _SynthParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
                 ("mb_width", "mb_height", "slice_type", "slice_qp", "chroma_format_idc", "transform_8x8_mode",
-                 "num_ref_idx_l0", "num_ref_idx_l1")] + [("seed", ctypes.c_uint64)]
+                 "num_ref_idx_l0", "num_ref_idx_l1")] + [("seed", ctypes.c_uint64)] + \
+               [("slices_per_picture", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 @dataclass
@@ -91,6 +92,7 @@ class SynthParams:
     num_ref_idx_l0: int = 1
     num_ref_idx_l1: int = 1
     seed: int = 0
+    slices_per_picture: int = 1
 
 
 _lib = None
@@ -303,7 +305,7 @@ class Context:
     def synthesize(self, params: SynthParams, n: int) -> bytes:
         sp = _SynthParams(params.mb_width, params.mb_height, params.slice_type, params.slice_qp,
                           params.chroma_format_idc, params.transform_8x8_mode, params.num_ref_idx_l0,
-                          params.num_ref_idx_l1, params.seed)
+                          params.num_ref_idx_l1, params.seed, params.slices_per_picture, 0)
         out, olen = ctypes.c_void_p(), ctypes.c_size_t()
         self._check(lib().avr_synthesize_stream(self._h, ctypes.byref(sp), int(n), ctypes.byref(out),
                                                 ctypes.byref(olen)), "synthesize")

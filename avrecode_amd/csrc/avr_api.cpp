@@ -850,7 +850,13 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
   HIP_TRY(c, hipSetDevice(c->device));
   Plan plan;
   const int mbs = p->mb_width * p->mb_height;
-  for (int i = 0; i < n; i++) {
+  const int spp = std::max(1, std::min(p->slices_per_picture, mbs));
+  std::vector<int> pic_of, first_of;
+  for (int i = 0; i < n * spp; i++) {
+    const int pic = i / spp, j = i % spp;
+    const int first = (int)((int64_t)j * mbs / spp), next = (int)((int64_t)(j + 1) * mbs / spp);
+    pic_of.push_back(pic);
+    first_of.push_back(first);
     avr_slice_desc d;
     memset(&d, 0, sizeof(d));
     d.slice_type = p->slice_type;
@@ -864,10 +870,11 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
     d.transform_8x8_mode = p->transform_8x8_mode;
     d.direct_8x8_inference = 1;
     d.x264_build = -1;
-    d.picture_id = i;
+    d.picture_id = pic;
+    d.first_mb = first;
     d.coded = 1;
     d.payload_offset = p->seed * 0x100000001B3ull + (uint64_t)i;  // generator seed
-    d.payload_size = (uint32_t)mbs;                               // generator: macroblocks to emit
+    d.payload_size = (uint32_t)(next - first);                    // generator: macroblocks to emit
     d.out_capacity = (uint32_t)std::min<uint64_t>((uint64_t)mbs * 384 + 4096, 0x7fffffffu);
     plan.descs.push_back(d);
   }
@@ -878,9 +885,10 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
   if (int r = run_plan(c, 2, false, plan, &res, &outb)) return r;
   std::vector<uint8_t> stream;
   avr::synth_write_parameter_sets(&stream, *p);
-  for (int i = 0; i < n; i++) {
+  for (int i = 0; i < (int)plan.descs.size(); i++) {
     if (res[i].status != 0) return fail(c, AVR_ERR_DEVICE, "generator failed on slice " + std::to_string(i));
-    avr::synth_write_slice(&stream, *p, i, outb.data() + plan.descs[i].out_offset, res[i].out_len);
+    avr::synth_write_slice(&stream, *p, pic_of[i], first_of[i], outb.data() + plan.descs[i].out_offset,
+                           res[i].out_len);
   }
   *out = (uint8_t*)malloc(stream.size());
   if (!*out) return AVR_ERR_OUT_OF_MEMORY;

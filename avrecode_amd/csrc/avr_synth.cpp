@@ -1,5 +1,5 @@
 // SPS / PPS / slice header writer for synthetic streams (ITU-T H.264 7.3.2.1.1, 7.3.2.2, 7.3.3)
-// and NAL emulation prevention (7.4.1).  Every slice is an independent picture.
+// and NAL emulation prevention (7.4.1).  A picture is one slice or several (equal MB runs).
 #include "avr_synth.h"
 
 namespace avr {
@@ -101,11 +101,11 @@ void synth_write_parameter_sets(std::vector<uint8_t>* out, const avr_synth_param
   put_nal(out, 3, 8, q.bytes);
 }
 
-void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int index, const uint8_t* payload,
-                       size_t payload_len) {
+void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int index, int first_mb,
+                       const uint8_t* payload, size_t payload_len) {
   const bool idr = p.slice_type == 2;
   BitWriter h;
-  h.ue(0);                       // first_mb_in_slice
+  h.ue((uint32_t)first_mb);      // first_mb_in_slice
   h.ue((uint32_t)p.slice_type + 5);
   h.ue(0);                       // pps id
   h.u(idr ? 0 : (uint32_t)(index & 0xffff), 16);

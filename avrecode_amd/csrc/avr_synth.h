@@ -8,6 +8,6 @@
 
 namespace avr {
 void synth_write_parameter_sets(std::vector<uint8_t>* out, const avr_synth_params& p);
-void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int index, const uint8_t* payload,
-                       size_t payload_len);
+void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int index, int first_mb,
+                       const uint8_t* payload, size_t payload_len);
 }  // namespace avr

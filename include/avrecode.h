@@ -204,9 +204,11 @@ typedef struct {
   int32_t transform_8x8_mode;
   int32_t num_ref_idx_l0, num_ref_idx_l1;
   uint64_t seed;
+  int32_t slices_per_picture;    /* 0 or 1: one slice per picture; k: k slices (equal MB runs) */
+  int32_t reserved;
 } avr_synth_params;
-/* Generate n independent single-slice pictures on the device and return them as one Annex-B
- * stream (SPS/PPS + n slice NAL units) in host memory. */
+/* Generate n pictures on the device (each slices_per_picture slices, in decode order) and return
+ * them as one Annex-B stream (SPS/PPS + the slice NAL units) in host memory. */
 int avr_synthesize_stream(avr_ctx* ctx, const avr_synth_params* params, int n, uint8_t** out, size_t* out_len);
 
 #ifdef __cplusplus
