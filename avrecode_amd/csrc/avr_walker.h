@@ -464,6 +464,7 @@ struct Walker {
   // v_writelane instead of an LDS round trip.  Switching category writes the lanes back.
   uint32_t rc_v;
   int rc_cat;
+  uint32_t sig8_v, last8_v;   // 8x8 significant / last ctxIdxInc tables, lane = scan position
   uint32_t byp_e;         // decompress: the estimator of &bypass_context (recode.cpp:1049), Shared::est[1024] while walking
   AVR_FI static uint32_t wlane(uint32_t v, uint32_t L, uint32_t x) { return __lane_id() == L ? x : v; }
   AVR_FI int rc_addr(int cat, uint32_t j) const {
@@ -835,7 +836,7 @@ struct Walker {
   // significance map of one residual block; returns the coefficient count
   AVR_FI int sig_map(int cat, int n, int max, int is_dc, int c422) {
     const int numc8x8 = cat_ == 2 ? 2 : 1;
-    const int sb = T->sig_base[cat], lb = T->last_base[cat];
+    const int sb = T->sig_base[cat], lb = T->last_base[cat], seb = T->sig_est_base[cat];
     const int bits = max > 16 ? 6 : max > 4 ? 4 : 2;
     const int mask = (1 << bits) - 1;
     int cnt = 0;
@@ -845,7 +846,10 @@ struct Walker {
       PROF_BEGIN(t3);
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
-        if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
+        if (max == 64) {
+          sc = (int)__builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);
+          lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
+        }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
         if (rdecide(sc)) {
@@ -879,10 +883,14 @@ struct Walker {
       int pos;
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
-        if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
+        if (max == 64) {
+          sc = (int)__builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);
+          lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
+        }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
-        int idx = sig_est_index(cat, max, is_dc, c422, pos, nnz_m, cnt);
+        const int zo = max == 64 ? sc : (is_dc && c422) ? (pos < 2 ? 0 : pos < 4 ? 1 : 2) : pos;
+        const int idx = seb + (zo * (max == 64 ? 64 : 16) + nnz_m) * (max == 64 ? 64 : 16) + cnt;   // sig_est_index
         uint32_t slot;
         uint32_t e = est_load(sh, est_g, idx, &slot);
         int b = rd_get(rd, in, p1(e));
@@ -903,7 +911,10 @@ struct Walker {
       int pos;
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
-        if (max == 64) { sc = T->sig8x8[pos]; lc = T->last8x8[pos]; }
+        if (max == 64) {
+          sc = (int)__builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);
+          lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
+        }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
         if (rbin(sc, sb + sc)) {
@@ -1505,6 +1516,8 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   vtab_load(w.vt, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
+  w.sig8_v = w.T->sig8x8[__lane_id()];
+  w.last8_v = w.T->last8x8[__lane_id()];
   if (MODE == MODE_DECOMPRESS) w.byp_e = w.sh->est[1024];
   w.mc_load();
   if (!RM && (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS)) {
