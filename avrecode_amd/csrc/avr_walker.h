@@ -258,7 +258,8 @@ AVR_FI void follow_prio(Shared* sh, uint32_t* cur) {
 
 // Producer end of ring r: entries go to LDS at once, the head counter every 32 entries (and on
 // demand), the tail is re-read only when the ring looks full.
-struct RingOut {
+template <bool STAGED>
+struct RingOutT {
   Shared* sh;
   int r;
   uint32_t head, room;
@@ -267,14 +268,39 @@ struct RingOut {
     r = ring;
     head = 0;
     room = kFifo;
+    stage_v = 0;
+    stage_n = 0;
   }
-  AVR_FI void publish() { st_volatile(&sh->fifo_head[r], head); }
+  AVR_FI void publish() {
+    flush();
+    st_volatile(&sh->fifo_head[r], head);
+  }
 #ifdef AVR_PROFILE
   uint64_t wait_cycles = 0;
 #endif
+  // STAGED: single ops are staged in a VGPR (lane k = k-th op) and stored 64 at a time (fewer
+  // instructions per op on the producer; measured 1 % faster for the decompress walker, 2 %
+  // slower for the compress walker, whose consumer then waits in bursts)
+  uint32_t stage_v, stage_n;
+  AVR_FI void flush() {
+    if (STAGED && stage_n) {
+      const uint32_t k = stage_n;
+      stage_n = 0;
+      push_v_raw(stage_v, k);
+    }
+  }
+  AVR_FI void push_v(uint32_t op_v, uint32_t n) {
+    flush();
+    push_v_raw(op_v, n);
+  }
   AVR_FI void push(uint32_t op) {
+    if (STAGED) {
+      stage_v = __lane_id() == stage_n ? op : stage_v;
+      if (++stage_n == 64) flush();
+      return;
+    }
     if (room == 0) {
-      publish();
+      st_volatile(&sh->fifo_head[r], head);
 #ifdef AVR_PROFILE
       const uint64_t tw = PROF_T();
 #endif
@@ -290,12 +316,12 @@ struct RingOut {
     sh->fifo[r][head & (kFifo - 1)] = op;
     head++;
     room--;
-    if ((head & 31) == 0) publish();
+    if ((head & 31) == 0) st_volatile(&sh->fifo_head[r], head);
   }
   // n <= 64 ops at once, op k in lane k (one vector store)
-  AVR_FI void push_v(uint32_t op_v, uint32_t n) {
+  AVR_FI void push_v_raw(uint32_t op_v, uint32_t n) {
     if (room < n) {
-      publish();
+      st_volatile(&sh->fifo_head[r], head);
 #ifdef AVR_PROFILE
       const uint64_t tw = PROF_T();
 #endif
@@ -312,7 +338,7 @@ struct RingOut {
     const uint32_t h0 = head;
     head += n;
     room -= n;
-    if ((h0 ^ head) & ~31u) publish();
+    if ((h0 ^ head) & ~31u) st_volatile(&sh->fifo_head[r], head);
   }
 };
 // Consumer end: wait for a batch, load it one entry per lane.  Returns the batch size.
@@ -452,7 +478,7 @@ struct Walker {
       if (__lane_id() == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->prio = p;
     }
   }
-  RingOut ring0;          // walker -> modeler (compress) / coder (decompress)
+  RingOutT<MODE == MODE_DECOMPRESS> ring0;   // walker -> modeler (compress) / coder (decompress)
   VTab vt;                // CABAC state records (compress / generate: the walker's engine)
 
   // ------------------------------------------------------------------ residual context registers
