@@ -80,6 +80,31 @@ __global__ void k_branch(uint64_t* out, uint32_t seed) {
   if (threadIdx.x == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = x; }
 }
 
+// dependent scalar loads from a small constant table (scalar-cache hits): the recoded decoder's
+// reciprocal lookup
+__global__ void k_sload(uint64_t* out, uint32_t seed, const uint32_t* tab) {
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  cu32* t = (cu32*)tab;
+  uint32_t x = seed & 255;
+  uint64_t t0 = clk();
+  for (int i = 0; i < N / 4; i++) x = t[x] & 255;
+  uint64_t t1 = clk();
+  if (threadIdx.x == 0) { out[blockIdx.x * 2] = (t1 - t0) * 4; out[blockIdx.x * 2 + 1] = x; }
+}
+__global__ void k_branch_taken(uint64_t* out, uint32_t seed) {
+  uint32_t x = seed;
+  uint64_t t0 = clk();
+  for (int i = 0; i < N; i++) {
+    asm volatile("s_cmp_lg_u32 %0, 12345\n s_cbranch_scc1 1f\n s_nop 0\n1:\n s_add_u32 %0, %0, 1\n" : "+s"(x) :: "scc");
+  }
+  uint64_t t1 = clk();
+  if (threadIdx.x == 0) { out[blockIdx.x * 2] = t1 - t0; out[blockIdx.x * 2 + 1] = x; }
+}
+static uint32_t* g_tab;
+static void k_sload_launch(uint64_t* d, uint32_t seed, int blocks) {
+  hipLaunchKernelGGL(k_sload, dim3(blocks), dim3(64), 0, 0, d, seed, g_tab);
+}
+
 int main() {
   uint64_t* d;
   (void)hipMalloc(&d, 2048 * 16);
@@ -87,8 +112,24 @@ int main() {
   struct K { const char* name; void (*f)(uint64_t*, uint32_t); int per; } ks[] = {
     {"salu dep (4 ops/iter)", k_salu, 4}, {"salu 4 indep chains", k_salu_indep, 4}, {"valu dep (4 ops/iter)", k_valu, 4},
     {"lds dep read + readfirstlane", k_lds, 1}, {"v_readlane dep", k_readlane, 1}, {"valu->readfirstlane->salu", k_valu_to_salu, 1},
-    {"s_cmp+s_cbranch(not taken)+s_add", k_branch, 3}};
+    {"s_cmp+s_cbranch(not taken)+s_add", k_branch, 3}, {"s_cmp+s_cbranch(taken)+s_add", k_branch_taken, 3}};
   setvbuf(stdout, nullptr, _IONBF, 0);
+  {
+    uint32_t ht[256];
+    for (int i = 0; i < 256; i++) ht[i] = (uint32_t)((i * 97 + 31) & 255);
+    (void)hipMalloc(&g_tab, sizeof(ht));
+    (void)hipMemcpy(g_tab, ht, sizeof(ht), hipMemcpyHostToDevice);
+    for (int blocks : {1, 1024}) {
+      k_sload_launch(d, 1, blocks);
+      (void)hipDeviceSynchronize();
+      k_sload_launch(d, 1, blocks);
+      if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 1; }
+      (void)hipMemcpy(h, d, blocks * 16, hipMemcpyDeviceToHost);
+      double s = 0;
+      for (int b = 0; b < blocks; b++) s += h[2 * b];
+      printf("%-40s waves=%5d  cycles/op = %.2f\n", "s_load dep (scalar cache)", blocks, s / blocks / N);
+    }
+  }
   for (auto& k : ks) {
     for (int blocks : {1, 256, 1024, 2048}) {
       printf("# %s %d\n", k.name, blocks);
