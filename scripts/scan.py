@@ -31,14 +31,17 @@ def main():
     ctx = avr.Context(0)
     stream = torch.cuda.Stream()
     for cfg in args.configs:
-        n_s, qps_s = cfg.split(":")
-        n, qps = int(n_s), [int(q) for q in qps_s.split(",")]
+        # n:qps[:slice_type[:mb_width:mb_height]]  (slice_type 0 P, 1 B, 2 I)
+        f = cfg.split(":")
+        n, qps = int(f[0]), [int(q) for q in f[1].split(",")]
+        st = int(f[2]) if len(f) > 2 else 2
+        mbw, mbh = (int(f[3]), int(f[4])) if len(f) > 4 else (args.mb_width, args.mb_height)
         parts = []
         for j, qp in enumerate(qps):
             k = (n - j + len(qps) - 1) // len(qps)
             if k:
-                parts.append(ctx.synthesize(avr.SynthParams(mb_width=args.mb_width, mb_height=args.mb_height,
-                                                            slice_type=2, slice_qp=qp, chroma_format_idc=1,
+                parts.append(ctx.synthesize(avr.SynthParams(mb_width=mbw, mb_height=mbh,
+                                                            slice_type=st, slice_qp=qp, chroma_format_idc=1,
                                                             transform_8x8_mode=1, seed=j), k))
         data = b"".join(parts)
         ps = avr.parse_stream(data)
