@@ -362,38 +362,10 @@ __device__ __forceinline__ void ce_terminate(CabacEncoder& e, OutStream& o, int 
 }
 
 // ----------------------------------------------------------------- recoded coder (u64 / u8)
-// floor(range / d) for range <= 2^63 (exact at 2^63 too: see check_reciprocals in avr_api.cpp)
-__device__ __forceinline__ uint64_t rc_div(uint64_t range, uint32_t d, const HotTables* T) {
-  return __umul64hi(range, T->div[d][0]) >> (uint32_t)T->div[d][1];
-}
-// The reciprocal table in six VGPRs (lane j: divisors j and 64 + j): a lookup with a uniform
-// divisor is three v_readlane pairs and scalar selects, no LDS round trip.
-struct VDiv {
-  uint32_t mlo0, mhi0, sh0, mlo1, mhi1, sh1;
-};
-__device__ __forceinline__ void vdiv_load(VDiv& v, const HotTables* T) {
-  const uint32_t j = __lane_id();
-  v.mlo0 = (uint32_t)T->div[j][0];
-  v.mhi0 = (uint32_t)(T->div[j][0] >> 32);
-  v.sh0 = (uint32_t)T->div[j][1];
-  v.mlo1 = (uint32_t)T->div[64 + j][0];
-  v.mhi1 = (uint32_t)(T->div[64 + j][0] >> 32);
-  v.sh1 = (uint32_t)T->div[64 + j][1];
-}
-__device__ __forceinline__ uint32_t sel32(uint32_t a, uint32_t b, uint32_t m) { return a ^ ((a ^ b) & m); }
-__device__ __forceinline__ uint64_t rc_p1v(uint64_t range, uint32_t est, const VDiv& v) {
-  const uint32_t pos = (est & 0xff) + 1, tot = pos + (est >> 8) + 1;
-  const uint32_t j = tot & 63, m = 0u - (tot >> 6);
-  const uint32_t mlo = sel32(__builtin_amdgcn_readlane(v.mlo0, j), __builtin_amdgcn_readlane(v.mlo1, j), m);
-  const uint32_t mhi = sel32(__builtin_amdgcn_readlane(v.mhi0, j), __builtin_amdgcn_readlane(v.mhi1, j), m);
-  const uint32_t sh = sel32(__builtin_amdgcn_readlane(v.sh0, j), __builtin_amdgcn_readlane(v.sh1, j), m);
-  return (__umul64hi(range, (uint64_t)mhi << 32 | mlo) >> sh) * pos;
-}
-// p1 = (range/(pos+neg))*pos  (recode.cpp:819); est = (pos-1) | (neg-1) << 8
-__device__ __forceinline__ uint64_t rc_p1(uint64_t range, uint32_t est, const HotTables* T) {
-  const uint32_t pos = (est & 0xff) + 1, tot = pos + (est >> 8) + 1;
-  return rc_div(range, tot, T) * pos;
-}
+// p1 = floor(range / (pos + neg)) * pos (recode.cpp:819), est = (pos - 1) | (neg - 1) << 8: the
+// walkers divide with HotTables::div (floor(n/d) = umulhi(n, m) >> shift, exact for n <= 2^63:
+// check_reciprocals in avr_api.cpp) -- by scalar load in the decompress walker (Walker::p1), by a
+// per-lane gather in the compress coder.
 // update_state_for_model_key (recode.cpp:1036-1045)
 __device__ __forceinline__ uint32_t est_update(uint32_t est, int bin, uint32_t thresh) {
   uint32_t pos = (est & 0xff) + 1 + (bin ? 1 : 0), neg = (est >> 8) + 1 + (bin ? 0 : 1);

@@ -558,7 +558,7 @@ struct Walker {
 
   // recoded-decoder probability (recode.cpp:816-820).  The reciprocal comes by a scalar load
   // from the constant table (s_load_dwordx4 into SGPRs, scalar-cache hit): fewer instructions on
-  // the walker than three v_readlane pairs and selects (VDiv), which measured 10 % slower.
+  // the walker than three v_readlane pairs and selects from a VGPR table (measured 10 % slower).
   typedef const __attribute__((address_space(4))) uint64_t cu64;
   AVR_FI uint64_t p1(uint32_t e) const {
     const uint32_t pos = (e & 0xff) + 1, tot = pos + (e >> 8) + 1;
