@@ -42,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "avr_create", "avr_destroy", "avr_last_error", "avr_free", "avr_compress_file", "avr_decompress_file",
     "avr_roundtrip_file", "avr_compress_slices", "avr_decompress_slices", "avr_pack_outputs",
     "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream", "avr_assemble_container", "avr_synthesize_stream",
+    "avr_container_describe",
     "avr_hooks_compress_begin", "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
     "avr_hook_get_bypass", "avr_hook_get_terminate", "avr_hook_skip_bytes", "avr_hook_frame_spec", "avr_hook_mb_xy",
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
@@ -77,7 +78,7 @@ class _SynthParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
                 ("mb_width", "mb_height", "slice_type", "slice_qp", "chroma_format_idc", "transform_8x8_mode",
                  "num_ref_idx_l0", "num_ref_idx_l1")] + [("seed", ctypes.c_uint64)] + \
-               [("slices_per_picture", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+               [("slices_per_picture", ctypes.c_int32), ("gop_length", ctypes.c_int32)]
 
 
 @dataclass
@@ -93,6 +94,7 @@ class SynthParams:
     num_ref_idx_l1: int = 1
     seed: int = 0
     slices_per_picture: int = 1
+    gop_length: int = 0          # > 0: IDR I picture every gop_length pictures, slice_type between
 
 
 _lib = None
@@ -129,6 +131,7 @@ def lib() -> ctypes.CDLL:
     L.avr_parse_stream.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
     L.avr_assemble_container.argtypes = [vp, sz, i32, vp, vp, vp, vp, pp, psz]
     L.avr_synthesize_stream.argtypes = [vp, ctypes.POINTER(_SynthParams), i32, pp, psz]
+    L.avr_container_describe.argtypes = [vp, sz, pp, pp, psz]
     for name in EXPORTED_SYMBOLS:   # fails here, not at first use, when the build is stale
         getattr(L, name)
     _lib = L
@@ -198,6 +201,21 @@ def assemble_container(data, status: np.ndarray, recoded: bytes, offsets: np.nda
     if r != AVR_OK:
         raise AvrError(r, "avr_assemble_container failed")
     return _take(out, olen.value)
+
+
+def describe_container(avrc) -> tuple[dict, bytes]:
+    """Parse a Recoded protobuf with the library's wire codec (avr_container_describe): its fields
+    (hex strings for bytes) and the message re-serialised by the library's writer.  Host only."""
+    import json
+    L = lib()
+    p, n, keep = _buf(avrc)
+    js, out, olen = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_size_t()
+    r = L.avr_container_describe(p, n, ctypes.byref(js), ctypes.byref(out), ctypes.byref(olen))
+    if r != AVR_OK:
+        raise AvrError(r, "avr_container_describe failed")
+    text = ctypes.string_at(js.value).decode()
+    L.avr_free(js)
+    return json.loads(text), _take(out, olen.value)
 
 
 class Context:
@@ -305,7 +323,7 @@ class Context:
     def synthesize(self, params: SynthParams, n: int) -> bytes:
         sp = _SynthParams(params.mb_width, params.mb_height, params.slice_type, params.slice_qp,
                           params.chroma_format_idc, params.transform_8x8_mode, params.num_ref_idx_l0,
-                          params.num_ref_idx_l1, params.seed, params.slices_per_picture, 0)
+                          params.num_ref_idx_l1, params.seed, params.slices_per_picture, params.gop_length)
         out, olen = ctypes.c_void_p(), ctypes.c_size_t()
         self._check(lib().avr_synthesize_stream(self._h, ctypes.byref(sp), int(n), ctypes.byref(out),
                                                 ctypes.byref(olen)), "synthesize")

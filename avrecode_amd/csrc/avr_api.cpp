@@ -65,6 +65,9 @@ struct avr_ctx {
   hipStream_t stream = nullptr;
   DevBuf tables, est, frames, frame_meta, in, out, descs, res, packed, offsets, order;
   DevBuf rm_goff, rm_counts, rm_stop, rm_off, rm_ops;   // parallel reference-model compress
+  DevBuf regen, dec_descs, res_d, verdict;               // compress-side roundtrip check
+  bool round_robin = false;   // placement probe passed: the CU schedule (order) may be used
+  int* order_or_null() { return round_robin ? order.as<int>() : nullptr; }
 };
 
 namespace {
@@ -306,8 +309,13 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total) {
 }
 
 // Upload plan, run the slice kernel over it (in chunks), download results and outputs.
+// verify (parallel compress only): also decompress every slice's output on the device, apply the
+// last-byte rule and compare with the payload (avr_roundtrip_slices); a slice whose output does not
+// regenerate its payload gets status kStatusNoRoundtrip, so no container ever holds a block that
+// cannot be decompressed.
+constexpr int32_t kStatusNoRoundtrip = -20;
 int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_slice_result>* res,
-             std::vector<uint8_t>* out_host) {
+             std::vector<uint8_t>* out_host, bool verify = false) {
   const int n = (int)plan.descs.size();
   res->assign(n, avr_slice_result{0, 0, 0, 0});
   uint64_t out_total = 0;
@@ -350,12 +358,36 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
       HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>() + s0,
                                     m, plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(),
                                     c->res.as<avr_slice_result>() + s0, c->est.as<uint16_t>(), nullptr, nullptr,
-                                    c->order.as<int>(), c->stream));
+                                    c->order_or_null(), c->stream));
     }
+  }
+  std::vector<int32_t> verdict;
+  if (verify && mode == 0 && !sequential) {
+    HIP_TRY(c, c->regen.reserve(plan.arena.size() + 4096));
+    HIP_TRY(c, c->dec_descs.reserve(sizeof(avr_slice_desc) * n));
+    HIP_TRY(c, c->res_d.reserve(sizeof(avr_slice_result) * n));
+    HIP_TRY(c, c->verdict.reserve(sizeof(int32_t) * n));
+    avr_slice_desc* dd = c->dec_descs.as<avr_slice_desc>();
+    avr_slice_result* rd = c->res_d.as<avr_slice_result>();
+    HIP_TRY(c, avr::launch_derive_decompress(c->descs.as<avr_slice_desc>(), c->res.as<avr_slice_result>(), n, dd,
+                                             c->stream));
+    const int chunk = std::min(n, kMaxSlicesPerLaunch);
+    for (int s0 = 0; s0 < n; s0 += chunk) {
+      const int m = std::min(chunk, n - s0);
+      HIP_TRY(c, avr::launch_slices(1, false, c->tables.as<avr::EngineTables>(), dd + s0, m, plan.max_w,
+                                    c->out.as<uint8_t>(), c->regen.as<uint8_t>(), rd + s0, c->est.as<uint16_t>(),
+                                    nullptr, nullptr, c->order_or_null(), c->stream));
+    }
+    HIP_TRY(c, avr::launch_verify(c->descs.as<avr_slice_desc>(), c->res.as<avr_slice_result>(), rd, n,
+                                  c->in.as<uint8_t>(), c->regen.as<uint8_t>(), c->verdict.as<int32_t>(), c->stream));
+    verdict.resize(n);
+    HIP_TRY(c, hipMemcpyAsync(verdict.data(), c->verdict.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
   }
   HIP_TRY(c, hipMemcpyAsync(res->data(), c->res.p, sizeof(avr_slice_result) * n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipMemcpyAsync(out_host->data(), c->out.p, out_total, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < (int)verdict.size(); k++)
+    if ((*res)[k].status == 0 && verdict[k] != 1) (*res)[k].status = kStatusNoRoundtrip;
   return AVR_OK;
 }
 
@@ -463,6 +495,9 @@ int avr_create(int device, avr_ctx** out) {
   if (!check_reciprocals(t)) return AVR_ERR_DEVICE;
   if (c->tables.reserve(sizeof(t)) != hipSuccess) return AVR_ERR_OUT_OF_MEMORY;
   if (hipMemcpy(c->tables.p, &t, sizeof(t), hipMemcpyHostToDevice) != hipSuccess) return AVR_ERR_DEVICE;
+  // CU grouping of the slice kernels only where the dispatcher deals workgroups round-robin
+  if (avr::probe_round_robin(avr::shared_bytes(120), &c->round_robin) != hipSuccess) return AVR_ERR_DEVICE;
+  if (getenv("AVR_NO_SCHEDULE")) c->round_robin = false;
   *out = c.release();
   return AVR_OK;
 }
@@ -505,7 +540,7 @@ int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_
   }
   std::vector<avr_slice_result> res;
   std::vector<uint8_t> outb;
-  if (int r = run_plan(c, 0, false, plan, &res, &outb)) return r;
+  if (int r = run_plan(c, 0, false, plan, &res, &outb, /*verify=*/true)) return r;
   std::vector<char> ok(pf.slices.size(), 0);
   for (size_t i = 0; i < pf.slices.size(); i++) ok[i] = cand_of[i] >= 0 && res[cand_of[i]].status == 0;
   // 2) segmentation (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297)
@@ -745,7 +780,7 @@ static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int 
   for (int s0 = 0; s0 < n; s0 += chunk) {
     const int m = std::min(chunk, n - s0);
     HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), d_desc + s0, m, max_w, d_in, d_out,
-                                  d_res + s0, c->est.as<uint16_t>(), nullptr, nullptr, c->order.as<int>(), s));
+                                  d_res + s0, c->est.as<uint16_t>(), nullptr, nullptr, c->order_or_null(), s));
   }
   return AVR_OK;
 }
@@ -843,9 +878,58 @@ int avr_pack_outputs(avr_ctx* c, const avr_slice_desc* d_desc, const avr_slice_r
   return AVR_OK;
 }
 
+int avr_container_describe(const uint8_t* in, size_t n, char** json, uint8_t** reserialized, size_t* len) {
+  if (!in || !json || !reserialized || !len) return AVR_ERR_INVALID_ARGUMENT;
+  *json = nullptr;
+  *reserialized = nullptr;
+  std::vector<avr::PbBlock> blocks;
+  std::string version;
+  bool has_md = false;
+  if (!avr::pb_parse(in, n, &blocks, &version, &has_md)) return AVR_ERR_FORMAT;
+  static const char* hexd = "0123456789abcdef";
+  auto hex = [&](const uint8_t* p, size_t k) {
+    std::string h;
+    h.reserve(2 * k);
+    for (size_t i = 0; i < k; i++) h += hexd[p[i] >> 4], h += hexd[p[i] & 15];
+    return h;
+  };
+  std::string j = "{\"version\": ";
+  j += has_md ? "\"" + hex((const uint8_t*)version.data(), version.size()) + "\"" : std::string("null");
+  j += ", \"blocks\": [";
+  std::vector<uint8_t> o;
+  if (has_md) avr::pb_put_metadata_version(&o, version);
+  for (size_t i = 0; i < blocks.size(); i++) {
+    const avr::PbBlock& b = blocks[i];
+    std::string e;
+    auto add = [&](const std::string& kv) { e += (e.empty() ? "" : ", ") + kv; };
+    if (b.has_size) add("\"size\": " + std::to_string(b.size));
+    if (b.has_literal) add("\"literal\": \"" + hex(b.literal, b.literal_len) + "\"");
+    if (b.has_skip) add(std::string("\"skip_coded\": ") + (b.skip_coded ? "true" : "false"));
+    if (b.has_cabac) add("\"cabac\": \"" + hex(b.cabac, b.cabac_len) + "\"");
+    if (b.has_parity) add(std::string("\"length_parity\": ") + (b.length_parity ? "true" : "false"));
+    if (b.has_last_byte) add("\"last_byte\": \"" + hex((const uint8_t*)b.last_byte.data(), b.last_byte.size()) + "\"");
+    j += (i ? ", {" : "{") + e + "}";
+    avr::pb_put_block(&o, b);
+  }
+  j += "]}";
+  *json = (char*)malloc(j.size() + 1);
+  *reserialized = (uint8_t*)malloc(o.size() ? o.size() : 1);
+  if (!*json || !*reserialized) {
+    free(*json);
+    free(*reserialized);
+    *json = nullptr;
+    *reserialized = nullptr;
+    return AVR_ERR_OUT_OF_MEMORY;
+  }
+  memcpy(*json, j.c_str(), j.size() + 1);
+  if (!o.empty()) memcpy(*reserialized, o.data(), o.size());
+  *len = o.size();
+  return AVR_OK;
+}
+
 int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t** out, size_t* out_len) {
   if (!c || !p || n <= 0 || !out || !out_len || p->mb_width <= 0 || p->mb_height <= 0 || p->slice_type < 0 ||
-      p->slice_type > 2 || p->chroma_format_idc < 1 || p->chroma_format_idc > 3)
+      p->slice_type > 2 || p->chroma_format_idc < 1 || p->chroma_format_idc > 3 || p->gop_length < 0)
     return AVR_ERR_INVALID_ARGUMENT;
   HIP_TRY(c, hipSetDevice(c->device));
   Plan plan;
@@ -859,13 +943,14 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
     first_of.push_back(first);
     avr_slice_desc d;
     memset(&d, 0, sizeof(d));
-    d.slice_type = p->slice_type;
+    const int st = (p->gop_length > 0 && pic % p->gop_length == 0) ? 2 : p->slice_type;
+    d.slice_type = st;
     d.slice_qp = p->slice_qp;
-    d.cabac_init_idc = p->slice_type == 2 ? -1 : 0;
+    d.cabac_init_idc = st == 2 ? -1 : 0;
     d.mb_width = p->mb_width;
     d.mb_height = p->mb_height;
-    d.num_ref_idx_l0 = p->slice_type == 2 ? 0 : std::max(1, p->num_ref_idx_l0);
-    d.num_ref_idx_l1 = p->slice_type == 1 ? std::max(1, p->num_ref_idx_l1) : 0;
+    d.num_ref_idx_l0 = st == 2 ? 0 : std::max(1, p->num_ref_idx_l0);
+    d.num_ref_idx_l1 = st == 1 ? std::max(1, p->num_ref_idx_l1) : 0;
     d.chroma_array_type = p->chroma_format_idc;
     d.transform_8x8_mode = p->transform_8x8_mode;
     d.direct_8x8_inference = 1;
@@ -887,8 +972,8 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
   avr::synth_write_parameter_sets(&stream, *p);
   for (int i = 0; i < (int)plan.descs.size(); i++) {
     if (res[i].status != 0) return fail(c, AVR_ERR_DEVICE, "generator failed on slice " + std::to_string(i));
-    avr::synth_write_slice(&stream, *p, pic_of[i], first_of[i], outb.data() + plan.descs[i].out_offset,
-                           res[i].out_len);
+    avr::synth_write_slice(&stream, *p, plan.descs[i].slice_type, pic_of[i], first_of[i],
+                           outb.data() + plan.descs[i].out_offset, res[i].out_len);
   }
   *out = (uint8_t*)malloc(stream.size());
   if (!*out) return AVR_ERR_OUT_OF_MEMORY;

@@ -108,25 +108,38 @@ bool parse_sps(const uint8_t* r, size_t n, Sps* sps_table) {
       for (int i = 0; i < (s.chroma_format_idc != 3 ? 8 : 12); i++)
         if (b.u1()) skip_scaling_list(b, i < 6 ? 16 : 64);
   }
-  s.log2_max_frame_num = 4 + (int)b.ue();
+  // spec ranges (7.4.2.1.1): log2_max_frame_num_minus4, log2_max_pic_order_cnt_lsb_minus4 <= 12,
+  // pic_order_cnt_type <= 2; anything else is a corrupt SPS (and would make u(n) loop)
+  const uint32_t lfn = b.ue();
+  if (lfn > 12) return false;
+  s.log2_max_frame_num = 4 + (int)lfn;
   s.poc_type = (int)b.ue();
+  if (s.poc_type > 2) return false;
   if (s.poc_type == 0) {
-    s.log2_max_poc_lsb = 4 + (int)b.ue();
+    const uint32_t lpoc = b.ue();
+    if (lpoc > 12) return false;
+    s.log2_max_poc_lsb = 4 + (int)lpoc;
   } else if (s.poc_type == 1) {
     s.delta_pic_order_always_zero = (int)b.u1();
     b.se();
     b.se();
     uint32_t k = b.ue();
+    if (k > 255) return false;
     for (uint32_t i = 0; i < k && !b.err(); i++) b.se();
   }
   b.ue();
   b.u1();
-  s.mb_width = 1 + (int)b.ue();
-  int map_h = 1 + (int)b.ue();
+  const uint32_t wm1 = b.ue(), hm1 = b.ue();
+  if (wm1 >= 1024 || hm1 >= 1024) return false;
+  s.mb_width = 1 + (int)wm1;
+  int map_h = 1 + (int)hm1;
   s.frame_mbs_only = (int)b.u1();
   if (!s.frame_mbs_only) s.mb_aff = (int)b.u1();
   s.direct_8x8_inference = (int)b.u1();
   s.mb_height = (2 - s.frame_mbs_only) * map_h;
+  // bound the picture (level 6.2 allows 139264 macroblocks per frame) so that mb_width * mb_height
+  // and the device frame sizing (W * H * 52 bytes) cannot overflow
+  if ((int64_t)s.mb_width * s.mb_height > 139264) return false;
   if (b.err()) return false;
   s.valid = true;
   sps_table[id] = s;
@@ -317,7 +330,8 @@ bool read_box(const uint8_t* f, size_t off, size_t lim, Box* b) {
   } else if (sz == 0) {
     sz = lim - off;
   }
-  if (sz < hdr || off + sz > lim) return false;
+  // sz > lim - off, not off + sz > lim: a 64-bit size must not wrap the end below the body
+  if (sz < hdr || off >= lim || sz > (uint64_t)(lim - off)) return false;
   b->body = off + hdr;
   b->end = off + (size_t)sz;
   return true;
@@ -399,12 +413,15 @@ bool demux_mp4(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
   uint32_t sample = 0;
   for (uint32_t e = 0; e < nstsc && sample < nsamples; e++) {
     const uint32_t first = rd32(stsc + 8 + 12 * e), per = rd32(stsc + 12 + 12 * e);
-    const uint32_t last = e + 1 < nstsc ? rd32(stsc + 8 + 12 * (e + 1)) - 1 : nchunks;
+    const uint32_t next_first = e + 1 < nstsc ? rd32(stsc + 8 + 12 * (e + 1)) : nchunks + 1;
+    // chunk numbers are 1-based and increase from entry to entry (ISO/IEC 14496-12 8.7.4)
+    if (first == 0 || next_first <= first) return false;
+    const uint32_t last = next_first - 1;
     for (uint32_t c = first; c <= last && c <= nchunks && sample < nsamples; c++) {
       size_t coff = video.co64 ? (size_t)rd64(stco + 8 + 8 * (c - 1)) : rd32(stco + 8 + 4 * (c - 1));
       for (uint32_t s = 0; s < per && sample < nsamples; s++, sample++) {
         size_t ssz = fixed ? fixed : rd32(stsz + 12 + 4 * sample);
-        if (coff + ssz > n) return false;
+        if (coff > n || ssz > n - coff) return false;
         for (size_t q = coff, qe = coff + ssz; q + (size_t)len_size <= qe;) {
           size_t l = 0;
           for (int k = 0; k < len_size; k++) l = l << 8 | f[q + k];
@@ -539,9 +556,10 @@ void pb_put_metadata_version(std::vector<uint8_t>* o, const std::string& version
   bytes_field(o, 1, m.data(), m.size());
 }
 
-bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version) {
+bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version, bool* has_metadata) {
   blocks->clear();
   version->clear();
+  if (has_metadata) *has_metadata = false;
   const uint8_t *p = in, *e = in + n;
   while (p < e) {
     uint64_t tag, len;
@@ -555,6 +573,7 @@ bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::st
     const uint8_t *q = p, *qe = p + len;
     p += len;
     if (field == 1) {  // Metadata
+      if (has_metadata) *has_metadata = true;
       while (q < qe) {
         uint64_t t2, l2;
         if (!rd_varint(&q, qe, &t2)) return false;

@@ -78,7 +78,8 @@ struct PbBlock {
 };
 void pb_put_block(std::vector<uint8_t>* o, const PbBlock& b);
 void pb_put_metadata_version(std::vector<uint8_t>* o, const std::string& version);
-bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version);
+bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version,
+              bool* has_metadata = nullptr);
 
 extern const char* const kParallelModelTag;   // Recoded.Metadata.version for the parallel model
 constexpr int kSurrogateMarkerBytes = 8;      // recode.cpp:27

@@ -22,6 +22,8 @@ constexpr int kEstGlobal = kEstLog + 2 * kEstLogCap;
 static_assert(kEstGlobal % 8 == 0 && kEstTable % 8 == 0, "16-byte clears");
 
 size_t shared_bytes(int max_mb_width);
+// does workgroup b of a 4G-workgroup launch land on CU group b mod G (schedule_kernel's assumption)?
+hipError_t probe_round_robin(size_t lds, bool* ok);
 // mode: 0 compress, 1 decompress, 2 generate, 3 trace (decode-only bin trace).  sequential = reference model (single wavefront).
 hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
                          int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,

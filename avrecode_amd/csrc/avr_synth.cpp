@@ -101,22 +101,22 @@ void synth_write_parameter_sets(std::vector<uint8_t>* out, const avr_synth_param
   put_nal(out, 3, 8, q.bytes);
 }
 
-void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int index, int first_mb,
-                       const uint8_t* payload, size_t payload_len) {
-  const bool idr = p.slice_type == 2;
+void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int slice_type, int index,
+                       int first_mb, const uint8_t* payload, size_t payload_len) {
+  const bool idr = slice_type == 2;
   BitWriter h;
   h.ue((uint32_t)first_mb);      // first_mb_in_slice
-  h.ue((uint32_t)p.slice_type + 5);
+  h.ue((uint32_t)slice_type + 5);
   h.ue(0);                       // pps id
   h.u(idr ? 0 : (uint32_t)(index & 0xffff), 16);
   if (idr) h.ue((uint32_t)(index & 0xffff));
-  if (p.slice_type == 1) h.u(1, 1);           // direct_spatial_mv_pred_flag
-  if (p.slice_type != 2) {
+  if (slice_type == 1) h.u(1, 1);           // direct_spatial_mv_pred_flag
+  if (slice_type != 2) {
     h.u(1, 1);                                // num_ref_idx_active_override_flag
     h.ue((uint32_t)(p.num_ref_idx_l0 > 0 ? p.num_ref_idx_l0 - 1 : 0));
-    if (p.slice_type == 1) h.ue((uint32_t)(p.num_ref_idx_l1 > 0 ? p.num_ref_idx_l1 - 1 : 0));
+    if (slice_type == 1) h.ue((uint32_t)(p.num_ref_idx_l1 > 0 ? p.num_ref_idx_l1 - 1 : 0));
     h.u(0, 1);                                // ref_pic_list_modification_flag_l0
-    if (p.slice_type == 1) h.u(0, 1);
+    if (slice_type == 1) h.u(0, 1);
   }
   if (idr) {
     h.u(0, 1);
@@ -124,7 +124,7 @@ void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int
   } else {
     h.u(0, 1);                                // adaptive_ref_pic_marking_mode_flag
   }
-  if (p.slice_type != 2) h.ue(0);             // cabac_init_idc
+  if (slice_type != 2) h.ue(0);             // cabac_init_idc
   h.se(p.slice_qp - 26);
   h.ue(1);                                    // disable_deblocking_filter_idc
   h.align_ones();                             // cabac_alignment_one_bit

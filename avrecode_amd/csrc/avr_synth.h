@@ -8,6 +8,7 @@
 
 namespace avr {
 void synth_write_parameter_sets(std::vector<uint8_t>* out, const avr_synth_params& p);
-void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int index, int first_mb,
-                       const uint8_t* payload, size_t payload_len);
+// slice_type: this slice's type (avr_synth_params.gop_length may make it differ from p.slice_type)
+void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int slice_type, int index,
+                       int first_mb, const uint8_t* payload, size_t payload_len);
 }  // namespace avr

@@ -237,6 +237,15 @@ AVR_FI uint32_t cu_cell() {
   if (__lane_id() == 0) slot = atomicAdd(&avr_cu_count[cu], 1u);
   return cu * 4 + (__builtin_amdgcn_readfirstlane(slot) & 3);
 }
+// Host side: zero this translation unit's board before a launch (stream-ordered).
+static inline hipError_t reset_cu_board(hipStream_t stream) {
+  void *cnt = nullptr, *rem = nullptr;
+  hipError_t e = hipGetSymbolAddress(&cnt, HIP_SYMBOL(avr_cu_count));
+  if (e == hipSuccess) e = hipGetSymbolAddress(&rem, HIP_SYMBOL(avr_cu_rem));
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(avr_cu_count), stream);
+  if (e == hipSuccess) e = hipMemsetAsync(rem, 0, sizeof(avr_cu_rem), stream);
+  return e;
+}
 AVR_FI void cu_post(uint32_t cell, uint32_t rem) {
   if (__lane_id() == 0) __hip_atomic_store(&avr_cu_rem[cell], rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }

@@ -116,8 +116,11 @@ def sharded_compress(ctx, data: bytes, device=None) -> bytes | None:
         rec = b.recoded()
         status = [0 if v[k] == 1 else -1 for k in range(hi - lo)]
         blobs = [rec[k] if v[k] == 1 else b"" for k in range(hi - lo)]
-    backend = dist.get_backend()
-    dev = device if (device is not None and backend == "nccl") else torch.device("cpu")
+    # RCCL ("nccl") moves device tensors only; gloo moves host tensors
+    if dist.get_backend() == "nccl":
+        dev = device if device is not None else torch.device("cuda", ctx.device)
+    else:
+        dev = torch.device("cpu")
     g = gather_blocks(blobs, status, dst=0, device=dev)
     if g is None:
         return None

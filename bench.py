@@ -22,6 +22,10 @@ traffic: HBM bytes per launch of that kernel from rocprofv3 FETCH_SIZE/WRITE_SIZ
 cpu_baseline: the oracle (CPU restatement of the reference algorithm, oracle/) compress +
 decompress of the first slices of the same batch on one host core (value), and on all host
 threads (all_cores), ~10-30 s.
+file_roundtrip (rank 0, N=1): the north-star command `recode roundtrip <file>` (recode.cpp:1594-1624)
+on whole files from host memory -- both fixtures and the BASELINE configs[1] clip (1080p, 64 frames,
+I + 31 P twice, QP 26) -- in both model modes, with the CPU oracle's R-mode single-core roundtrip
+beside each.
 """
 import argparse
 import json
@@ -126,6 +130,77 @@ def cpu_baseline(ctx, args, n_bytes_hint):
     return line
 
 
+CLIP_GOP = 32        # BASELINE configs[1]: 64 frames x 1 slice, GOP I + 31 P (twice), QP 26, 1080p
+
+
+def make_clip(ctx, args, frames=64):
+    """BASELINE configs[1] / SURVEY 8d config 2: a 1080p High 4:2:0 clip, one slice per frame,
+    I + 31 P twice, QP 26, seed 0 -- consecutive frames, so the reference model's previous-frame
+    nnz contexts (recode.cpp:824-843, 884, 910) are live."""
+    import avrecode_amd as avr
+    return ctx.synthesize(avr.SynthParams(mb_width=args.mb_width, mb_height=args.mb_height, slice_type=0,
+                                          slice_qp=26, chroma_format_idc=1, transform_8x8_mode=1, seed=0,
+                                          gop_length=CLIP_GOP), frames)
+
+
+def _oracle_roundtrip_s(path):
+    """CPU oracle, R-mode (the reference's own model and thread count, recode.cpp:122), one core:
+    `recode_oracle roundtrip file` -> (compress s, decompress s) as it prints them."""
+    import re
+    import subprocess
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _oracle
+    _, cli = _oracle.build_oracle()
+    r = subprocess.run([str(cli), "roundtrip", str(path)], capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return None
+    m = re.search(r"compress ([0-9.]+)s decompress ([0-9.]+)s", r.stdout)
+    return (float(m.group(1)), float(m.group(2))) if m else None
+
+
+def file_roundtrips(ctx, args):
+    """The north-star command, `recode roundtrip <file>` (recode.cpp:1594-1624), on whole files from
+    host memory: avr_roundtrip_file = demux + compress (device) + container + decompress (device) +
+    byte compare, both model modes.  MB/s = file bytes / wall time of one roundtrip call (median of
+    the timed reps after one untimed warm-up; PCIe copies and host container work included).  Beside
+    each file: the CPU oracle's R-mode roundtrip on one host core."""
+    import tempfile
+    import avrecode_amd as avr
+    files = [(name, (ROOT / "tests" / "fixtures" / name).read_bytes()) for name in ("realshort.mp4", "cockatoo.mp4")]
+    if not args.no_clip:
+        files.append(("clip_1080p_64f_IP31_qp26 (configs[1])", make_clip(ctx, args)))
+    out = {}
+    for name, data in files:
+        rec = {"bytes": len(data)}
+        for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+            avrc, st = ctx.roundtrip(data, model)   # warm-up (raises on any mismatch)
+            walls, comps, decs = [], [], []
+            for _ in range(args.file_reps):
+                t0 = time.perf_counter()
+                avrc, st = ctx.roundtrip(data, model)
+                walls.append(time.perf_counter() - t0)
+                comps.append(st["compress_s"])
+                decs.append(st["decompress_s"])
+            k = sorted(range(len(walls)), key=walls.__getitem__)[len(walls) // 2]
+            rec[tag] = {"MB_s": len(data) / walls[k] / 1e6, "wall_s": walls[k], "compress_s": comps[k],
+                        "decompress_s": decs[k], "avrc_bytes": len(avrc), "ratio": len(avrc) / len(data),
+                        "slices": int(st["slices"]), "coded": int(st["coded_slices"]), "bit_exact": True}
+        if args.no_cpu_baseline:
+            out[name] = rec
+            continue
+        with tempfile.NamedTemporaryFile(suffix=".264", delete=False) as fh:
+            fh.write(data)
+        try:
+            cpu = _oracle_roundtrip_s(fh.name)
+        finally:
+            os.unlink(fh.name)
+        if cpu:
+            rec["cpu_oracle_R_1core"] = {"MB_s": len(data) / sum(cpu) / 1e6, "compress_s": cpu[0],
+                                         "decompress_s": cpu[1], "cores": 1, "kind": "port"}
+        out[name] = rec
+    return out
+
+
 def load_traffic(args, kernel):
     p = ROOT / "profiles" / f"{args.round}_pmc.json"
     if not p.exists():
@@ -150,7 +225,10 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r01")
+    ap.add_argument("--round", default="r02")
+    ap.add_argument("--file-reps", type=int, default=3)
+    ap.add_argument("--no-files", action="store_true", help="skip the whole-file roundtrips")
+    ap.add_argument("--no-clip", action="store_true", help="skip the configs[1] clip in the file roundtrips")
     args = ap.parse_args()
 
     import numpy as np
@@ -260,6 +338,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ctx, args, len(data))
+        if world == 1 and not args.no_files:
+            line["file_roundtrip"] = file_roundtrips(ctx, args)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

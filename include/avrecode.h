@@ -152,6 +152,14 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
 int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
                            const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len);
 
+/* Container codec check (host only): parse a Recoded protobuf (recode.proto:1-19) with the
+ * library's own wire codec -- the one avr_decompress_file uses -- and return (a) its fields as JSON,
+ * {"version": null | hex, "blocks": [{"size": int, "literal": hex, "skip_coded": bool, "cabac": hex,
+ * "length_parity": bool, "last_byte": hex}, ...]} with only the fields present, and (b) the message
+ * re-serialised by the library's writer (the one avr_compress_file uses; Metadata.version only).
+ * Both buffers are malloc'd (avr_free).  AVR_ERR_FORMAT when the bytes are not a Recoded message. */
+int avr_container_describe(const uint8_t* in, size_t n, char** json, uint8_t** reserialized, size_t* len);
+
 /* ------------------------------------------------ libavcodec-hooks callback surface (AVCodecHooks) */
 /* For a caller that drives the recode path from its own H.264 decoder exactly as the reference's
  * libavcodec-hooks fork does (recode.cpp:137-228).  A session runs the whole file on the device up
@@ -205,10 +213,13 @@ typedef struct {
   int32_t num_ref_idx_l0, num_ref_idx_l1;
   uint64_t seed;
   int32_t slices_per_picture;    /* 0 or 1: one slice per picture; k: k slices (equal MB runs) */
-  int32_t reserved;
+  int32_t gop_length;            /* 0: every picture has slice_type; g > 0: picture i is an IDR
+                                  * I picture when i % g == 0, else slice_type (e.g. I + 31 P) */
 } avr_synth_params;
 /* Generate n pictures on the device (each slices_per_picture slices, in decode order) and return
- * them as one Annex-B stream (SPS/PPS + the slice NAL units) in host memory. */
+ * them as one Annex-B stream (SPS/PPS + the slice NAL units) in host memory.  Pictures are
+ * consecutive frames (frame_num / idr_pic_id = picture index), so the reference model's
+ * previous-frame contexts (recode.cpp:824-843, 884) see each P picture's predecessor. */
 int avr_synthesize_stream(avr_ctx* ctx, const avr_synth_params* params, int n, uint8_t** out, size_t* out_len);
 
 #ifdef __cplusplus
