@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "avr_create", "avr_destroy", "avr_last_error", "avr_free", "avr_compress_file", "avr_decompress_file",
     "avr_roundtrip_file", "avr_compress_slices", "avr_decompress_slices", "avr_pack_outputs",
     "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream", "avr_assemble_container", "avr_synthesize_stream",
-    "avr_container_describe",
+    "avr_container_describe", "avr_compress_files", "avr_decompress_files",
     "avr_hooks_compress_begin", "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
     "avr_hook_get_bypass", "avr_hook_get_terminate", "avr_hook_skip_bytes", "avr_hook_frame_spec", "avr_hook_mb_xy",
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
@@ -78,7 +78,8 @@ class _SynthParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
                 ("mb_width", "mb_height", "slice_type", "slice_qp", "chroma_format_idc", "transform_8x8_mode",
                  "num_ref_idx_l0", "num_ref_idx_l1")] + [("seed", ctypes.c_uint64)] + \
-               [("slices_per_picture", ctypes.c_int32), ("gop_length", ctypes.c_int32)]
+               [("slices_per_picture", ctypes.c_int32), ("gop_length", ctypes.c_int32), ("repeat", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 @dataclass
@@ -95,6 +96,7 @@ class SynthParams:
     seed: int = 0
     slices_per_picture: int = 1
     gop_length: int = 0          # > 0: IDR I picture every gop_length pictures, slice_type between
+    repeat: int = 1              # > 1: the pictures written this many times (frame numbers advance)
 
 
 _lib = None
@@ -132,6 +134,8 @@ def lib() -> ctypes.CDLL:
     L.avr_assemble_container.argtypes = [vp, sz, i32, vp, vp, vp, vp, pp, psz]
     L.avr_synthesize_stream.argtypes = [vp, ctypes.POINTER(_SynthParams), i32, pp, psz]
     L.avr_container_describe.argtypes = [vp, sz, pp, pp, psz]
+    L.avr_compress_files.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
+    L.avr_decompress_files.argtypes = [vp, i32, vp, vp, vp, vp, vp]
     for name in EXPORTED_SYMBOLS:   # fails here, not at first use, when the build is stale
         getattr(L, name)
     _lib = L
@@ -274,6 +278,32 @@ class Context:
         stats = {f: getattr(st, f) for f, _ in _FileStats._fields_}
         return _take(out, olen.value), stats
 
+    def _files(self, fn, datas, *extra):
+        n = len(datas)
+        keep = [_buf(d) for d in datas]
+        ptrs = (ctypes.c_void_p * max(1, n))(*[k[0].value for k in keep])
+        lens = (ctypes.c_size_t * max(1, n))(*[k[1] for k in keep])
+        outs = (ctypes.c_void_p * max(1, n))()
+        olens = (ctypes.c_size_t * max(1, n))()
+        st = (ctypes.c_int32 * max(1, n))()
+        self._check(fn(self._h, n, ptrs, lens, *extra, outs, olens, st), fn.__name__)
+        res = []
+        for k in range(n):
+            if st[k] != AVR_OK:
+                res.append(AvrError(st[k], f"file {k}: {lib().avr_last_error(self._h).decode(errors='replace')}"))
+            else:
+                res.append(_take(ctypes.c_void_p(outs[k]), olens[k]))
+        del keep
+        return res
+
+    def compress_files(self, datas, model: int = MODEL_REFERENCE) -> list:
+        """avr_compress_files: one container (bytes) or AvrError per input file."""
+        return self._files(lib().avr_compress_files, datas, model)
+
+    def decompress_files(self, datas) -> list:
+        """avr_decompress_files: the original file (bytes) or AvrError per container."""
+        return self._files(lib().avr_decompress_files, datas)
+
     # ------------------------------------------------------- device-resident slice batches
     # All tensor arguments are torch tensors on this context's device (uint8 buffers, and uint8
     # views of descriptor/result arrays); `stream` is a torch.cuda.Stream or None (= its current).
@@ -323,7 +353,8 @@ class Context:
     def synthesize(self, params: SynthParams, n: int) -> bytes:
         sp = _SynthParams(params.mb_width, params.mb_height, params.slice_type, params.slice_qp,
                           params.chroma_format_idc, params.transform_8x8_mode, params.num_ref_idx_l0,
-                          params.num_ref_idx_l1, params.seed, params.slices_per_picture, params.gop_length)
+                          params.num_ref_idx_l1, params.seed, params.slices_per_picture, params.gop_length,
+                          params.repeat, 0)
         out, olen = ctypes.c_void_p(), ctypes.c_size_t()
         self._check(lib().avr_synthesize_stream(self._h, ctypes.byref(sp), int(n), ctypes.byref(out),
                                                 ctypes.byref(olen)), "synthesize")

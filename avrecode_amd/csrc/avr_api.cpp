@@ -47,6 +47,7 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
   }
+  ~DevBuf() { release(); }
   template <class T>
   T* as() const {
     return (T*)p;
@@ -66,6 +67,7 @@ struct avr_ctx {
   DevBuf tables, est, frames, frame_meta, in, out, descs, res, packed, offsets, order;
   DevBuf rm_goff, rm_counts, rm_stop, rm_off, rm_ops;   // parallel reference-model compress
   DevBuf regen, dec_descs, res_d, verdict;               // compress-side roundtrip check
+  DevBuf file_first, file_op_off;                        // reference model over several files
   bool round_robin = false;   // placement probe passed: the CU schedule (order) may be used
   int* order_or_null() { return round_robin ? order.as<int>() : nullptr; }
 };
@@ -198,6 +200,12 @@ struct Plan {
   std::vector<avr_slice_desc> descs;
   std::vector<uint8_t> arena;   // payloads (compress) or recoded streams (decompress)
   int max_w = 1;
+  // sequential (reference-model) plans over several files: file f is descs[file_first[f] ..
+  // file_first[f + 1]); empty = one file
+  std::vector<int> file_first;
+  int n_files() const { return file_first.empty() ? 1 : (int)file_first.size() - 1; }
+  int file_begin(int f) const { return file_first.empty() ? 0 : file_first[f]; }
+  int file_end(int f) const { return file_first.empty() ? (int)descs.size() : file_first[f + 1]; }
 };
 
 void append_aligned(std::vector<uint8_t>* arena, const uint8_t* p, size_t n, size_t extra, uint64_t* off) {
@@ -235,11 +243,20 @@ constexpr int kRModeFallback = 1;
 // frame is left to the sequential kernel (kRModeFallback), as is a plan too large for one pass.
 int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total) {
   const int n = (int)plan.descs.size();
+  const int nf = plan.n_files();
+  if (nf > avr::rmode_max_files_per_pass()) return kRModeFallback;
   struct Fb { int gen = -1, w = 0, h = 0, fid = 0; } fb[2];
   int cur = 0;
   std::vector<int64_t> gen_off, goff(2 * (size_t)n);
   int64_t fbytes = 0;
+  std::vector<char> file_start(n + 1, 0);
+  for (int f = 0; f < nf; f++) file_start[plan.file_begin(f)] = 1;
   for (int k = 0; k < n; k++) {
+    if (file_start[k]) {   // a new file: a fresh model, frames of its own
+      fb[0] = Fb();
+      fb[1] = Fb();
+      cur = 0;
+    }
     const avr_slice_desc& d = plan.descs[k];
     const int W = d.mb_width, H = d.mb_height;
     if (fb[cur].w != W || fb[cur].h != H || !(fb[cur].fid == d.picture_id && fb[cur].w && fb[cur].h)) {
@@ -286,7 +303,12 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total) {
   const uint64_t N = off[n];
   if (N >= (1ull << 30)) return kRModeFallback;
   HIP_TRY(c, hipMemcpyAsync(c->rm_off.p, off.data(), sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, c->stream));
-  const size_t tb = avr::rmode_sort_temp_bytes(N);
+  std::vector<uint64_t> fop(nf + 1);
+  for (int f = 0; f <= nf; f++) fop[f] = off[f < nf ? plan.file_begin(f) : n];
+  HIP_TRY(c, c->file_op_off.reserve(sizeof(uint64_t) * (nf + 1)));
+  HIP_TRY(c, hipMemcpyAsync(c->file_op_off.p, fop.data(), sizeof(uint64_t) * (nf + 1), hipMemcpyHostToDevice,
+                            c->stream));
+  const size_t tb = avr::rmode_sort_temp_bytes(N, nf);
   HIP_TRY(c, c->rm_ops.reserve(sizeof(uint32_t) * (N + 1) * 6 + tb + 256));
   uint32_t* ops = c->rm_ops.as<uint32_t>();
   uint32_t* keys = ops + (N + 1);
@@ -300,7 +322,8 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total) {
                                c->in.as<uint8_t>(), c->frames.as<uint8_t>(), c->rm_goff.as<int64_t>(),
                                c->rm_counts.as<uint32_t>(), ops, c->rm_off.as<uint64_t>(),
                                c->res.as<avr_slice_result>(), c->rm_stop.as<int32_t>(), c->stream));
-  HIP_TRY(c, avr::launch_rmode_estimators(ops, N, keys, vals, skeys, svals, temp, tb, rops, c->stream));
+  HIP_TRY(c, avr::launch_rmode_estimators(ops, N, c->file_op_off.as<uint64_t>(), nf, keys, vals, skeys, svals, temp,
+                                          tb, rops, c->stream));
   HIP_TRY(c, avr::launch_rcode(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, rops,
                                c->rm_off.as<uint64_t>(), c->rm_counts.as<uint32_t>(), c->out.as<uint8_t>(),
                                c->res.as<avr_slice_result>(), c->rm_stop.as<int32_t>(), c->stream));
@@ -340,15 +363,26 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
   if (sequential && rm == AVR_OK) {
     // done: the parallel reference-model compress
   } else if (sequential) {
-    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * avr::kEstGlobal, true));
+    // one workgroup per file (the reference model is sequential within a file only)
+    const int nf = plan.n_files();
+    avr::SeqFiles sf;
+    sf.n_files = nf;
     size_t fbytes = 0;
     for (auto& d : plan.descs) fbytes = std::max(fbytes, (size_t)2 * d.mb_width * d.mb_height * 52);
-    HIP_TRY(c, c->frames.reserve(fbytes + 64));
-    HIP_TRY(c, c->frame_meta.reserve(64));
+    sf.frame_stride = (fbytes + 255) & ~(size_t)255;
+    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * avr::kEstGlobal * (size_t)nf, true));
+    HIP_TRY(c, c->frames.reserve(sf.frame_stride * nf + 64));
+    HIP_TRY(c, c->frame_meta.reserve(sizeof(int) * (size_t)nf + 64));
+    if (!plan.file_first.empty()) {
+      HIP_TRY(c, c->file_first.reserve(sizeof(int) * plan.file_first.size()));
+      HIP_TRY(c, hipMemcpyAsync(c->file_first.p, plan.file_first.data(), sizeof(int) * plan.file_first.size(),
+                                hipMemcpyHostToDevice, c->stream));
+      sf.file_first = c->file_first.as<int>();
+    }
     HIP_TRY(c, avr::launch_slices(mode, true, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n,
                                   plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(), c->res.as<avr_slice_result>(),
                                   c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), nullptr,
-                                  c->stream));
+                                  c->stream, sf));
   } else {
     const int chunk = std::min(n, kMaxSlicesPerLaunch);
     HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk, true));
@@ -476,6 +510,296 @@ int emit_container(const uint8_t* in, size_t n, const ParsedFile& pf, const std:
   return AVR_OK;
 }
 
+// compressor::run (recode.cpp:1102-1132) for several files at once.  The device work of every
+// file is batched: one parallel launch checks every candidate slice of every file (parse, restore,
+// device roundtrip), and the reference model runs all files in one pass (the parallel R-mode
+// pipeline over all their slices with per-file estimators, or one workgroup per file).  out[f] is
+// malloc'd; status[f] (optional) is file f's result; the return value is the first failure.
+int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* in_len, int model, uint8_t** out,
+                   size_t* out_len, int32_t* status) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  std::vector<int32_t> st(nf, AVR_OK);
+  std::vector<ParsedFile> pf(nf);
+  for (int f = 0; f < nf; f++) {
+    out[f] = nullptr;
+    out_len[f] = 0;
+    st[f] = parse_file(c, in[f], in_len[f], &pf[f]);
+  }
+  // 1) every candidate slice of every file through the parallel kernel: per-slice parse, restore
+  //    check and device roundtrip (and the parallel model's output)
+  Plan plan;
+  std::vector<std::vector<int>> cand_of(nf);
+  for (int f = 0; f < nf; f++) {
+    cand_of[f].assign(pf[f].slices.size(), -1);
+    if (st[f]) continue;
+    for (size_t i = 0; i < pf[f].slices.size(); i++) {
+      const avr::SliceInfo& s = pf[f].slices[i];
+      if (!recodable_candidate(s)) continue;
+      avr_slice_desc d = desc_from_header(s);
+      append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
+      d.payload_size = (uint32_t)s.size;
+      d.read_limit = (uint32_t)s.read_limit;
+      d.out_capacity = (uint32_t)(s.size * 2 + 256);
+      plan.max_w = std::max(plan.max_w, d.mb_width);
+      cand_of[f][i] = (int)plan.descs.size();
+      plan.descs.push_back(d);
+    }
+  }
+  std::vector<avr_slice_result> res;
+  std::vector<uint8_t> outb;
+  if (int r = run_plan(c, 0, false, plan, &res, &outb, /*verify=*/true)) return r;
+  // 2) segmentation (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297)
+  std::vector<std::vector<char>> ok(nf);
+  std::vector<std::vector<const uint8_t*>> found(nf);
+  for (int f = 0; f < nf; f++) {
+    ok[f].assign(pf[f].slices.size(), 0);
+    for (size_t i = 0; i < pf[f].slices.size(); i++) ok[f][i] = cand_of[f][i] >= 0 && res[cand_of[f][i]].status == 0;
+    found[f] = segment(in[f], in_len[f], pf[f], ok[f]);
+  }
+  // 3) reference model: the coded slices of every file in file order, estimators per file; a
+  //    slice that fails there is demoted to skip_coded and its file's pass repeated
+  std::vector<std::vector<std::vector<uint8_t>>> recoded(nf);
+  for (int f = 0; f < nf; f++) recoded[f].resize(pf[f].slices.size());
+  if (model == AVR_MODEL_REFERENCE) {
+    std::vector<char> todo(nf, 0);
+    for (int f = 0; f < nf; f++) todo[f] = st[f] == AVR_OK;
+    for (int attempt = 0;; attempt++) {
+      Plan rp;
+      std::vector<std::pair<int, int>> idx;   // (file, slice) per desc
+      for (int f = 0; f < nf; f++) {
+        if (!todo[f]) continue;
+        rp.file_first.push_back((int)rp.descs.size());
+        for (size_t i = 0; i < pf[f].slices.size(); i++) {
+          const avr::SliceInfo& s = pf[f].slices[i];
+          avr_slice_desc d = desc_from_header(s);
+          d.coded = found[f][i] != nullptr;
+          if (d.coded) {
+            append_aligned(&rp.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
+            d.payload_size = (uint32_t)s.size;
+            d.read_limit = (uint32_t)s.read_limit;
+            d.out_capacity = (uint32_t)(s.size * 4 + 4096);
+          }
+          rp.max_w = std::max(rp.max_w, d.mb_width);
+          idx.push_back({f, (int)i});
+          rp.descs.push_back(d);
+        }
+      }
+      if (rp.file_first.empty()) break;
+      rp.file_first.push_back((int)rp.descs.size());
+      std::vector<avr_slice_result> rr;
+      std::vector<uint8_t> ro;
+      if (int r = run_plan(c, 0, true, rp, &rr, &ro)) return r;
+      std::fill(todo.begin(), todo.end(), 0);
+      for (size_t k = 0; k < idx.size(); k++) {
+        const int f = idx[k].first, i = idx[k].second;
+        if (!found[f][i]) continue;
+        if (rr[k].status != 0) {
+          found[f][i] = nullptr;
+          todo[f] = 1;
+          continue;
+        }
+        recoded[f][i].assign(ro.begin() + rp.descs[k].out_offset,
+                             ro.begin() + rp.descs[k].out_offset + rr[k].out_len);
+      }
+      bool again = false;
+      for (int f = 0; f < nf; f++) {
+        if (!todo[f]) continue;
+        again = true;
+        // a demoted slice changes the literal gaps of later ones: redo the segmentation
+        for (size_t i = 0; i < pf[f].slices.size(); i++) ok[f][i] = ok[f][i] && found[f][i] != nullptr;
+        found[f] = segment(in[f], in_len[f], pf[f], ok[f]);
+        if (attempt == 7) {
+          st[f] = fail(c, AVR_ERR_DEVICE, "reference-model pass did not converge");
+          todo[f] = 0;
+        }
+      }
+      if (!again) break;
+    }
+  } else {
+    for (int f = 0; f < nf; f++)
+      for (size_t i = 0; i < pf[f].slices.size(); i++)
+        if (found[f][i]) {
+          const int k = cand_of[f][i];
+          recoded[f][i].assign(outb.begin() + plan.descs[k].out_offset,
+                               outb.begin() + plan.descs[k].out_offset + res[k].out_len);
+        }
+  }
+  // 4) containers (compressor::run, recode.cpp:1115-1125)
+  int first_err = AVR_OK;
+  for (int f = 0; f < nf; f++) {
+    if (st[f] == AVR_OK) {
+      std::vector<std::pair<const uint8_t*, size_t>> blobs(pf[f].slices.size(), {nullptr, 0});
+      for (size_t i = 0; i < pf[f].slices.size(); i++) blobs[i] = {recoded[f][i].data(), recoded[f][i].size()};
+      st[f] = emit_container(in[f], in_len[f], pf[f], found[f], blobs, model == AVR_MODEL_PARALLEL, &out[f],
+                             &out_len[f]);
+    }
+    if (status) status[f] = st[f];
+    if (st[f] && !first_err) first_err = st[f];
+  }
+  return status ? AVR_OK : first_err;
+}
+
+// decompressor::run (recode.cpp:1312-1357) for several files at once: the slices of every
+// parallel-model file go to one parallel launch, every reference-model file to one workgroup of a
+// sequential launch.
+struct DecJob {
+  std::vector<avr::PbBlock> blocks;
+  std::vector<uint8_t> stream;       // read_packet's stream: literals + surrogate blocks
+  bool parallel = false;
+  std::vector<int> desc_of_block;    // plan index per coded block (-1: none)
+};
+
+int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* plan) {
+  std::string version;
+  if (!avr::pb_parse(in, n, &j->blocks, &version)) return fail(c, AVR_ERR_FORMAT, "not a Recoded protobuf");
+  j->parallel = version == avr::kParallelModelTag;
+  // read_packet (recode.cpp:1359-1409): literals and surrogate blocks form the stream
+  uint64_t seq = 1;
+  for (auto& b : j->blocks) {
+    if ((int)b.has_literal + (int)b.has_cabac + (int)b.has_skip != 1)
+      return fail(c, AVR_ERR_FORMAT, "Invalid input block: must have exactly one type");
+    if (b.has_literal) {
+      j->stream.insert(j->stream.end(), b.literal, b.literal + b.literal_len);
+    } else if (b.has_cabac) {
+      if (!b.has_size) return fail(c, AVR_ERR_FORMAT, "CABAC block requires size field.");
+      if (b.size < avr::kSurrogateMarkerBytes || b.size > ((int64_t)1 << 31))
+        return fail(c, AVR_ERR_FORMAT, "Invalid coded block size for surrogate: " + std::to_string(b.size));
+      uint8_t mk[8];
+      avr::surrogate_marker(seq++, mk);
+      j->stream.insert(j->stream.end(), mk, mk + 8);
+      j->stream.insert(j->stream.end(), (size_t)b.size - 8, (uint8_t)'X');
+    } else if (!b.skip_coded) {
+      return fail(c, AVR_ERR_FORMAT, "Unknown input block type");
+    }
+  }
+  ParsedFile pf;
+  if (int r = parse_file(c, j->stream.data(), j->stream.size(), &pf)) return r;
+  // recognize_coded_block (recode.cpp:1546-1573): slices claim coded blocks in order
+  j->desc_of_block.assign(j->blocks.size(), -1);
+  size_t next_coded = 0;
+  uint64_t seq_check = 1;
+  std::vector<avr_slice_desc> descs;
+  std::vector<int> block_of;
+  Plan local;
+  for (auto& s : pf.slices) {
+    while (next_coded < j->blocks.size() && !j->blocks[next_coded].has_cabac && !j->blocks[next_coded].has_skip)
+      next_coded++;
+    if (next_coded >= j->blocks.size())
+      return fail(c, AVR_ERR_FORMAT, "Coded block expected, but not recorded in the compressed data.");
+    const avr::PbBlock& b = j->blocks[next_coded];
+    if ((size_t)b.size != s.size) return fail(c, AVR_ERR_FORMAT, "Invalid surrogate block size.");
+    avr_slice_desc d = desc_from_header(s);
+    if (b.has_cabac) {
+      uint8_t mk[8];
+      avr::surrogate_marker(seq_check++, mk);
+      if (memcmp(s.payload(), mk, 8) != 0) return fail(c, AVR_ERR_FORMAT, "Invalid surrogate marker in coded block.");
+      d.payload_size = (uint32_t)b.cabac_len;
+      d.read_limit = (uint32_t)b.cabac_len;
+      d.out_capacity = (uint32_t)(b.size + 64);
+    } else {
+      d.coded = 0;
+    }
+    if (j->parallel && !d.coded) {   // the parallel model has no cross-slice state: skip it
+      next_coded++;
+      continue;
+    }
+    block_of.push_back((int)next_coded);
+    descs.push_back(d);
+    next_coded++;
+  }
+  // all checks passed: append to the shared plan
+  for (size_t k = 0; k < descs.size(); k++) {
+    avr_slice_desc d = descs[k];
+    const avr::PbBlock& b = j->blocks[block_of[k]];
+    if (d.coded) append_aligned(&plan->arena, b.cabac, b.cabac_len, 16, &d.payload_offset);
+    plan->max_w = std::max(plan->max_w, d.mb_width);
+    j->desc_of_block[block_of[k]] = (int)plan->descs.size();
+    plan->descs.push_back(d);
+  }
+  return AVR_OK;
+}
+
+int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* in_len, uint8_t** out,
+                     size_t* out_len, int32_t* status) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  std::vector<int32_t> st(nf, AVR_OK);
+  std::vector<DecJob> jobs(nf);
+  Plan pp, rp;   // parallel-model slices; reference-model files (one workgroup each)
+  for (int f = 0; f < nf; f++) {
+    out[f] = nullptr;
+    out_len[f] = 0;
+    std::string version;
+    std::vector<avr::PbBlock> probe;
+    const bool parallel = avr::pb_parse(in[f], in_len[f], &probe, &version) && version == avr::kParallelModelTag;
+    Plan* plan = parallel ? &pp : &rp;
+    const size_t n0 = plan->descs.size();
+    if (!parallel) rp.file_first.push_back((int)n0);
+    st[f] = decompress_setup(c, in[f], in_len[f], &jobs[f], plan);
+    if (st[f]) {   // drop whatever the failed file left (nothing: setup appends only on success)
+      plan->descs.resize(n0);
+      if (!parallel) rp.file_first.pop_back();
+    }
+  }
+  std::vector<avr_slice_result> pres, rres;
+  std::vector<uint8_t> pout, rout;
+  if (!pp.descs.empty())
+    if (int r = run_plan(c, 1, false, pp, &pres, &pout)) return r;
+  if (!rp.file_first.empty()) {
+    rp.file_first.push_back((int)rp.descs.size());
+    if (int r = run_plan(c, 1, true, rp, &rres, &rout)) return r;
+  }
+  int first_err = AVR_OK;
+  for (int f = 0; f < nf; f++) {
+    DecJob& j = jobs[f];
+    const Plan& plan = j.parallel ? pp : rp;
+    const std::vector<avr_slice_result>& res = j.parallel ? pres : rres;
+    const std::vector<uint8_t>& outb = j.parallel ? pout : rout;
+    std::vector<uint8_t> o;
+    if (st[f] == AVR_OK) {
+      o.reserve(j.stream.size());
+      for (size_t i = 0; i < j.blocks.size() && st[f] == AVR_OK; i++) {
+        const avr::PbBlock& b = j.blocks[i];
+        if (b.has_literal) {
+          o.insert(o.end(), b.literal, b.literal + b.literal_len);
+          continue;
+        }
+        if (!b.has_cabac) continue;
+        const int k = j.desc_of_block[i];
+        if (k < 0) {
+          st[f] = fail(c, AVR_ERR_FORMAT, "Not all blocks were decoded.");
+          break;
+        }
+        if (res[k].status != 0) {
+          st[f] = fail(c, AVR_ERR_FORMAT, "slice " + std::to_string(k) + " failed to decode (" +
+                                              std::to_string(res[k].status) + ")");
+          break;
+        }
+        const size_t o0 = o.size();
+        o.insert(o.end(), outb.begin() + plan.descs[k].out_offset,
+                 outb.begin() + plan.descs[k].out_offset + res[k].out_len);
+        // x264 padding correction (recode.cpp:1345-1356)
+        if (b.has_parity && b.has_last_byte && !b.last_byte.empty()) {
+          const size_t len = o.size() - o0;
+          if ((int)b.length_parity != (int)(len & 1)) o.push_back((uint8_t)b.last_byte[0]);
+          else if (len) o.back() = (uint8_t)b.last_byte[0];
+        }
+      }
+    }
+    if (st[f] == AVR_OK) {
+      out[f] = (uint8_t*)malloc(o.size() ? o.size() : 1);
+      if (!out[f]) {
+        st[f] = AVR_ERR_OUT_OF_MEMORY;
+      } else {
+        if (!o.empty()) memcpy(out[f], o.data(), o.size());
+        out_len[f] = o.size();
+      }
+    }
+    if (status) status[f] = st[f];
+    if (st[f] && !first_err) first_err = st[f];
+  }
+  return status ? AVR_OK : first_err;
+}
+
 }  // namespace
 
 // ================================================================================ C ABI
@@ -505,11 +829,9 @@ int avr_create(int device, avr_ctx** out) {
 void avr_destroy(avr_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  for (DevBuf* b : {&c->tables, &c->est, &c->frames, &c->frame_meta, &c->in, &c->out, &c->descs, &c->res, &c->packed,
-                    &c->offsets})
-    b->release();
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  delete c;
+  delete c;   // every DevBuf frees itself
 }
 
 const char* avr_last_error(const avr_ctx* c) { return c ? c->err.c_str() : "no context"; }
@@ -519,85 +841,19 @@ void avr_free(void* p) { free(p); }
 int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** out, size_t* out_len) {
   if (!c || !in || !out || !out_len || (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL))
     return AVR_ERR_INVALID_ARGUMENT;
-  HIP_TRY(c, hipSetDevice(c->device));
-  ParsedFile pf;
-  if (int r = parse_file(c, in, n, &pf)) return r;
-  // 1) every candidate slice through the parallel kernel: per-slice parse + restore check (and
-  //    the parallel model's output)
-  Plan plan;
-  std::vector<int> cand_of(pf.slices.size(), -1);
-  for (size_t i = 0; i < pf.slices.size(); i++) {
-    const avr::SliceInfo& s = pf.slices[i];
-    if (!recodable_candidate(s)) continue;
-    avr_slice_desc d = desc_from_header(s);
-    append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
-    d.payload_size = (uint32_t)s.size;
-    d.read_limit = (uint32_t)s.read_limit;
-    d.out_capacity = (uint32_t)(s.size * 2 + 256);
-    plan.max_w = std::max(plan.max_w, d.mb_width);
-    cand_of[i] = (int)plan.descs.size();
-    plan.descs.push_back(d);
-  }
-  std::vector<avr_slice_result> res;
-  std::vector<uint8_t> outb;
-  if (int r = run_plan(c, 0, false, plan, &res, &outb, /*verify=*/true)) return r;
-  std::vector<char> ok(pf.slices.size(), 0);
-  for (size_t i = 0; i < pf.slices.size(); i++) ok[i] = cand_of[i] >= 0 && res[cand_of[i]].status == 0;
-  // 2) segmentation (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297)
-  std::vector<const uint8_t*> found = segment(in, n, pf, ok);
-  // 3) reference model: re-run the coded slices through the sequential kernel in file order;
-  //    a slice that fails there is demoted to skip_coded and the pass repeated.
-  std::vector<std::vector<uint8_t>> recoded(pf.slices.size());
-  if (model == AVR_MODEL_REFERENCE) {
-    for (int attempt = 0; attempt < 8; attempt++) {
-      Plan rp;
-      std::vector<int> idx;
-      for (size_t i = 0; i < pf.slices.size(); i++) {
-        const avr::SliceInfo& s = pf.slices[i];
-        avr_slice_desc d = desc_from_header(s);
-        d.coded = found[i] != nullptr;
-        if (d.coded) {
-          append_aligned(&rp.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
-          d.payload_size = (uint32_t)s.size;
-          d.read_limit = (uint32_t)s.read_limit;
-          d.out_capacity = (uint32_t)(s.size * 4 + 4096);
-        }
-        rp.max_w = std::max(rp.max_w, d.mb_width);
-        idx.push_back((int)i);
-        rp.descs.push_back(d);
-      }
-      std::vector<avr_slice_result> rr;
-      std::vector<uint8_t> ro;
-      if (int r = run_plan(c, 0, true, rp, &rr, &ro)) return r;
-      bool again = false;
-      for (size_t k = 0; k < idx.size(); k++) {
-        const int i = idx[k];
-        if (!found[i]) continue;
-        if (rr[k].status != 0) {
-          found[i] = nullptr;
-          again = true;
-          continue;
-        }
-        recoded[i].assign(ro.begin() + rp.descs[k].out_offset, ro.begin() + rp.descs[k].out_offset + rr[k].out_len);
-      }
-      if (!again) break;
-      // a demoted slice changes the literal gaps of later ones: redo the segmentation
-      for (size_t i = 0; i < pf.slices.size(); i++) ok[i] = ok[i] && found[i] != nullptr;
-      found = segment(in, n, pf, ok);
-      if (attempt == 7) return fail(c, AVR_ERR_DEVICE, "reference-model pass did not converge");
-    }
-  } else {
-    for (size_t i = 0; i < pf.slices.size(); i++)
-      if (found[i]) {
-        const int k = cand_of[i];
-        recoded[i].assign(outb.begin() + plan.descs[k].out_offset,
-                          outb.begin() + plan.descs[k].out_offset + res[k].out_len);
-      }
-  }
-  // 4) container (compressor::run, recode.cpp:1115-1125)
-  std::vector<std::pair<const uint8_t*, size_t>> blobs(pf.slices.size(), {nullptr, 0});
-  for (size_t i = 0; i < pf.slices.size(); i++) blobs[i] = {recoded[i].data(), recoded[i].size()};
-  return emit_container(in, n, pf, found, blobs, model == AVR_MODEL_PARALLEL, out, out_len);
+  int32_t st = 0;
+  const int r = compress_files(c, 1, &in, &n, model, out, out_len, &st);
+  return r ? r : st;
+}
+
+int avr_compress_files(avr_ctx* c, int n_files, const uint8_t* const* in, const size_t* in_len, int model,
+                       uint8_t** out, size_t* out_len, int32_t* status) {
+  if (!c || n_files < 0 || (n_files && (!in || !in_len || !out || !out_len)) ||
+      (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL))
+    return AVR_ERR_INVALID_ARGUMENT;
+  for (int f = 0; f < n_files; f++)
+    if (!in[f]) return AVR_ERR_INVALID_ARGUMENT;
+  return compress_files(c, n_files, in, in_len, model, out, out_len, status);
 }
 
 int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
@@ -621,100 +877,17 @@ int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const in
 
 int avr_decompress_file(avr_ctx* c, const uint8_t* in, size_t n, uint8_t** out, size_t* out_len) {
   if (!c || !in || !out || !out_len) return AVR_ERR_INVALID_ARGUMENT;
-  HIP_TRY(c, hipSetDevice(c->device));
-  std::vector<avr::PbBlock> blocks;
-  std::string version;
-  if (!avr::pb_parse(in, n, &blocks, &version)) return fail(c, AVR_ERR_FORMAT, "not a Recoded protobuf");
-  const bool parallel = version == avr::kParallelModelTag;
-  // read_packet (recode.cpp:1359-1409): literals and surrogate blocks form the stream
-  std::vector<uint8_t> stream;
-  uint64_t seq = 1;
-  for (auto& b : blocks) {
-    if ((int)b.has_literal + (int)b.has_cabac + (int)b.has_skip != 1)
-      return fail(c, AVR_ERR_FORMAT, "Invalid input block: must have exactly one type");
-    if (b.has_literal) {
-      stream.insert(stream.end(), b.literal, b.literal + b.literal_len);
-    } else if (b.has_cabac) {
-      if (!b.has_size) return fail(c, AVR_ERR_FORMAT, "CABAC block requires size field.");
-      if (b.size < avr::kSurrogateMarkerBytes)
-        return fail(c, AVR_ERR_FORMAT, "Invalid coded block size for surrogate: " + std::to_string(b.size));
-      uint8_t mk[8];
-      avr::surrogate_marker(seq++, mk);
-      stream.insert(stream.end(), mk, mk + 8);
-      stream.insert(stream.end(), (size_t)b.size - 8, (uint8_t)'X');
-    } else if (!b.skip_coded) {
-      return fail(c, AVR_ERR_FORMAT, "Unknown input block type");
-    }
-  }
-  ParsedFile pf;
-  if (int r = parse_file(c, stream.data(), stream.size(), &pf)) return r;
-  // recognize_coded_block (recode.cpp:1546-1573): slices claim coded blocks in order
-  Plan plan;
-  std::vector<int> block_of_desc;
-  size_t next_coded = 0;
-  uint64_t seq_check = 1;
-  for (auto& s : pf.slices) {
-    while (next_coded < blocks.size() && !blocks[next_coded].has_cabac && !blocks[next_coded].has_skip) next_coded++;
-    if (next_coded >= blocks.size())
-      return fail(c, AVR_ERR_FORMAT, "Coded block expected, but not recorded in the compressed data.");
-    const avr::PbBlock& b = blocks[next_coded];
-    if ((size_t)b.size != s.size) return fail(c, AVR_ERR_FORMAT, "Invalid surrogate block size.");
-    avr_slice_desc d = desc_from_header(s);
-    if (b.has_cabac) {
-      uint8_t mk[8];
-      avr::surrogate_marker(seq_check++, mk);
-      if (memcmp(s.payload(), mk, 8) != 0) return fail(c, AVR_ERR_FORMAT, "Invalid surrogate marker in coded block.");
-      append_aligned(&plan.arena, b.cabac, b.cabac_len, 16, &d.payload_offset);
-      d.payload_size = (uint32_t)b.cabac_len;
-      d.read_limit = (uint32_t)b.cabac_len;
-      d.out_capacity = (uint32_t)(b.size + 64);
-    } else {
-      d.coded = 0;
-    }
-    plan.max_w = std::max(plan.max_w, d.mb_width);
-    if (parallel && !d.coded) {
-      next_coded++;
-      continue;
-    }
-    block_of_desc.push_back((int)next_coded);
-    plan.descs.push_back(d);
-    next_coded++;
-  }
-  std::vector<avr_slice_result> res;
-  std::vector<uint8_t> outb;
-  if (int r = run_plan(c, 1, !parallel, plan, &res, &outb)) return r;
-  std::vector<std::vector<uint8_t>> regen(blocks.size());
-  std::vector<char> done(blocks.size(), 0);
-  for (size_t k = 0; k < plan.descs.size(); k++) {
-    const int bi = block_of_desc[k];
-    if (!plan.descs[k].coded) continue;
-    if (res[k].status != 0)
-      return fail(c, AVR_ERR_FORMAT, "slice " + std::to_string(k) + " failed to decode (" + std::to_string(res[k].status) + ")");
-    const avr::PbBlock& b = blocks[bi];
-    std::vector<uint8_t> v(outb.begin() + plan.descs[k].out_offset,
-                           outb.begin() + plan.descs[k].out_offset + res[k].out_len);
-    // x264 padding correction (recode.cpp:1345-1356)
-    if (b.has_parity && b.has_last_byte && !b.last_byte.empty()) {
-      if ((int)b.length_parity != (int)(v.size() & 1)) v.push_back((uint8_t)b.last_byte[0]);
-      else if (!v.empty()) v.back() = (uint8_t)b.last_byte[0];
-    }
-    regen[bi] = std::move(v);
-    done[bi] = 1;
-  }
-  std::vector<uint8_t> o;
-  o.reserve(stream.size());
-  for (size_t i = 0; i < blocks.size(); i++) {
-    if (blocks[i].has_literal) o.insert(o.end(), blocks[i].literal, blocks[i].literal + blocks[i].literal_len);
-    else if (blocks[i].has_cabac) {
-      if (!done[i]) return fail(c, AVR_ERR_FORMAT, "Not all blocks were decoded.");
-      o.insert(o.end(), regen[i].begin(), regen[i].end());
-    }
-  }
-  *out = (uint8_t*)malloc(o.size() ? o.size() : 1);
-  if (!*out) return AVR_ERR_OUT_OF_MEMORY;
-  memcpy(*out, o.data(), o.size());
-  *out_len = o.size();
-  return AVR_OK;
+  int32_t st = 0;
+  const int r = decompress_files(c, 1, &in, &n, out, out_len, &st);
+  return r ? r : st;
+}
+
+int avr_decompress_files(avr_ctx* c, int n_files, const uint8_t* const* in, const size_t* in_len, uint8_t** out,
+                         size_t* out_len, int32_t* status) {
+  if (!c || n_files < 0 || (n_files && (!in || !in_len || !out || !out_len))) return AVR_ERR_INVALID_ARGUMENT;
+  for (int f = 0; f < n_files; f++)
+    if (!in[f]) return AVR_ERR_INVALID_ARGUMENT;
+  return decompress_files(c, n_files, in, in_len, out, out_len, status);
 }
 
 int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** compressed,
@@ -929,7 +1102,8 @@ int avr_container_describe(const uint8_t* in, size_t n, char** json, uint8_t** r
 
 int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t** out, size_t* out_len) {
   if (!c || !p || n <= 0 || !out || !out_len || p->mb_width <= 0 || p->mb_height <= 0 || p->slice_type < 0 ||
-      p->slice_type > 2 || p->chroma_format_idc < 1 || p->chroma_format_idc > 3 || p->gop_length < 0)
+      p->slice_type > 2 || p->chroma_format_idc < 1 || p->chroma_format_idc > 3 || p->gop_length < 0 ||
+      p->repeat < 0)
     return AVR_ERR_INVALID_ARGUMENT;
   HIP_TRY(c, hipSetDevice(c->device));
   Plan plan;
@@ -943,7 +1117,10 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
     first_of.push_back(first);
     avr_slice_desc d;
     memset(&d, 0, sizeof(d));
-    const int st = (p->gop_length > 0 && pic % p->gop_length == 0) ? 2 : p->slice_type;
+    // GOP: an IDR I picture every gop_length pictures; with slice_type B the pictures between
+    // follow B B P B B P ... (decode order), with P every picture between
+    const int g = p->gop_length > 0 ? pic % p->gop_length : -1;
+    const int st = g == 0 ? 2 : (g > 0 && p->slice_type == 1 && g % 3 == 0) ? 0 : p->slice_type;
     d.slice_type = st;
     d.slice_qp = p->slice_qp;
     d.cabac_init_idc = st == 2 ? -1 : 0;
@@ -970,11 +1147,17 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
   if (int r = run_plan(c, 2, false, plan, &res, &outb)) return r;
   std::vector<uint8_t> stream;
   avr::synth_write_parameter_sets(&stream, *p);
-  for (int i = 0; i < (int)plan.descs.size(); i++) {
+  for (int i = 0; i < (int)plan.descs.size(); i++)
     if (res[i].status != 0) return fail(c, AVR_ERR_DEVICE, "generator failed on slice " + std::to_string(i));
-    avr::synth_write_slice(&stream, *p, plan.descs[i].slice_type, pic_of[i], first_of[i],
-                           outb.data() + plan.descs[i].out_offset, res[i].out_len);
-  }
+  const int reps = std::max(1, p->repeat);
+  size_t bytes = 0;
+  for (int i = 0; i < (int)plan.descs.size(); i++) bytes += res[i].out_len + 64;
+  if ((uint64_t)bytes * reps > ((uint64_t)1 << 36)) return fail(c, AVR_ERR_INVALID_ARGUMENT, "stream too large");
+  stream.reserve(bytes * reps + 256);
+  for (int t = 0; t < reps; t++)
+    for (int i = 0; i < (int)plan.descs.size(); i++)
+      avr::synth_write_slice(&stream, *p, plan.descs[i].slice_type, t * n + pic_of[i], first_of[i],
+                             outb.data() + plan.descs[i].out_offset, res[i].out_len);
   *out = (uint8_t*)malloc(stream.size());
   if (!*out) return AVR_ERR_OUT_OF_MEMORY;
   memcpy(*out, stream.data(), stream.size());
@@ -985,7 +1168,7 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
 }  // extern "C"
 
 // Debug only (not part of include/avrecode.h): section cycle counters (32 slots) of an AVR_PROFILE build of
-// the parallel kernels (mode 0 compress, 1 decompress, 2 generate), read and cleared.
+// the slice kernels (mode 0 compress, 1 decompress, 2 generate, 3/4 sequential compress/decompress), read and cleared.
 // Diagnostic (AVR_PROFILE builds): 8 u32 per slice of the last parallel compress (mode 0) or
 // decompress (1) launch: HW_ID of waves 0-2, XCC_ID, walker start/end cycle counters.
 extern "C" int avr_debug_placement(int mode, uint32_t* out8n, int n) {
@@ -996,6 +1179,8 @@ extern "C" int avr_debug_placement(int mode, uint32_t* out8n, int n) {
 extern "C" int avr_debug_profile(int mode, unsigned long long* out16) {
   hipError_t e = mode == 0 ? avr::profile_parallel_compress(out16)
                : mode == 1 ? avr::profile_parallel_decompress(out16)
+               : mode == 3 ? avr::profile_sequential_compress(out16)
+               : mode == 4 ? avr::profile_sequential_decompress(out16)
                            : avr::profile_parallel_generate(out16);
   return e == hipSuccess ? AVR_OK : AVR_ERR_DEVICE;
 }

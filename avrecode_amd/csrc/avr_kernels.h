@@ -25,9 +25,18 @@ size_t shared_bytes(int max_mb_width);
 // does workgroup b of a 4G-workgroup launch land on CU group b mod G (schedule_kernel's assumption)?
 hipError_t probe_round_robin(size_t lds, bool* ok);
 // mode: 0 compress, 1 decompress, 2 generate, 3 trace (decode-only bin trace).  sequential = reference model (single wavefront).
+// Sequential (reference-model) launches walk n_files files at once, one workgroup each: file f is
+// the slices [file_first[f], file_first[f + 1]) (device array; nullptr = one file of all n slices)
+// with est + f kEstGlobal, frames + f frame_stride and frame_meta[f] of its own.
+struct SeqFiles {
+  const int* file_first = nullptr;
+  int n_files = 1;
+  uint64_t frame_stride = 0;
+};
 hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
                          int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                         uint8_t* frames, int* frame_meta, int* order, hipStream_t stream);
+                         uint8_t* frames, int* frame_meta, int* order, hipStream_t stream,
+                         const SeqFiles& files = SeqFiles());
 // one per kernel translation unit (avr_k_*.hip); lds = shared_bytes(max_mb_width)
 hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
@@ -43,18 +52,24 @@ hipError_t launch_parallel_trace(const EngineTables* T, const avr_slice_desc* de
                                  const int* order, hipStream_t stream);
 hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                      uint8_t* frames, int* frame_meta, hipStream_t stream);
+                                      uint8_t* frames, int* frame_meta, const int* file_first, int n_files,
+                                      uint64_t frame_stride, hipStream_t stream);
 hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                         const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                        uint8_t* frames, int* frame_meta, hipStream_t stream);
+                                        uint8_t* frames, int* frame_meta, const int* file_first, int n_files,
+                                      uint64_t frame_stride, hipStream_t stream);
 // reference-model compress in parallel (avr_k_rmode.hip): scan (count: ops == nullptr; write),
 // estimator chains over the op stream, per-slice coder
 hipError_t launch_rscan(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
                         uint8_t* frames, const int64_t* goff, uint32_t* counts, uint32_t* ops,
                         const uint64_t* op_off, avr_slice_result* res, int32_t* stop_ok, hipStream_t stream);
-size_t rmode_sort_temp_bytes(uint64_t N);
-hipError_t launch_rmode_estimators(const uint32_t* ops, uint64_t N, uint32_t* keys, uint32_t* vals, uint32_t* skeys,
-                                   uint32_t* svals, void* temp, size_t temp_bytes, uint32_t* rops, hipStream_t stream);
+// Several files in one pass (a corpus): file f's ops are [file_op_off[f], file_op_off[f + 1]) (device,
+// n_files + 1 entries; ignored for one file), each file with estimators of its own.
+size_t rmode_sort_temp_bytes(uint64_t N, int n_files);
+int rmode_max_files_per_pass();
+hipError_t launch_rmode_estimators(const uint32_t* ops, uint64_t N, const uint64_t* file_op_off, int n_files,
+                                   uint32_t* keys, uint32_t* vals, uint32_t* skeys, uint32_t* svals, void* temp,
+                                   size_t temp_bytes, uint32_t* rops, hipStream_t stream);
 hipError_t launch_rcode(const EngineTables* T, const avr_slice_desc* descs, int n, const uint32_t* rops,
                         const uint64_t* op_off, const uint32_t* counts, uint8_t* out, avr_slice_result* res,
                         const int32_t* stop_ok, hipStream_t stream);

@@ -1963,15 +1963,25 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
 }
 
-// Reference model: one workgroup (walker + coder wave) walks every slice in file order with
-// persistent estimators and frame metadata.
+// Reference model: one workgroup (walker + coder wave) walks every slice of a file in file order
+// with persistent estimators and frame metadata.  Several files at once: workgroup f walks file f,
+// the slices [file_first[f], file_first[f + 1]) (file_first == nullptr: one file, all n slices),
+// with its own estimator table (est_g + f kEstGlobal), frames (frames + f frame_stride) and
+// frame_meta[f] -- files share nothing, as separate runs of the reference would not.
 template <int MODE>
 __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                   const uint8_t* in, uint8_t* out,
                                                                   avr_slice_result* res, uint16_t* est_g,
-                                                                  uint8_t* frames, int* frame_meta) {
+                                                                  uint8_t* frames, int* frame_meta,
+                                                                  const int* file_first, uint64_t frame_stride) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int tid = threadIdx.x, nt = blockDim.x;
+  const int file = (int)blockIdx.x;
+  const int s_begin = file_first ? file_first[file] : 0;
+  const int s_end = file_first ? file_first[file + 1] : n;
+  est_g += (size_t)file * kEstGlobal;
+  frames += (size_t)file * frame_stride;
+  frame_meta += file;
   Walker<MODE, true> w;
   w.sh = (Shared*)smem;
   w.ring = (EdgeRec*)(smem + sizeof(Shared));
@@ -1994,7 +2004,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
   // frame_meta: [0] cur_frame.  Frame ids / sizes of the two frames, as scalars (no private arrays).
   int cur = 0, fid0 = 0, fid1 = 0, fw0 = 0, fw1 = 0, fh0 = 0, fh1 = 0;
   __syncthreads();
-  for (int s = 0; s < n; s++) {
+  for (int s = s_begin; s < s_end; s++) {
     const avr_slice_desc* d = &descs[s];
     const int W = d->mb_width, H = d->mb_height;
     // update_frame_spec (recode.cpp:824-843)

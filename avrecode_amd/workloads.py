@@ -1,0 +1,59 @@
+"""Synthetic workloads of BASELINE.json, made by the device generator
+(avr_synthesize_stream).  No GPU-independent data exists for them: the reference's own file
+(data/GOPR4542.MP4) is absent, so these seeded streams stand in, as SURVEY.md 8d specifies.
+
+  clip(ctx)        configs[1]: 1080p High 4:2:0, 64 frames x 1 slice, GOP I + 31 P (twice), QP 26
+  corpus(ctx)      configs[4]: mixed I/P/B GOPs, 1/2/4/8/17 slices per frame, 720p/1080p/4K, plus
+                   the two real fixtures (tests/fixtures)
+  stream_4k(ctx)   configs[3]: one 4K stream, 1 slice per frame, 1-s GOP (I + 29 P) tiled with
+                   rewritten frame numbers (avr_synthesize_stream's repeat)
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+from . import SynthParams
+
+ROOT = Path(__file__).resolve().parents[1]
+FIXTURES = ("realshort.mp4", "cockatoo.mp4")
+
+
+def clip(ctx, frames: int = 64, mb_width: int = 120, mb_height: int = 68, seed: int = 0) -> bytes:
+    return ctx.synthesize(SynthParams(mb_width=mb_width, mb_height=mb_height, slice_type=0, slice_qp=26,
+                                      chroma_format_idc=1, transform_8x8_mode=1, seed=seed, gop_length=32), frames)
+
+
+# (name, mb_width, mb_height, slices per frame, frames, gop, slice type between I pictures, QP, chroma)
+CORPUS = [
+    ("720p_IBBP_2spf", 80, 45, 2, 24, 12, 1, 24, 1),
+    ("720p_IP_1spf", 80, 45, 1, 32, 16, 0, 28, 1),
+    ("1080p_IBBP_4spf", 120, 68, 4, 16, 8, 1, 26, 1),
+    ("1080p_IP_17spf", 120, 68, 17, 8, 8, 0, 22, 1),
+    ("1080p_I_8spf_422", 120, 68, 8, 4, 1, 2, 30, 2),
+    ("4K_IP_8spf", 240, 135, 8, 6, 6, 0, 27, 1),
+    ("4K_IBBP_1spf_444", 240, 135, 1, 4, 4, 1, 30, 3),
+]
+
+
+def corpus(ctx, scale: float = 1.0, fixtures: bool = True) -> list[tuple[str, bytes]]:
+    """configs[4]: [(name, file bytes)].  scale < 1 shortens every stream (tests)."""
+    out = []
+    for k, (name, w, h, spf, frames, gop, st, qp, cf) in enumerate(CORPUS):
+        n = max(1, int(round(frames * scale)))
+        p = SynthParams(mb_width=w, mb_height=h, slice_type=st, slice_qp=qp, chroma_format_idc=cf,
+                        transform_8x8_mode=1, num_ref_idx_l0=2, num_ref_idx_l1=1, seed=4000 + k,
+                        slices_per_picture=spf, gop_length=gop)
+        out.append((name, ctx.synthesize(p, n)))
+    if fixtures:
+        for f in FIXTURES:
+            out.append((f, (ROOT / "tests" / "fixtures" / f).read_bytes()))
+    return out
+
+
+def stream_4k(ctx, seconds: int = 600, fps: int = 30, mb_width: int = 240, mb_height: int = 135,
+              seed: int = 0) -> bytes:
+    """configs[3]: `seconds` of 4K at `fps`, one slice per frame: one 1-s GOP (I + fps-1 P, QP 26)
+    generated once and tiled `seconds` times with rewritten frame_num / idr_pic_id."""
+    p = SynthParams(mb_width=mb_width, mb_height=mb_height, slice_type=0, slice_qp=26, chroma_format_idc=1,
+                    transform_8x8_mode=1, seed=seed, gop_length=fps, repeat=seconds)
+    return ctx.synthesize(p, fps)

@@ -9,6 +9,7 @@
  *   avr_compress_file    compressor(...).run()           recode.cpp:1102-1125, 1275-1297
  *   avr_decompress_file  decompressor(...).run()         recode.cpp:1312-1357, 1359-1409, 1527-1573
  *   avr_roundtrip_file   roundtrip(input, out)           recode.cpp:1594-1624
+ *   avr_compress_files / avr_decompress_files  the two runs above over a corpus of files at once
  *   avr_compress_slices  compressor::cabac_decoder x N    recode.cpp:1134-1268 (+ h264_model 615-1059,
  *                        (one CABAC slice per wavefront)  h264_symbol::execute 1061-1100,
  *                                                         arithmetic_code.h encoder 89-203)
@@ -64,6 +65,21 @@ void avr_free(void* p);
 int avr_compress_file(avr_ctx* ctx, const uint8_t* in, size_t n, int model, uint8_t** out, size_t* out_len);
 /* in: a Recoded protobuf.  *out: the original file bytes. */
 int avr_decompress_file(avr_ctx* ctx, const uint8_t* in, size_t n, uint8_t** out, size_t* out_len);
+
+/* Several files at once (a corpus): compressor::run / decompressor::run (recode.cpp:1102-1357) for
+ * each of in[0 .. n_files), with the device work of all files batched.  A file is the reference
+ * model's unit of sequential work (its estimators persist across ITS slices, recode.cpp:662-665, and
+ * nothing crosses files), so reference-model files run side by side: the compress side in one
+ * parallel pass over every slice of every file with per-file estimators, the decompress side one
+ * workgroup (wavefront) per file; parallel-model slices of all files run one wavefront each.
+ * out[f] / out_len[f]: file f's result (malloc'd, avr_free; NULL on failure).  status (optional,
+ * n_files entries) receives each file's status and the call returns AVR_OK unless the batch as a
+ * whole failed; without it the call returns the first file failure.  Output bytes equal
+ * avr_compress_file / avr_decompress_file on each file alone. */
+int avr_compress_files(avr_ctx* ctx, int n_files, const uint8_t* const* in, const size_t* in_len, int model,
+                       uint8_t** out, size_t* out_len, int32_t* status);
+int avr_decompress_files(avr_ctx* ctx, int n_files, const uint8_t* const* in, const size_t* in_len, uint8_t** out,
+                         size_t* out_len, int32_t* status);
 
 typedef struct {
   uint64_t file_bytes, slices, coded_slices, skipped_slices, payload_bytes, recoded_bytes, bins;
@@ -214,7 +230,12 @@ typedef struct {
   uint64_t seed;
   int32_t slices_per_picture;    /* 0 or 1: one slice per picture; k: k slices (equal MB runs) */
   int32_t gop_length;            /* 0: every picture has slice_type; g > 0: picture i is an IDR
-                                  * I picture when i % g == 0, else slice_type (e.g. I + 31 P) */
+                                  * I picture when i % g == 0, else slice_type (e.g. I + 31 P);
+                                  * with slice_type B: I B B P B B P ... (P when (i % g) % 3 == 0) */
+  int32_t repeat;                /* 0 or 1: once; r > 1: the n generated pictures are written r
+                                  * times, copy t with frame_num / idr_pic_id advanced by t n (a
+                                  * long stream tiled from one GOP; the payloads repeat) */
+  int32_t reserved;
 } avr_synth_params;
 /* Generate n pictures on the device (each slices_per_picture slices, in decode order) and return
  * them as one Annex-B stream (SPS/PPS + the slice NAL units) in host memory.  Pictures are
