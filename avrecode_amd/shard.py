@@ -34,50 +34,67 @@ def partition(sizes, world: int) -> list[tuple[int, int]]:
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
-def gather_blocks(local: list[bytes], status: list[int], dst: int = 0, device=None):
+def gather_flat(flat, status, offsets, lens, dst: int = 0, device=None):
     """Gather every rank's per-slice (status, bytes) to `dst`, in rank order.
 
-    Returns (status int32[n_total], blob bytes, offsets uint64, lens uint32) on dst, None elsewhere.
-    Sizes first (fixed-size all_gather of counts), then one send/recv of a flat byte tensor per
-    rank: RCCL has no gatherv."""
+    flat: this rank's outputs packed in one uint8 tensor (device tensor with RCCL), slice k's bytes
+    at flat[offsets[k] : offsets[k] + lens[k]].  Returns (status int32[n_total], blob bytes,
+    offsets uint64, lens uint32) on dst, None elsewhere.  Counts first (a fixed-size all_gather),
+    then one send/recv of the per-slice metadata and one of the flat bytes per rank: RCCL has no
+    gatherv, and the payload moves device to device over xGMI."""
     import torch
     import torch.distributed as dist
 
     rank, world = dist.get_rank(), dist.get_world_size()
-    dev = device if device is not None else torch.device("cpu")
-    lens = np.array([len(b) for b in local], dtype=np.int64)
-    hdr = torch.tensor([len(local), int(lens.sum())], dtype=torch.int64, device=dev)
+    dev = device if device is not None else flat.device
+    status = np.asarray(status, dtype=np.int64)
+    offsets = np.asarray(offsets, dtype=np.int64)
+    lens = np.asarray(lens, dtype=np.int64)
+    n = len(status)
+    nbytes = int((offsets + lens).max()) if n else 0
+    hdr = torch.tensor([n, nbytes], dtype=torch.int64, device=dev)
     allh = [torch.zeros_like(hdr) for _ in range(world)]
     dist.all_gather(allh, hdr)
     counts = [int(h[0]) for h in allh]
-    nbytes = [int(h[1]) for h in allh]
-    meta = torch.from_numpy(np.concatenate([np.asarray(status, dtype=np.int64), lens])).to(dev)
-    flat = torch.from_numpy(np.frombuffer(b"".join(local), dtype=np.uint8).copy()).to(dev)
+    sizes = [int(h[1]) for h in allh]
+    meta = torch.from_numpy(np.concatenate([status, offsets, lens])).to(dev)
+    body = flat[:nbytes].to(dev)
     if rank != dst:
         if counts[rank]:
             dist.send(meta, dst)
-        if nbytes[rank]:
-            dist.send(flat, dst)
+        if sizes[rank]:
+            dist.send(body, dst)
         return None
-    statuses, blobs, all_lens = [], [], []
+    st, offs, ln, blobs, base = [], [], [], [], 0
     for r in range(world):
         if r == rank:
-            m, f = meta, flat
+            m, f = meta, body
         else:
-            m = torch.empty(2 * counts[r], dtype=torch.int64, device=dev)
-            f = torch.empty(nbytes[r], dtype=torch.uint8, device=dev)
+            m = torch.empty(3 * counts[r], dtype=torch.int64, device=dev)
+            f = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
             if counts[r]:
                 dist.recv(m, r)
-            if nbytes[r]:
+            if sizes[r]:
                 dist.recv(f, r)
         m = m.cpu().numpy()
-        statuses.append(m[: counts[r]])
-        all_lens.append(m[counts[r]:])
+        c = counts[r]
+        st.append(m[:c])
+        offs.append(m[c:2 * c] + base)
+        ln.append(m[2 * c:])
         blobs.append(f.cpu().numpy().tobytes())
-    st = np.concatenate(statuses).astype(np.int32) if statuses else np.zeros(0, np.int32)
-    ln = np.concatenate(all_lens).astype(np.uint32) if all_lens else np.zeros(0, np.uint32)
-    offs = np.concatenate([[0], np.cumsum(ln, dtype=np.uint64)[:-1]]).astype(np.uint64) if len(ln) else ln.astype(np.uint64)
-    return st, b"".join(blobs), offs, ln
+        base += sizes[r]
+    cat = lambda xs, t: np.concatenate(xs).astype(t) if xs else np.zeros(0, t)  # noqa: E731
+    return cat(st, np.int32), b"".join(blobs), cat(offs, np.uint64), cat(ln, np.uint32)
+
+
+def gather_blocks(local: list[bytes], status: list[int], dst: int = 0, device=None):
+    """gather_flat for host byte strings (one per slice)."""
+    import torch
+    lens = np.array([len(b) for b in local], dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(lens) else lens
+    flat = torch.from_numpy(np.frombuffer(b"".join(local), dtype=np.uint8).copy())
+    dev = device if device is not None else torch.device("cpu")
+    return gather_flat(flat, status, offs, lens, dst=dst, device=dev)
 
 
 def subset(ps: ParsedStream, lo: int, hi: int) -> ParsedStream:
@@ -94,34 +111,42 @@ def subset(ps: ParsedStream, lo: int, hi: int) -> ParsedStream:
     return ParsedStream(d, ps.arena[a0:a1].copy(), w1 - w0, ps.max_mb_width, ps.max_mb_height)
 
 
-def sharded_compress(ctx, data: bytes, device=None) -> bytes | None:
+def sharded_compress(ctx, data: bytes, device=None, ps: ParsedStream | None = None) -> bytes | None:
     """PARALLEL-model compress of one file across all ranks; the container is returned on rank 0.
 
-    Byte-identical to ctx.compress(data, MODEL_PARALLEL) on one GPU."""
+    Every rank parses the file (host), takes its contiguous slice range (partition), runs it on its
+    GPU (compress + device roundtrip check: a slice is coded only if it regenerates its payload),
+    packs the re-coded bytes on the device and sends them to rank 0 (gather_flat over RCCL), which
+    assembles the Recoded container.  Byte-identical to ctx.compress(data, MODEL_PARALLEL)."""
     import torch
     import torch.distributed as dist
 
     from .batch import DeviceBatch
 
     rank, world = dist.get_rank(), dist.get_world_size()
-    ps = parse_stream(data)
+    ps = ps if ps is not None else parse_stream(data)
     lo, hi = partition(ps.descs["payload_size"], world)[rank]
     part = subset(ps, lo, hi)
-    blobs, status = [], []
-    if hi > lo:
-        b = DeviceBatch(ctx, part)
-        b.roundtrip(MODEL_PARALLEL)
-        torch.cuda.synchronize()
-        v = b.verdicts()
-        rec = b.recoded()
-        status = [0 if v[k] == 1 else -1 for k in range(hi - lo)]
-        blobs = [rec[k] if v[k] == 1 else b"" for k in range(hi - lo)]
     # RCCL ("nccl") moves device tensors only; gloo moves host tensors
     if dist.get_backend() == "nccl":
         dev = device if device is not None else torch.device("cuda", ctx.device)
     else:
         dev = torch.device("cpu")
-    g = gather_blocks(blobs, status, dst=0, device=dev)
+    if hi > lo:
+        b = DeviceBatch(ctx, part)
+        b.roundtrip(MODEL_PARALLEL)
+        flat, d_off = b.pack()
+        torch.cuda.synchronize()
+        v = b.verdicts()
+        res = b.results("c")
+        offs = d_off.cpu().numpy()[: hi - lo].astype(np.int64)
+        lens = np.where(res["status"] == 0, res["out_len"], 0).astype(np.int64)
+        status = np.where(v == 1, 0, -1).astype(np.int64)
+    else:
+        import torch as _t
+        flat = _t.zeros(16, dtype=_t.uint8, device=dev)
+        offs = lens = status = np.zeros(0, np.int64)
+    g = gather_flat(flat, status, offs, lens, dst=0, device=dev)
     if g is None:
         return None
     st, blob, offs, lens = g

@@ -80,10 +80,12 @@ def _cpu_slice_task(job):
 
 
 def cpu_baseline(ctx, args, n_bytes_hint):
-    """Oracle (CPU restatement of the reference, fresh model per slice) compress+decompress of the
-    first slices of the same batch: on one core (the reference's own thread_count = 1,
-    recode.cpp:122), and on all host threads, one slice per task (ctypes releases the GIL)."""
-    from concurrent.futures import ThreadPoolExecutor
+    """The oracle (CPU restatement of the reference) on a bounded sample of the same batch:
+    value = the reference's own configuration -- R-mode (one model for the whole file,
+    recode.cpp:662-665), one thread (recode.cpp:122) -- `recode_oracle roundtrip` of the first
+    slices of the batch written as one Annex-B file; all_cores = the parallel model on every host
+    thread, one slice per worker process."""
+    import tempfile
     sys.path.insert(0, str(ROOT / "tests"))
     import _oracle
     _oracle.build_oracle()
@@ -93,17 +95,22 @@ def cpu_baseline(ctx, args, n_bytes_hint):
     k = 1
     while True:
         sample = b"".join(ctx.synthesize(synth_params(qp, args.seed + j, args), k) for j, qp in enumerate(QPS))
-        t0 = time.perf_counter()
-        _, recs = _oracle.slices_p(sample, check_recodable=False)
-        dt = time.perf_counter() - t0
-        assert all(r["status_c"] == 0 and r["status_d"] == 0 for r in recs)
-        total_bytes, total_t, slices = len(sample), dt, len(recs)
+        with tempfile.NamedTemporaryFile(suffix=".264", delete=False) as fh:
+            fh.write(sample)
+        try:
+            t0 = time.perf_counter()
+            cpu = _oracle_roundtrip_s(fh.name)
+            dt = time.perf_counter() - t0
+        finally:
+            os.unlink(fh.name)
+        assert cpu, "oracle R-mode roundtrip failed on the sample"
+        total_bytes, total_t, slices = len(sample), sum(cpu), 3 * k
         if dt >= t_budget * 0.5 or k >= 64:
             break
         k = max(k + 1, min(64, int(k * t_budget / max(dt, 1e-3))))
     line = {"value": total_bytes / total_t / 1e6, "unit": "MB/s", "cores": 1, "kind": "port",
-            "sample": f"first {slices} slices of the batch ({k} per QP group, {total_bytes} input bytes), oracle "
-                      f"fresh-model compress+decompress, {total_t:.1f} s"}
+            "sample": f"first {slices} slices of the batch ({k} per QP group, {total_bytes} input bytes) as one file, "
+                      f"oracle R-mode (reference model) compress+decompress on one thread, {total_t:.1f} s"}
     # all host threads: the same per-slice work, one slice per task, in spawned worker processes
     # (the oracle allocates heavily, so threads in one process do not scale)
     nt = cpu_threads()
@@ -125,8 +132,8 @@ def cpu_baseline(ctx, args, n_bytes_hint):
             os.unlink(fh.name)
         assert all(ok for ok, _ in outs)
         line["all_cores"] = {"value": len(big) / dt / 1e6, "unit": "MB/s", "cores": nt,
-                             "sample": f"{n} slices ({len(big)} input bytes), one slice per task, {nt} worker "
-                                       f"processes, {dt:.1f} s"}
+                             "sample": f"{n} slices ({len(big)} input bytes), parallel model (fresh model per "
+                                       f"slice), one slice per task, {nt} worker processes, {dt:.1f} s"}
     return line
 
 
@@ -201,6 +208,144 @@ def file_roundtrips(ctx, args):
     return out
 
 
+def corpus_section(ctx, args):
+    """BASELINE configs[4]: a mixed I/P/B corpus (avrecode_amd/workloads.py: 720p/1080p/4K,
+    1/2/4/8/17 slices per frame, IBBP and IP GOPs, 4:2:0/4:2:2/4:4:4, plus the two fixtures) as ONE
+    batch through avr_compress_files + avr_decompress_files, both model modes, every file checked
+    byte-exact.  MB/s = corpus bytes / (compress + decompress wall time, median of reps);
+    compression ratio = container bytes / input bytes, P-mode against R-mode (the reference model).
+    CPU beside it: the oracle's R-mode roundtrip of every file, one core."""
+    import tempfile
+    import avrecode_amd as avr
+    from avrecode_amd import workloads
+    files = workloads.corpus(ctx, scale=args.corpus_scale)
+    datas = [d for _, d in files]
+    total = sum(map(len, datas))
+    rec = {"files": len(files), "bytes": total, "names": [n for n, _ in files]}
+    sizes = {}
+    for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+        outs = ctx.compress_files(datas, model)          # warm-up
+        walls, tc, td = [], [], []
+        for _ in range(args.file_reps):
+            t0 = time.perf_counter()
+            outs = ctx.compress_files(datas, model)
+            t1 = time.perf_counter()
+            back = ctx.decompress_files(outs)
+            t2 = time.perf_counter()
+            assert back == datas, f"corpus {tag}: decompress did not restore every file"
+            walls.append(t2 - t0)
+            tc.append(t1 - t0)
+            td.append(t2 - t1)
+        k = sorted(range(len(walls)), key=walls.__getitem__)[len(walls) // 2]
+        sizes[tag] = [len(o) for o in outs]
+        rec[tag] = {"MB_s": total / walls[k] / 1e6, "wall_s": walls[k], "compress_s": tc[k], "decompress_s": td[k],
+                    "avrc_bytes": sum(sizes[tag]), "ratio": sum(sizes[tag]) / total, "bit_exact": True}
+    rec["ratio_P_over_R"] = rec["P"]["avrc_bytes"] / rec["R"]["avrc_bytes"]
+    rec["per_file_ratio"] = {n: {"R": sizes["R"][i] / len(d), "P": sizes["P"][i] / len(d)}
+                             for i, (n, d) in enumerate(files)}
+    if not args.no_cpu_baseline:
+        tot = 0.0
+        for n, d in files:
+            with tempfile.NamedTemporaryFile(suffix=".264", delete=False) as fh:
+                fh.write(d)
+            try:
+                cpu = _oracle_roundtrip_s(fh.name)
+            finally:
+                os.unlink(fh.name)
+            if not cpu:
+                tot = None
+                break
+            tot += sum(cpu)
+        if tot:
+            rec["cpu_oracle_R_1core"] = {"MB_s": total / tot / 1e6, "wall_s": tot, "cores": 1, "kind": "port"}
+    return rec
+
+
+def main_stream_shard(args):
+    """BASELINE configs[3]: ONE 4K stream (1 slice per frame, a 1-s GOP I + 29 P tiled to
+    --stream-seconds with rewritten frame numbers) cut by NAL unit into contiguous slice ranges
+    balanced by bytes (shard.partition), one range per GPU.  Timed: every rank's device roundtrip
+    of its range (compress + decompress + verify), the device pack of its re-coded blocks, the RCCL
+    gather to rank 0 (shard.gather_flat) and rank 0's Recoded container assembly.  value = stream
+    bytes / max-over-ranks time (strong scaling: the stream is the same at every N)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import avrecode_amd as avr
+    from avrecode_amd import shard, workloads
+    from avrecode_amd.batch import DeviceBatch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if not dist.is_initialized():
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    ctx = avr.Context(local)
+    data = workloads.stream_4k(ctx, seconds=args.stream_seconds, fps=30, mb_width=args.stream_mb[0],
+                               mb_height=args.stream_mb[1])
+    ps = avr.parse_stream(data)
+    lo, hi = shard.partition(ps.descs["payload_size"], world)[rank]
+    part = shard.subset(ps, lo, hi)
+    batch = DeviceBatch(ctx, part)
+
+    def step():
+        batch.roundtrip(avr.MODEL_PARALLEL)
+        flat, d_off = batch.pack()
+        torch.cuda.synchronize()
+        v = batch.verdicts()
+        res = batch.results("c")
+        offs = d_off.cpu().numpy()[: hi - lo].astype(np.int64)
+        lens = np.where(res["status"] == 0, res["out_len"], 0).astype(np.int64)
+        st = np.where(v == 1, 0, -1).astype(np.int64)
+        g = shard.gather_flat(flat, st, offs, lens, dst=0, device=dev)
+        if g is None:
+            return None, bool((v == 1).all())
+        return avr.assemble_container(data, *g), bool((v == 1).all())
+
+    for _ in range(args.warmup):
+        step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ok = True
+    for _ in range(args.steps):
+        avrc, good = step()
+        ok = ok and good
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
+    dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+    if rank == 0:
+        # the container must decompress to the stream (checked outside the timed region)
+        exact = bool(t[1] == 0) and ctx.decompress(avrc) == data
+        line = {
+            "metric": METRIC, "value": len(data) * args.steps / float(t[0]) / 1e6, "unit": "MB/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": float(t[0]) / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (device generator, seeded; one GOP tiled)",
+            "bit_exact": exact,
+            "config": {"workload": "one 4K stream sharded by NAL unit, RCCL gather reassembly (BASELINE configs[3])",
+                       "seconds": args.stream_seconds, "fps": 30, "mb": list(args.stream_mb), "slices": len(ps.descs),
+                       "stream_bytes": len(data), "container_bytes": len(avrc), "model": "parallel",
+                       "parallelism": f"slice ranges over {world} GPU(s)"},
+            "roofline": None, "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    ctx.close()
+
+
 def load_traffic(args, kernel):
     p = ROOT / "profiles" / f"{args.round}_pmc.json"
     if not p.exists():
@@ -229,7 +374,15 @@ def main():
     ap.add_argument("--file-reps", type=int, default=3)
     ap.add_argument("--no-files", action="store_true", help="skip the whole-file roundtrips")
     ap.add_argument("--no-clip", action="store_true", help="skip the configs[1] clip in the file roundtrips")
+    ap.add_argument("--no-corpus", action="store_true", help="skip the configs[4] corpus")
+    ap.add_argument("--corpus-scale", type=float, default=1.0)
+    ap.add_argument("--stream-shard", action="store_true",
+                    help="configs[3]: one 4K stream sharded over the GPUs with the RCCL gather (strong scaling)")
+    ap.add_argument("--stream-seconds", type=int, default=600)
+    ap.add_argument("--stream-mb", type=int, nargs=2, default=(240, 135))
     args = ap.parse_args()
+    if args.stream_shard:
+        return main_stream_shard(args)
 
     import numpy as np
     import torch
@@ -340,6 +493,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(ctx, args, len(data))
         if world == 1 and not args.no_files:
             line["file_roundtrip"] = file_roundtrips(ctx, args)
+        if world == 1 and not args.no_corpus:
+            line["corpus"] = corpus_section(ctx, args)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
