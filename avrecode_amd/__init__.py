@@ -58,8 +58,12 @@ SLICE_DESC = np.dtype([
     ("chroma_array_type", "<i4"), ("transform_8x8_mode", "<i4"), ("direct_8x8_inference", "<i4"),
     ("x264_build", "<i4"), ("picture_id", "<i4"), ("coded", "<i4"),
 ], align=True)
-SLICE_RESULT = np.dtype([("out_len", "<u4"), ("status", "<i4"), ("bins", "<u4"), ("mbs", "<u4")], align=True)
-assert SLICE_DESC.itemsize == 88 and SLICE_RESULT.itemsize == 16
+SLICE_RESULT = np.dtype([("out_len", "<u4"), ("status", "<i4"), ("bins", "<u4"), ("mbs", "<u4"),
+                         ("bill", "<u4", (6,))], align=True)
+# avr_pip_coding_type (CodingType, recode.cpp:616): the index of avr_file_stats.bill / cabac_bill
+CODING_TYPES = ("PIP_UNKNOWN", "PIP_UNREACHABLE", "PIP_SIGNIFICANCE_MAP", "PIP_SIGNIFICANCE_EOB",
+                "PIP_SIGNIFICANCE_NZ", "PIP_RESIDUALS")
+assert SLICE_DESC.itemsize == 88 and SLICE_RESULT.itemsize == 40
 
 
 class AvrError(RuntimeError):
@@ -71,7 +75,8 @@ class AvrError(RuntimeError):
 class _FileStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("file_bytes", "slices", "coded_slices", "skipped_slices", "payload_bytes", "recoded_bytes", "bins")] + \
-               [("compress_s", ctypes.c_double), ("decompress_s", ctypes.c_double)]
+               [("compress_s", ctypes.c_double), ("decompress_s", ctypes.c_double),
+                ("bill", ctypes.c_uint64 * 6), ("cabac_bill", ctypes.c_uint64 * 6)]
 
 
 class _SynthParams(ctypes.Structure):
@@ -276,6 +281,8 @@ class Context:
         self._check(lib().avr_roundtrip_file(self._h, p, n, model, ctypes.byref(out), ctypes.byref(olen),
                                              ctypes.byref(st)), "roundtrip")
         stats = {f: getattr(st, f) for f, _ in _FileStats._fields_}
+        for f in ("bill", "cabac_bill"):   # by CodingType name, nonzero entries (~h264_model's print)
+            stats[f] = {CODING_TYPES[i]: int(v) for i, v in enumerate(stats[f]) if v}
         return _take(out, olen.value), stats
 
     def _files(self, fn, datas, *extra):

@@ -6,7 +6,7 @@ HBM layout of a batch (DESIGN.md "Data layout"):
   d_work    re-coded output: slice k at desc[k].out_offset, desc[k].out_capacity bytes reserved
   d_regen   regenerated CABAC bytes, laid out like d_in
   d_desc / d_dec_desc   avr_slice_desc[n] (88 B each) for compress / derived decompress
-  d_res_c / d_res_d     avr_slice_result[n] (16 B each); d_verdict int32[n]
+  d_res_c / d_res_d     avr_slice_result[n] (40 B each); d_verdict int32[n]
 torch only allocates and owns these buffers and supplies the stream; all compute is in
 libavrecode.so.
 """

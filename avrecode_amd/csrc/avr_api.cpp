@@ -10,6 +10,7 @@
 // AVR_ERR_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -241,7 +242,7 @@ constexpr int kRModeFallback = 1;
 // Frame metadata generations mirror update_frame_spec (recode.cpp:824-843) as
 // slices_sequential_kernel implements it; a stream whose frame size changes with a stale other
 // frame is left to the sequential kernel (kRModeFallback), as is a plan too large for one pass.
-int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total) {
+int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flags) {
   const int n = (int)plan.descs.size();
   const int nf = plan.n_files();
   if (nf > avr::rmode_max_files_per_pass()) return kRModeFallback;
@@ -326,7 +327,7 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total) {
                                           tb, rops, c->stream));
   HIP_TRY(c, avr::launch_rcode(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, rops,
                                c->rm_off.as<uint64_t>(), c->rm_counts.as<uint32_t>(), c->out.as<uint8_t>(),
-                               c->res.as<avr_slice_result>(), c->rm_stop.as<int32_t>(), c->stream));
+                               c->res.as<avr_slice_result>(), c->rm_stop.as<int32_t>(), flags, c->stream));
   (void)out_total;
   return AVR_OK;
 }
@@ -338,9 +339,9 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total) {
 // cannot be decompressed.
 constexpr int32_t kStatusNoRoundtrip = -20;
 int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_slice_result>* res,
-             std::vector<uint8_t>* out_host, bool verify = false) {
+             std::vector<uint8_t>* out_host, bool verify = false, uint32_t flags = 0) {
   const int n = (int)plan.descs.size();
-  res->assign(n, avr_slice_result{0, 0, 0, 0});
+  res->assign(n, avr_slice_result{0, 0, 0, 0, {0, 0, 0, 0, 0, 0}});
   uint64_t out_total = 0;
   for (auto& d : plan.descs) {
     d.out_offset = out_total;
@@ -357,7 +358,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
                             c->stream));
   int rm = kRModeFallback;
   if (sequential && mode == 0 && !getenv("AVR_RMODE_SEQUENTIAL")) {
-    rm = run_rmode_compress(c, plan, out_total);
+    rm = run_rmode_compress(c, plan, out_total, flags);
     if (rm < 0) return rm;
   }
   if (sequential && rm == AVR_OK) {
@@ -382,7 +383,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
     HIP_TRY(c, avr::launch_slices(mode, true, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n,
                                   plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(), c->res.as<avr_slice_result>(),
                                   c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), nullptr,
-                                  c->stream, sf));
+                                  c->stream, sf, flags));
   } else {
     const int chunk = std::min(n, kMaxSlicesPerLaunch);
     HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk, true));
@@ -392,7 +393,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
       HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>() + s0,
                                     m, plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(),
                                     c->res.as<avr_slice_result>() + s0, c->est.as<uint16_t>(), nullptr, nullptr,
-                                    c->order_or_null(), c->stream));
+                                    c->order_or_null(), c->stream, avr::SeqFiles(), flags));
     }
   }
   std::vector<int32_t> verdict;
@@ -515,8 +516,14 @@ int emit_container(const uint8_t* in, size_t n, const ParsedFile& pf, const std:
 // device roundtrip), and the reference model runs all files in one pass (the parallel R-mode
 // pipeline over all their slices with per-file estimators, or one workgroup per file).  out[f] is
 // malloc'd; status[f] (optional) is file f's result; the return value is the first failure.
+typedef std::array<uint64_t, 6> Bill;   // h264_model::bill / cabac_bill by avr_pip_coding_type
+void add_bill(Bill* b, const avr_slice_result& r) {
+  for (int i = 0; i < 6; i++) (*b)[i] += r.bill[i];
+}
+
 int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* in_len, int model, uint8_t** out,
-                   size_t* out_len, int32_t* status) {
+                   size_t* out_len, int32_t* status, std::vector<Bill>* bills = nullptr) {
+  if (bills) bills->assign(nf, Bill{});
   HIP_TRY(c, hipSetDevice(c->device));
   std::vector<int32_t> st(nf, AVR_OK);
   std::vector<ParsedFile> pf(nf);
@@ -547,7 +554,9 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   }
   std::vector<avr_slice_result> res;
   std::vector<uint8_t> outb;
-  if (int r = run_plan(c, 0, false, plan, &res, &outb, /*verify=*/true)) return r;
+  if (int r = run_plan(c, 0, false, plan, &res, &outb, /*verify=*/true,
+                       bills && model == AVR_MODEL_PARALLEL ? avr::kFlagBill : 0))
+    return r;
   // 2) segmentation (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297)
   std::vector<std::vector<char>> ok(nf);
   std::vector<std::vector<const uint8_t*>> found(nf);
@@ -568,6 +577,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
       std::vector<std::pair<int, int>> idx;   // (file, slice) per desc
       for (int f = 0; f < nf; f++) {
         if (!todo[f]) continue;
+        if (bills) (*bills)[f] = Bill{};   // this pass re-codes the whole file
         rp.file_first.push_back((int)rp.descs.size());
         for (size_t i = 0; i < pf[f].slices.size(); i++) {
           const avr::SliceInfo& s = pf[f].slices[i];
@@ -588,7 +598,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
       rp.file_first.push_back((int)rp.descs.size());
       std::vector<avr_slice_result> rr;
       std::vector<uint8_t> ro;
-      if (int r = run_plan(c, 0, true, rp, &rr, &ro)) return r;
+      if (int r = run_plan(c, 0, true, rp, &rr, &ro, false, bills ? avr::kFlagBill : 0)) return r;
       std::fill(todo.begin(), todo.end(), 0);
       for (size_t k = 0; k < idx.size(); k++) {
         const int f = idx[k].first, i = idx[k].second;
@@ -600,6 +610,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
         }
         recoded[f][i].assign(ro.begin() + rp.descs[k].out_offset,
                              ro.begin() + rp.descs[k].out_offset + rr[k].out_len);
+        if (bills) add_bill(&(*bills)[f], rr[k]);
       }
       bool again = false;
       for (int f = 0; f < nf; f++) {
@@ -622,6 +633,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
           const int k = cand_of[f][i];
           recoded[f][i].assign(outb.begin() + plan.descs[k].out_offset,
                                outb.begin() + plan.descs[k].out_offset + res[k].out_len);
+          if (bills) add_bill(&(*bills)[f], res[k]);
         }
   }
   // 4) containers (compressor::run, recode.cpp:1115-1125)
@@ -720,8 +732,10 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
 }
 
 int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* in_len, uint8_t** out,
-                     size_t* out_len, int32_t* status) {
+                     size_t* out_len, int32_t* status, std::vector<Bill>* bills = nullptr) {
   HIP_TRY(c, hipSetDevice(c->device));
+  if (bills) bills->assign(nf, Bill{});
+  const uint32_t flags = bills ? avr::kFlagBill : 0;
   std::vector<int32_t> st(nf, AVR_OK);
   std::vector<DecJob> jobs(nf);
   Plan pp, rp;   // parallel-model slices; reference-model files (one workgroup each)
@@ -743,10 +757,10 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
   std::vector<avr_slice_result> pres, rres;
   std::vector<uint8_t> pout, rout;
   if (!pp.descs.empty())
-    if (int r = run_plan(c, 1, false, pp, &pres, &pout)) return r;
+    if (int r = run_plan(c, 1, false, pp, &pres, &pout, false, flags)) return r;
   if (!rp.file_first.empty()) {
     rp.file_first.push_back((int)rp.descs.size());
-    if (int r = run_plan(c, 1, true, rp, &rres, &rout)) return r;
+    if (int r = run_plan(c, 1, true, rp, &rres, &rout, false, flags)) return r;
   }
   int first_err = AVR_OK;
   for (int f = 0; f < nf; f++) {
@@ -777,6 +791,7 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
         const size_t o0 = o.size();
         o.insert(o.end(), outb.begin() + plan.descs[k].out_offset,
                  outb.begin() + plan.descs[k].out_offset + res[k].out_len);
+        if (bills) add_bill(&(*bills)[f], res[k]);
         // x264 padding correction (recode.cpp:1345-1356)
         if (b.has_parity && b.has_last_byte && !b.last_byte.empty()) {
           const size_t len = o.size() - o0;
@@ -893,12 +908,18 @@ int avr_decompress_files(avr_ctx* c, int n_files, const uint8_t* const* in, cons
 int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** compressed,
                        size_t* compressed_len, avr_file_stats* stats) {
   if (!c || !in) return AVR_ERR_INVALID_ARGUMENT;
+  if (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL) return AVR_ERR_INVALID_ARGUMENT;
   uint8_t *comp = nullptr, *dec = nullptr;
   size_t cn = 0, dn = 0;
+  std::vector<Bill> cbill, dbill;
+  int32_t st = 0;
   const double t0 = now_s();
-  if (int r = avr_compress_file(c, in, n, model, &comp, &cn)) return r;
+  if (int r = compress_files(c, 1, &in, &n, model, &comp, &cn, &st, &cbill)) return r;
+  if (st) return st;
   const double t1 = now_s();
-  int r = avr_decompress_file(c, comp, cn, &dec, &dn);
+  const uint8_t* cp = comp;
+  int r = decompress_files(c, 1, &cp, &cn, &dec, &dn, &st, &dbill);
+  if (!r) r = st;
   const double t2 = now_s();
   if (r) {
     free(comp);
@@ -911,6 +932,10 @@ int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8
     stats->file_bytes = n;
     stats->compress_s = t1 - t0;
     stats->decompress_s = t2 - t1;
+    for (int i = 0; i < 6; i++) {
+      stats->bill[i] = cbill[0][i];
+      stats->cabac_bill[i] = dbill[0][i];
+    }
     std::vector<avr::PbBlock> blocks;
     std::string v;
     if (avr::pb_parse(comp, cn, &blocks, &v)) {

@@ -424,6 +424,78 @@ __device__ __forceinline__ void re_put(RecodedEncoder& e, OutStream& o, int bin,
     } while (hi32(e.range) < (1u << 23) && e.range != 0);  // until range >= 2^55
   }
 }
+// Billing (h264_model::billable_bytes, recode.cpp:656-658, 1074-1078): encoder::put returns the
+// bytes its renormalisation emitted (arithmetic_code.h:106-126, 147-190), and the reference emits a
+// digit only once its top digit cannot change (deferring it, and every digit after it, while
+// low and low + range - 1 disagree on it), so its count per put differs from the bytes this
+// encoder's cache scheme writes at that put.  re_put_billed runs re_put and returns the
+// reference's count: at each renormalisation step the reference's low is this low without the
+// carry bit (bit 63), its range is this range; *pend counts the reference's deferred digits.
+__device__ __forceinline__ uint32_t re_put_billed(RecodedEncoder& e, OutStream& o, int bin, uint64_t r1,
+                                                  uint32_t* pend) {
+  const uint64_t r0 = e.range - r1;
+  e.low += bin ? r0 : 0;
+  e.range = bin ? r1 : r0;
+  uint32_t bytes = 0;
+  if (hi32(e.range) < (1u << 19)) {
+    if (e.range == 0) e.err = 1;
+    #pragma clang loop unroll(disable)
+    do {
+      const uint64_t lo = e.low & ((1ull << 63) - 1);
+      const bool deferred = ((lo >> 55) & 0xff) != (((lo + e.range - 1) >> 55) & 0xff);
+      bytes += deferred ? 0u : *pend + 1;
+      *pend = deferred ? *pend + 1 : 0u;
+      re_shift(e, o);
+      e.range <<= 8;
+    } while (hi32(e.range) < (1u << 23) && e.range != 0);
+  }
+  return bytes;
+}
+
+// The generic coder behind cabac_code.h (arithmetic_code<uint32_t, uint16_t, 0x200>: fixed_one
+// 2^31, 16-bit digits of 2 bytes, min_range 0x200, renormalised while range < 2^15), tracked only
+// for its billing (h264_model::billable_cabac_bytes, recode.cpp:659-661, 1443-1468): the CABAC
+// encoder above writes the same bytes, but at other moments.
+struct CabacBill {
+  uint32_t low, range, pend;
+};
+__device__ __forceinline__ void cb_init(CabacBill& b) {
+  b.low = 0;
+  b.range = (0x80000000u / 0x200u) * 0x1FEu;   // cabac_code.h:30
+  b.pend = 0;
+}
+// encoder::put(symbol, range_of_1): the bytes it reports
+__device__ __forceinline__ uint32_t cb_put(CabacBill& b, int sym, uint32_t r1) {
+  const uint32_t r0 = b.range - r1;
+  b.low += sym ? r0 : 0u;
+  b.range = sym ? r1 : r0;
+  uint32_t bytes = 0;
+  if (b.range < 0x200u) {
+    #pragma clang loop unroll(disable)
+    while (b.range < 0x8000u && b.range != 0) {
+      if (b.low >= 0x80000000u) b.low -= 0x80000000u;   // carry into the deferred digits
+      const uint32_t d = b.low >> 15, dhi = ((b.low + b.range - 1) >> 15) & 0xffffu;
+      bytes += d != dhi ? 0u : 2u * (b.pend + 1);
+      b.pend = d != dhi ? b.pend + 1 : 0u;
+      b.low = (b.low - (d << 15)) << 16;
+      b.range <<= 16;
+    }
+  }
+  return bytes;
+}
+// normalize = log2(range / 0x100) (cabac_code.h:39, 70-79): range >> normalize is 9 bits
+__device__ __forceinline__ uint32_t cb_norm(uint32_t range) { return 23u - (uint32_t)__clz(range); }
+// cabac::encoder::put (cabac_code.h:33-49): state s before the bin
+__device__ __forceinline__ uint32_t cb_decision(CabacBill& b, int bin, uint32_t s, CabacRec r) {
+  const uint32_t nrm = cb_norm(b.range);
+  const uint32_t lps = cabac_lps(b.range >> nrm, r) << nrm;
+  return cb_put(b, ((uint32_t)bin ^ s) & 1u, lps);
+}
+__device__ __forceinline__ uint32_t cb_bypass(CabacBill& b, int bin) { return cb_put(b, bin, b.range >> 1); }
+__device__ __forceinline__ uint32_t cb_terminate(CabacBill& b, int bin) {
+  return cb_put(b, bin, 2u << cb_norm(b.range));
+}
+
 __device__ __forceinline__ void re_finish(RecodedEncoder& e, OutStream& o) {  // arith:128-144
   #pragma clang loop unroll(disable)
   for (uint64_t sb = 1ull << 62; sb; sb >>= 1) {

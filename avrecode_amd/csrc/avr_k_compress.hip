@@ -4,11 +4,11 @@
 namespace avr {
 
 hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
-                    uint8_t* out, avr_slice_result* res, uint16_t* est, const int* order, hipStream_t stream) {
+                    uint8_t* out, avr_slice_result* res, uint16_t* est, const int* order, uint32_t flags, hipStream_t stream) {
   // the per-CU priority board of this kernel starts empty on every launch (cu_cell's slot counter
   // must not carry a previous launch's residue)
   if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
-  hipLaunchKernelGGL(slices_parallel_kernel<MODE_COMPRESS>, dim3(n), dim3(slice_threads<MODE_COMPRESS>()), lds, stream, T, descs, n, in, out, res, est, order);
+  hipLaunchKernelGGL(slices_parallel_kernel<MODE_COMPRESS>, dim3(n), dim3(slice_threads<MODE_COMPRESS>()), lds, stream, T, descs, n, in, out, res, est, order, flags);
   return hipGetLastError();
 }
 

@@ -5,9 +5,10 @@ namespace avr {
 
 hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
                     uint8_t* out, avr_slice_result* res, uint16_t* est, uint8_t* frames, int* frame_meta,
-                    const int* file_first, int n_files, uint64_t frame_stride, hipStream_t stream) {
+                    const int* file_first, int n_files, uint64_t frame_stride, uint32_t flags,
+                    hipStream_t stream) {
   hipLaunchKernelGGL(slices_sequential_kernel<MODE_COMPRESS>, dim3(n_files), dim3(slice_threads<MODE_COMPRESS>()), lds, stream, T, descs, n, in, out, res, est,
-                     frames, frame_meta, file_first, frame_stride);
+                     frames, frame_meta, file_first, frame_stride, flags);
   return hipGetLastError();
 }
 

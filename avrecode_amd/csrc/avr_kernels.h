@@ -21,6 +21,7 @@ constexpr uint32_t kEstLogOverflow = 0xffffffffu;
 constexpr int kEstGlobal = kEstLog + 2 * kEstLogCap;
 static_assert(kEstGlobal % 8 == 0 && kEstTable % 8 == 0, "16-byte clears");
 
+constexpr uint32_t kFlagBill = 1;   // launch flag: the coders bill per CodingType (avr_slice_result.bill)
 size_t shared_bytes(int max_mb_width);
 // does workgroup b of a 4G-workgroup launch land on CU group b mod G (schedule_kernel's assumption)?
 hipError_t probe_round_robin(size_t lds, bool* ok);
@@ -33,31 +34,32 @@ struct SeqFiles {
   int n_files = 1;
   uint64_t frame_stride = 0;
 };
+// flags: kFlagBill (1) = the coders bill per CodingType into avr_slice_result.bill
 hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
                          int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                          uint8_t* frames, int* frame_meta, int* order, hipStream_t stream,
-                         const SeqFiles& files = SeqFiles());
+                         const SeqFiles& files = SeqFiles(), uint32_t flags = 0);
 // one per kernel translation unit (avr_k_*.hip); lds = shared_bytes(max_mb_width)
 hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                    const int* order, hipStream_t stream);
+                                    const int* order, uint32_t flags, hipStream_t stream);
 hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                      const int* order, hipStream_t stream);
+                                      const int* order, uint32_t flags, hipStream_t stream);
 hipError_t launch_parallel_generate(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                    const int* order, hipStream_t stream);
+                                    const int* order, uint32_t flags, hipStream_t stream);
 hipError_t launch_parallel_trace(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                  const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                 const int* order, hipStream_t stream);
+                                 const int* order, uint32_t flags, hipStream_t stream);
 hipError_t launch_sequential_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                       uint8_t* frames, int* frame_meta, const int* file_first, int n_files,
-                                      uint64_t frame_stride, hipStream_t stream);
+                                      uint64_t frame_stride, uint32_t flags, hipStream_t stream);
 hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                         const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                         uint8_t* frames, int* frame_meta, const int* file_first, int n_files,
-                                      uint64_t frame_stride, hipStream_t stream);
+                                      uint64_t frame_stride, uint32_t flags, hipStream_t stream);
 // reference-model compress in parallel (avr_k_rmode.hip): scan (count: ops == nullptr; write),
 // estimator chains over the op stream, per-slice coder
 hipError_t launch_rscan(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
@@ -72,7 +74,7 @@ hipError_t launch_rmode_estimators(const uint32_t* ops, uint64_t N, const uint64
                                    size_t temp_bytes, uint32_t* rops, hipStream_t stream);
 hipError_t launch_rcode(const EngineTables* T, const avr_slice_desc* descs, int n, const uint32_t* rops,
                         const uint64_t* op_off, const uint32_t* counts, uint8_t* out, avr_slice_result* res,
-                        const int32_t* stop_ok, hipStream_t stream);
+                        const int32_t* stop_ok, uint32_t flags, hipStream_t stream);
 // section cycle counters of AVR_PROFILE builds (avr_walker.h); zeros otherwise
 hipError_t profile_parallel_compress(unsigned long long* out16);
 hipError_t placement_parallel_compress(uint32_t* out8n, int n);

@@ -141,6 +141,7 @@ struct Shared {
   uint32_t elog_n;           // entries appended to the HBM table's write log by this model
   uint32_t prio;             // the slice's current wave priority (walker -> modeler / coder)
   uint32_t c_len, c_last;
+  uint32_t bill[6];          // the coder's h264_model billing by CodingType (kFlagBill launches)
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
   uint8_t state[1024];
   uint16_t est[kEstDefault + 2];
@@ -170,7 +171,14 @@ struct Shared {
 //   before its update.
 // ring 0, decompress: bit 0 bin, bits 1-2 kind (0 decision, 1 bypass, 2 terminate), bits 3-12
 //   ctxIdx.
+// Billing classes (h264_model::coding_type at the put, recode.cpp:615-661): compress coder ops
+//   carry it in bits 15-16 (0 UNKNOWN, 1 SIGNIFICANCE_MAP, 2 SIGNIFICANCE_NZ), decompress walker
+//   ops in bits 13-14 (0 UNKNOWN, 1 SIGNIFICANCE_MAP, 2 SIGNIFICANCE_EOB).
 // OP_FINISH = arithmetic_code::encoder::finish (terminate = 1); OP_END closes a slice's stream.
+enum { PIPC_UNKNOWN = 0, PIPC_UNREACHABLE, PIPC_SIG_MAP, PIPC_SIG_EOB, PIPC_SIG_NZ, PIPC_RESIDUALS };
+constexpr uint32_t OPC_SHIFT_C = 15, OPC_SHIFT_D = 13;
+__host__ __device__ inline int op_class_pip_c(uint32_t c) { return c == 1 ? PIPC_SIG_MAP : c == 2 ? PIPC_SIG_NZ : PIPC_UNKNOWN; }
+__host__ __device__ inline int op_class_pip_d(uint32_t c) { return c == 1 ? PIPC_SIG_MAP : c == 2 ? PIPC_SIG_EOB : PIPC_UNKNOWN; }
 constexpr uint32_t OP_FINISH = 1u << 30;
 constexpr uint32_t OP_END = 1u << 31;
 enum { OPK_DECISION = 0, OPK_BYPASS = 1, OPK_TERMINATE = 2 };
@@ -931,12 +939,12 @@ struct Walker {
         int b = rd_get(rd, in, p1(e));
         est_store(sh, est_g, idx, slot, est_update(e, b, 0x50));
         bins++;
-        push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3);
+        push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3 | 1u << OPC_SHIFT_D);
         if (b) {
           cnt++;
           int last = nnz_m == cnt;   // derived EOB (recode.cpp:1437-1438)
           bins++;
-          push((uint32_t)last | OPK_DECISION << 1 | (uint32_t)(lb + lc) << 3);
+          push((uint32_t)last | OPK_DECISION << 1 | (uint32_t)(lb + lc) << 3 | 2u << OPC_SHIFT_D);
           if (last) break;
         }
       }
@@ -1697,6 +1705,10 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
     // ---- 2. the recurrences, key by key, ops in order
     const uint32_t key_v = (op_v >> 1) & 0xfffffdu;            // cache bit + index (bin, threshold excluded)
     const uint64_t bins_m = __ballot(op_v & 1), thr_m = __ballot(op_v & OPM_THR50);
+    // billing class of op j: significance map (threshold 0x50), nnz bits (the other SIG/NZ
+    // estimators), or anything else
+    const uint64_t nz_m = __ballot(cache && !(op_v & OPM_THR50));
+    auto cls_of = [&](uint32_t j) -> uint32_t { return ((thr_m >> j) & 1) ? 1u : ((nz_m >> j) & 1) ? 2u : 0u; };
     uint32_t out_v = op_v;                                     // control ops pass through
     uint32_t fin_v = 0;
     uint64_t last_m = 0;
@@ -1710,7 +1722,7 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
       uint32_t j = l;
       for (;;) {
         const uint32_t b = (uint32_t)(bins_m >> j) & 1u;
-        out_v = writelane(out_v, j, op_recode((int)b, e));
+        out_v = writelane(out_v, j, op_recode((int)b, e) | cls_of(j) << OPC_SHIFT_C);
         e = est_update(e, (int)b, ((thr_m >> j) & 1) ? 0x50u : 0x60u);
         m &= m - 1;
         if (!m) break;
@@ -1774,7 +1786,12 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
 // decompress retires ring 0 (cabac::encoder::put / put_bypass / put_terminate,
 // recode.cpp:1443-1474, cabac_code.h:33-67).
 template <int MODE>
-AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out) {
+AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out, uint32_t flags) {
+  const bool billing = (flags & kFlagBill) != 0;
+  uint32_t bill[6] = {0, 0, 0, 0, 0, 0};
+  uint32_t bill_pend = 0;
+  CabacBill cbill;
+  cb_init(cbill);
   OutStream o;
   o.g = out + d->out_offset;
   o.cap = d->out_capacity;
@@ -1817,12 +1834,24 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
       uint64_t ctrl = __ballot(__lane_id() < n && (op_v & (OP_END | OP_FINISH)));
       for (uint32_t j = 0;;) {
         const uint32_t stop = ctrl ? (uint32_t)__builtin_ctzll(ctrl) : n;
-        for (; j < stop; j++) {
-          const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
-          const uint64_t m = readlane64(m_v, j);
-          const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
-          const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
-          re_put(re, o, op & 1, p1);
+        if (billing) {
+          for (; j < stop; j++) {
+            const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
+            const uint64_t m = readlane64(m_v, j);
+            const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
+            const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
+            const uint32_t bytes = re_put_billed(re, o, op & 1, p1, &bill_pend);
+            const int c = op_class_pip_c((op >> OPC_SHIFT_C) & 3);
+            if (bytes) bill[c] += bytes;
+          }
+        } else {
+          for (; j < stop; j++) {
+            const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
+            const uint64_t m = readlane64(m_v, j);
+            const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
+            const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
+            re_put(re, o, op & 1, p1);
+          }
         }
         if (j >= n) break;
         const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
@@ -1833,7 +1862,28 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
       }
       asm volatile("; MARK_CODER_END");
     } else {
-      for (uint32_t j = 0; j < n; j++) {
+      if (billing) {   // the generic coder's emission counts beside the re-encode, op by op
+        for (uint32_t j = 0; j < n; j++) {
+          const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
+          if (op & OP_END) { done = true; break; }
+          const int b = op & 1;
+          const uint32_t kind = (op >> 1) & 3;
+          uint32_t bytes;
+          if (kind == OPK_DECISION) {
+            uint8_t* stp = &sh->state[(op >> 3) & 1023];
+            const uint32_t st = *stp;
+            bytes = cb_decision(cbill, b, st, vtab_rec(vt, st));
+            ce_decision_v(ce, o, b, stp, vt);
+          } else if (kind == OPK_BYPASS) {
+            bytes = cb_bypass(cbill, b);
+            ce_bypass(ce, o, b);
+          } else {
+            bytes = cb_terminate(cbill, b);
+            ce_terminate(ce, o, b);
+          }
+          if (bytes) bill[op_class_pip_d((op >> OPC_SHIFT_D) & 3)] += bytes;
+        }
+      } else for (uint32_t j = 0; j < n; j++) {
         const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
         if (op & OP_END) { done = true; break; }
         const int b = op & 1;
@@ -1860,6 +1910,7 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
     sh->c_err = MODE == MODE_COMPRESS ? re.err : ce.err;
     sh->c_len = out_total(o);
     sh->c_last = o.last;
+    for (int i = 0; i < 6; i++) sh->bill[i] = bill[i];
   }
 }
 
@@ -1874,6 +1925,7 @@ AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_re
   if (MODE == MODE_DECOMPRESS && !status && len && sh->c_last == 0x80) len--;  // recode.cpp:1503-1505
   res->out_len = len;
   res->status = status;
+  for (int i = 0; i < 6; i++) res->bill[i] = sh->bill[i];
 }
 
 // Single-wave slice (the generator: CABAC encode inline, no coder wave).
@@ -1893,6 +1945,7 @@ AVR_FI void run_slice_inline(Walker<MODE, RM>& w, const avr_slice_desc* d, const
     res->status = status;
     res->bins = w.bins;
     res->mbs = (uint32_t)w.mbs_done;
+    for (int i = 0; i < 6; i++) res->bill[i] = 0;
   }
 }
 
@@ -1913,7 +1966,8 @@ constexpr int slice_threads() {
 template <int MODE>
 __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                 const uint8_t* in, uint8_t* out, avr_slice_result* res,
-                                                                uint16_t* est_scratch, const int* order) {
+                                                                uint16_t* est_scratch, const int* order,
+                                                                uint32_t flags) {
   extern __shared__ __align__(16) uint8_t smem[];
   if ((int)blockIdx.x >= n) return;
   const int s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
@@ -1937,6 +1991,7 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
       res[s].status = 1;
       res[s].bins = 0;
       res[s].mbs = 0;
+      for (int i = 0; i < 6; i++) res[s].bill[i] = 0;
     }
     return;
   }
@@ -1958,7 +2013,7 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
     AVR_PLACE_T(s, 1);
   }
   else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
-  else coder_slice<MODE>(w.sh, w.T, d, out);
+  else coder_slice<MODE>(w.sh, w.T, d, out, flags);
   __syncthreads();
   if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
 }
@@ -1973,7 +2028,8 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
                                                                   const uint8_t* in, uint8_t* out,
                                                                   avr_slice_result* res, uint16_t* est_g,
                                                                   uint8_t* frames, int* frame_meta,
-                                                                  const int* file_first, uint64_t frame_stride) {
+                                                                  const int* file_first, uint64_t frame_stride,
+                                                                  uint32_t flags) {
   extern __shared__ __align__(16) uint8_t smem[];
   const int tid = threadIdx.x, nt = blockDim.x;
   const int file = (int)blockIdx.x;
@@ -2032,6 +2088,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
         res[s].status = 1;
         res[s].bins = 0;
         res[s].mbs = 0;
+      for (int i = 0; i < 6; i++) res[s].bill[i] = 0;
       }
       continue;
     }
@@ -2046,7 +2103,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
     const int wave = tid >> 6;
     if (wave == 0) walker_slice(w, d, in, &res[s]);
     else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
-    else coder_slice<MODE>(w.sh, w.T, d, out);
+    else coder_slice<MODE>(w.sh, w.T, d, out, flags);
     __syncthreads();
     if (tid == 0) finish_slice<MODE>(w.sh, d, &res[s]);
     __syncthreads();

@@ -18,6 +18,20 @@ static bool read_file(const char* p, std::vector<uint8_t>* v) {
   return true;
 }
 
+// ~h264_model (recode.cpp:634-655): the bills to stderr, nonzero entries by CodingType name -- the
+// compressor's (re-coded bytes) and the decompressor's (CABAC bytes), summed over the file.
+static const char* const kBillingNames[6] = {"PIP_UNKNOWN", "PIP_UNREACHABLE", "PIP_SIGNIFICANCE_MAP",
+                                             "PIP_SIGNIFICANCE_EOB", "PIP_SIGNIFICANCE_NZ", "PIP_RESIDUALS"};
+static void print_bill(const char* title, const uint64_t* b) {
+  bool first = true;
+  for (int i = 0; i < 6; i++) {
+    if (!b[i]) continue;
+    if (first) std::cerr << title << "\n=============\n";
+    first = false;
+    std::cerr << kBillingNames[i] << " : " << b[i] << "\n";
+  }
+}
+
 int main(int argc, char** argv) {
   if (argc < 3) {
     std::cerr << "Usage: " << argv[0] << " [compress|decompress|roundtrip] [-p] <input> [output]" << std::endl;
@@ -55,6 +69,8 @@ int main(int argc, char** argv) {
       std::cout << " slices " << st.slices << " coded " << st.coded_slices << " skipped " << st.skipped_slices
                 << " payload " << st.payload_bytes << " recoded " << st.recoded_bytes << std::endl;
       std::cout << " compress " << st.compress_s << "s decompress " << st.decompress_s << "s" << std::endl;
+      print_bill("Avrecode Bill", st.bill);
+      print_bill("CABAC Bill", st.cabac_bill);
     } else {
       std::cerr << "Compress-decompress roundtrip failed: " << avr_last_error(ctx) << std::endl;
       avr_destroy(ctx);

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define AVRECODE_ABI_VERSION 1
+#define AVRECODE_ABI_VERSION 2
 
 typedef enum {
   AVR_OK = 0,
@@ -84,6 +84,11 @@ int avr_decompress_files(avr_ctx* ctx, int n_files, const uint8_t* const* in, co
 typedef struct {
   uint64_t file_bytes, slices, coded_slices, skipped_slices, payload_bytes, recoded_bytes, bins;
   double compress_s, decompress_s;  /* wall time of the two halves (host + device) */
+  /* h264_model::bill / cabac_bill (recode.cpp:615-661), indexed by avr_pip_coding_type: bytes the
+   * re-coded encoder emitted per put during compress (recode.cpp:1074-1078, 1213-1220) and bytes
+   * the CABAC encoder emitted per put during decompress (1443-1446, 1455-1457, 1466-1468), summed
+   * over the file's coded slices (the parallel model's per-slice models included). */
+  uint64_t bill[6], cabac_bill[6];
 } avr_file_stats;
 /* compress, decompress, compare (recode.cpp:1594-1624).  Returns AVR_ERR_ROUNDTRIP on mismatch. */
 int avr_roundtrip_file(avr_ctx* ctx, const uint8_t* in, size_t n, int model, uint8_t** compressed,
@@ -111,6 +116,10 @@ typedef struct {
   int32_t status;            /* 0 ok, <0 parse/overflow error (slice must be stored skip_coded) */
   uint32_t bins;             /* CABAC bins processed */
   uint32_t mbs;              /* macroblocks parsed */
+  /* h264_model billing of this slice by avr_pip_coding_type (recode.cpp:615-661), filled only
+   * by the whole-file calls (zero from the batch entry points): compress = re-coded bytes emitted
+   * per put (h264_model::bill), decompress = CABAC bytes emitted per put (cabac_bill). */
+  uint32_t bill[6];
 } avr_slice_result;
 
 /* All pointers are device pointers; stream is a hipStream_t (NULL = default stream).

@@ -225,6 +225,12 @@ typedef struct {
   size_t file_bytes, slices, coded_slices, skipped_slices, payload_bytes, recoded_bytes, bins;
 } avr_stats_t;
 extern avr_stats_t avr_last_stats;
+/* h264_model::bill / cabac_bill (recode.cpp:615-661) of the last avr_compress / avr_decompress,
+ * summed over its model(s), indexed by avr_coding_type: bytes the re-coded encoder emitted per
+ * put (compress, recode.cpp:1074-1078, 1213-1220) and bytes the CABAC encoder emitted per put
+ * (decompress, 1443-1446, 1455-1457, 1466-1468). */
+extern size_t avr_last_bill[8], avr_last_cabac_bill[8];
+void avr_model_bills(const avr_model_t *m, size_t bill[8], size_t cabac_bill[8]);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Slice-level API used by the tests to cross-check the GPU kernels slice by slice.          */

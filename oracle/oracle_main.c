@@ -95,6 +95,25 @@ static int cmd_slices(const uint8_t *file, size_t n) {
   return bad != 0;
 }
 
+/* ~h264_model (recode.cpp:634-655): the bills to stderr, nonzero entries only, by CodingType
+ * name; once for the compressor's model(s) (re-coded bytes), once for the decompressor's (CABAC
+ * bytes), summed over the fresh per-slice models in the parallel mode. */
+static const char *const billing_names[6] = {"PIP_UNKNOWN", "PIP_UNREACHABLE", "PIP_SIGNIFICANCE_MAP",
+                                            "PIP_SIGNIFICANCE_EOB", "PIP_SIGNIFICANCE_NZ", "PIP_RESIDUALS"};
+static void print_bill(const char *title, const size_t *b) {
+  int first = 1;
+  for (int i = 0; i < 6; i++) {
+    if (!b[i]) continue;
+    if (first) fprintf(stderr, "%s\n=============\n", title);
+    first = 0;
+    fprintf(stderr, "%s : %ld\n", billing_names[i], (long)b[i]);
+  }
+}
+static void print_bills(const size_t *bill, const size_t *cabac_bill) {
+  print_bill("Avrecode Bill", bill);
+  print_bill("CABAC Bill", cabac_bill);
+}
+
 int main(int argc, char **argv) {
   int mode = AVR_MODE_R;
   int a = 1;
@@ -129,6 +148,8 @@ int main(int argc, char **argv) {
     if (avr_compress(file, n, mode, &c, &cn)) { fprintf(stderr, "compress failed\n"); return 1; }
     double t1 = now_s();
     avr_stats_t st = avr_last_stats;
+    size_t bill[8];
+    memcpy(bill, avr_last_bill, sizeof(bill));
     int r = avr_decompress(c, cn, &d, &dn);
     double t2 = now_s();
     if (r || dn != n || memcmp(d, file, n)) {
@@ -146,6 +167,7 @@ int main(int argc, char **argv) {
     printf(" slices %zu coded %zu skipped %zu payload %zu recoded %zu bins %zu\n", st.slices, st.coded_slices,
            st.skipped_slices, st.payload_bytes, st.recoded_bytes, st.bins);
     printf(" compress %.3fs decompress %.3fs (%.2f MB/s roundtrip)\n", t1 - t0, t2 - t1, n / 1e6 / (t2 - t0));
+    print_bills(bill, avr_last_cabac_bill);
     return 0;
   }
   fprintf(stderr, "Unknown command: %s\n", cmd);

@@ -107,6 +107,13 @@ avr_model_t *avr_model_new(void) {
   m->used = (uint8_t *)calloc(m->cap, 1);
   return m;
 }
+void avr_model_bills(const avr_model_t *m, size_t bill[8], size_t cabac_bill[8]) {
+  for (int i = 0; i < 8; i++) {
+    bill[i] += m->bill[i];
+    cabac_bill[i] += m->cabac_bill[i];
+  }
+}
+
 void avr_model_free(avr_model_t *m) {
   if (!m) return;
   for (int i = 0; i < 2; i++) { free(m->frames[i].meta); free(m->frames[i].image); }

@@ -26,6 +26,7 @@
 #include "oracle_model.h"
 
 avr_stats_t avr_last_stats;
+size_t avr_last_bill[8], avr_last_cabac_bill[8];
 static const int SURROGATE_MARKER_BYTES = 8; /* recode.cpp:27 */
 #define AVR_P_MODE_TAG "avrecode-amd:P"
 
@@ -598,6 +599,7 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
   }
   size_t prev_end = 0;
   memset(&avr_last_stats, 0, sizeof(avr_last_stats));
+  memset(avr_last_bill, 0, sizeof(avr_last_bill));
   avr_last_stats.file_bytes = n;
   for (int i = 0; i < nn; i++) {
     slice_t s;
@@ -618,7 +620,11 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
       obuf_t rc;
       size_t bins = 0;
       int r = compress_slice_with_model(m, &s, &rc, &bins);
-      if (mode != AVR_MODE_R) avr_model_free(m);
+      if (mode != AVR_MODE_R) {
+        size_t unused[8] = {0};
+        avr_model_bills(m, avr_last_bill, unused);
+        avr_model_free(m);
+      }
       if (r != 0) abort(); /* pre-check passed, so the walk must succeed */
       avr_pb_block_t b = {0};
       b.has_size = 1;
@@ -653,6 +659,10 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
   lit.literal = file + prev_end;
   lit.literal_len = n - prev_end;
   avr_pb_put_block(&o, &lit);
+  if (model) {
+    size_t unused[8] = {0};
+    avr_model_bills(model, avr_last_bill, unused);
+  }
   avr_model_free(model);
   free(st);
   free(nals);
@@ -704,6 +714,8 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
   st->x264_build = -1;
   avr_model_t *model = avr_model_new();
   int mode_r = avr_pb_mode(in, n) == AVR_MODE_R;
+  size_t unused_bill[8] = {0};
+  memset(avr_last_cabac_bill, 0, sizeof(avr_last_cabac_bill));
   int next_coded = 0;
   obuf_t *regen = (obuf_t *)calloc((size_t)nb, sizeof(obuf_t));
   for (int i = 0; i < nn && ret == 0; i++) {
@@ -719,7 +731,10 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
       if (!mode_r) m = fresh = avr_model_new();
       obuf_t cab;
       int r = decompress_slice_with_model(m, &s.h, s.picture_id, b->cabac, b->cabac_len, &cab);
-      if (fresh) avr_model_free(fresh);
+      if (fresh) {
+        avr_model_bills(fresh, unused_bill, avr_last_cabac_bill);
+        avr_model_free(fresh);
+      }
       if (r != 0) { ret = -8; ob_free(&cab); free(s.rbsp); break; }
       if (b->has_parity && b->has_last_byte && b->last_byte_len) {
         size_t sz = cab.len;
@@ -744,6 +759,7 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
   }
   for (int i = 0; i < nb; i++) ob_free(&regen[i]);
   free(regen);
+  if (mode_r) avr_model_bills(model, unused_bill, avr_last_cabac_bill);
   avr_model_free(model);
   free(st);
   free(nals);

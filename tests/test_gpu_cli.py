@@ -90,3 +90,39 @@ def test_sharded_compress_world1_rccl():
                 assert hashlib.sha256(got).hexdigest() == GOLD[(name, "P")]["avrc_sha256"]
     finally:
         dist.destroy_process_group()
+
+
+def _bills(stderr: str) -> dict:
+    """The "Avrecode Bill" / "CABAC Bill" sections of ~h264_model's stderr print (recode.cpp:634-655)."""
+    out, cur = {}, None
+    for line in stderr.splitlines():
+        if line in ("Avrecode Bill", "CABAC Bill"):
+            cur = out.setdefault(line, {})
+        elif " : " in line and cur is not None:
+            k, v = line.split(" : ")
+            cur[k.strip()] = int(v)
+    return out
+
+
+@pytest.mark.parametrize("name,mode", CASES)
+def test_cli_billing_matches_oracle(name, mode):
+    """h264_model::bill (re-coded bytes per put by CodingType, compress) and cabac_bill (CABAC bytes
+    per put, decompress) -- recode.cpp:615-661, 1074-1078, 1213-1220, 1443-1468 -- equal the oracle's."""
+    from _oracle import build_oracle
+    _, oracle = build_oracle()
+    args = ["roundtrip"] + (["-p"] if mode == "P" else []) + [str(FIX / name)]
+    r = _run(args)
+    assert r.returncode == 0, r.stderr.decode()
+    o = subprocess.run([str(oracle)] + args, capture_output=True, timeout=300)
+    assert o.returncode == 0
+    got, want = _bills(r.stderr.decode()), _bills(o.stderr.decode())
+    assert want["Avrecode Bill"] and want["CABAC Bill"]
+    assert got == want
+    # the bills account for every re-coded byte but the finish() flushes (one per coded slice at most
+    # a handful of bytes), and for every regenerated CABAC byte likewise
+    data = (FIX / name).read_bytes()
+    import avrecode_amd as avr
+    with avr.Context(0) as ctx:
+        _, st = ctx.roundtrip(data, avr.MODEL_REFERENCE if mode == "R" else avr.MODEL_PARALLEL)
+    assert st["bill"] == want["Avrecode Bill"] and st["cabac_bill"] == want["CABAC Bill"]
+    assert 0 <= st["recoded_bytes"] - sum(st["bill"].values()) <= 16 * st["coded_slices"]
