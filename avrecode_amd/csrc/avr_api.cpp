@@ -532,13 +532,16 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
     out_len[f] = 0;
     st[f] = parse_file(c, in[f], in_len[f], &pf[f]);
   }
-  // 1) every candidate slice of every file through the parallel kernel: per-slice parse, restore
-  //    check and device roundtrip (and the parallel model's output)
+  // 1) parallel model: every candidate slice of every file through the parallel kernel -- per-slice
+  //    parse, restore check, device roundtrip and the model's output.  Reference model: nothing
+  //    here; the reference-model pass below parses and checks every candidate itself (its statuses
+  //    carry the same parse / restore verdict) and demotes the failures, so a well-formed file
+  //    costs one reference-model pass, not a parallel-model pass before it.
   Plan plan;
   std::vector<std::vector<int>> cand_of(nf);
   for (int f = 0; f < nf; f++) {
     cand_of[f].assign(pf[f].slices.size(), -1);
-    if (st[f]) continue;
+    if (st[f] || model == AVR_MODEL_REFERENCE) continue;
     for (size_t i = 0; i < pf[f].slices.size(); i++) {
       const avr::SliceInfo& s = pf[f].slices[i];
       if (!recodable_candidate(s)) continue;
@@ -562,7 +565,9 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   std::vector<std::vector<const uint8_t*>> found(nf);
   for (int f = 0; f < nf; f++) {
     ok[f].assign(pf[f].slices.size(), 0);
-    for (size_t i = 0; i < pf[f].slices.size(); i++) ok[f][i] = cand_of[f][i] >= 0 && res[cand_of[f][i]].status == 0;
+    for (size_t i = 0; i < pf[f].slices.size(); i++)
+      ok[f][i] = model == AVR_MODEL_REFERENCE ? st[f] == AVR_OK && recodable_candidate(pf[f].slices[i])
+                                              : cand_of[f][i] >= 0 && res[cand_of[f][i]].status == 0;
     found[f] = segment(in[f], in_len[f], pf[f], ok[f]);
   }
   // 3) reference model: the coded slices of every file in file order, estimators per file; a
