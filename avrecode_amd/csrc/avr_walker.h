@@ -35,7 +35,14 @@
 #define PROF_BEGINW(v) const uint64_t v = PROF_T(); const uint32_t v##_b = w.bins
 #define PROF_END(i, v) prof[i] += PROF_T() - (v), profb[i] += bins - v##_b
 #define PROF_ENDW(i, v) w.prof[i] += PROF_T() - (v), w.profb[i] += w.bins - v##_b
+// macroblock-layer sub-sections (avr_prof[32 + i] cycles, [40 + i] bins): 0 macroblock start,
+// 1 mb_skip_flag, 2 mb_type + sub_mb_type, 3 intra prediction modes, 4 ref_idx, 5 mvd,
+// 6 coded_block_pattern + transform_size_8x8_flag + mb_qp_delta, 7 end_of_slice + publish
+#define SPROF_END(i, v) sprof[i] += PROF_T() - (v), sprofb[i] += bins - v##_b
+#define SPROF_ENDW(i, v) w.sprof[i] += PROF_T() - (v), w.sprofb[i] += w.bins - v##_b
 #else
+#define SPROF_END(i, v)
+#define SPROF_ENDW(i, v)
 #define PROF_BEGINW(v)
 #define PROF_ENDW(i, v)
 #define PROF_BEGIN(v)
@@ -45,7 +52,7 @@
 namespace avr {
 
 #ifdef AVR_PROFILE
-static __device__ unsigned long long avr_prof[32];
+static __device__ unsigned long long avr_prof[64];
 // wave placement per slice (AVR_PROFILE builds): HW_ID of waves 0..2, XCC_ID, walker start / end
 // (s_memtime low 32 bits), walker start / end (s_memrealtime, 100 MHz) -- scripts/placement.py
 constexpr int kPlaceSlices = 4096;
@@ -96,17 +103,19 @@ struct MbRec {
   uint8_t direct8[4];
   uint8_t mnnz[52];     // model BlockMeta.num_nonzeros[51]
 };
-struct EdgeRec {        // bottom edge of the macroblock above
+// bottom edge of the macroblock above, dword j gathered from MbRec dword Walker::edge_src (lane j)
+// at the publish; 92 B keeps four 1080p workgroups within a CU's LDS
+struct EdgeRec {
   uint8_t flags, pad;
   uint16_t cbp;
-  uint8_t nnz[3][4];
-  uint8_t mvd[2][4][2];
-  int8_t ref[2][2];
-  uint8_t direct8[2];
+  uint8_t nnz[3][4];    // bottom row of each plane
+  uint8_t mvd[2][4][2]; // bottom row
+  int8_t ref[2][2];     // bottom two 8x8 of each list
+  uint8_t direct8[2], pad2[2];
   uint8_t mnnz[52];
-  uint8_t pad2[2];
 };
 static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
+static_assert(sizeof(MbRec) == 180, "MbRec layout (dword map in Walker::edge_src)");
 
 // LDS layout (per workgroup = one slice); the ring is sized by mb_width at launch.
 // SIG + NZ estimators: an LDS hash table (4096 slots, 16 KB) in front of the dense per-model
@@ -478,6 +487,13 @@ struct Walker {
   // slice state
   int W, H, mb_x, mb_y, slice_type, is_b, cat_, t8mode;
   int left_ok, top_ok, last_dqp_nz;
+  // flags (bits 0-6, F_*) and coded_block_pattern (bits 16-31) of the current macroblock and of
+  // its left / upper neighbours, in one scalar register each for the whole macroblock (the
+  // neighbours' read once at its start): context selection reads no LDS for them.  Bit 7 of cf:
+  // the current macroblock has an 8x8 residual block (finished_queueing's is_8x8).
+  uint32_t cf, lf, tf;
+  static constexpr uint32_t CF_8X8 = 0x80;
+  uint32_t edge_src;      // lane j < 23: the MbRec dword that becomes EdgeRec dword j (set per slice)
   int err, finished;
   uint32_t bins;
   int target_mbs, mbs_done, last_mb;
@@ -612,8 +628,8 @@ struct Walker {
     ring0.push_v(op_v, n);
   }
 #ifdef AVR_PROFILE
-  uint64_t prof[8];
-  uint32_t profb[8];
+  uint64_t prof[8], sprof[8];
+  uint32_t profb[8], sprofb[8];
 #endif
 
   // ------------------------------------------------------------------ bins through the model
@@ -745,29 +761,29 @@ struct Walker {
   // ------------------------------------------------------------------ neighbours (parser)
   AVR_FI const EdgeRec& top() const { return ring[mb_x]; }
   AVR_FI uint16_t nb_cbp_left() const {
-    return left_ok ? sh->left.cbp : ((sh->cur.flags & F_INTRA) ? 0x7CF : 0x00F);
+    return left_ok ? (lf >> 16) : ((cf & F_INTRA) ? 0x7CF : 0x00F);
   }
   AVR_FI uint16_t nb_cbp_top() const {
-    return top_ok ? ring[mb_x].cbp : ((sh->cur.flags & F_INTRA) ? 0x7CF : 0x00F);
+    return top_ok ? (tf >> 16) : ((cf & F_INTRA) ? 0x7CF : 0x00F);
   }
   // FFmpeg 4:4:4 8x8 coded_block_flag quirk for x264 < r151 (see oracle_walker.c)
-  AVR_FI int nnz_override(uint8_t nbflags, int* v) const {
-    if (cat_ != 3 || !(sh->cur.flags & F_T8) || (nbflags & F_T8)) return 0;
-    *v = (uint32_t)x264_build < 151u ? ((sh->cur.flags & F_INTRA) ? 64 : 0) : 0;
+  AVR_FI int nnz_override(uint32_t nbflags, int* v) const {
+    if (cat_ != 3 || !(cf & F_T8) || (nbflags & F_T8)) return 0;
+    *v = (uint32_t)x264_build < 151u ? ((cf & F_INTRA) ? 64 : 0) : 0;
     return 1;
   }
   AVR_FI int nnz_left(int p, int pw, int x4, int y4) const {
     if (x4 > 0) return sh->cur.nnz[p][y4 * 4 + x4 - 1];
-    if (!left_ok) return (sh->cur.flags & F_INTRA) ? 64 : 0;
+    if (!left_ok) return (cf & F_INTRA) ? 64 : 0;
     int v;
-    if (nnz_override(sh->left.flags, &v)) return v;
+    if (nnz_override(lf, &v)) return v;
     return sh->left.nnz[p][y4 * 4 + pw - 1];
   }
   AVR_FI int nnz_top(int p, int x4, int y4) const {
     if (y4 > 0) return sh->cur.nnz[p][(y4 - 1) * 4 + x4];
-    if (!top_ok) return (sh->cur.flags & F_INTRA) ? 64 : 0;
+    if (!top_ok) return (cf & F_INTRA) ? 64 : 0;
     int v;
-    if (nnz_override(ring[mb_x].flags, &v)) return v;
+    if (nnz_override(tf, &v)) return v;
     return ring[mb_x].nnz[p][x4];
   }
 
@@ -805,7 +821,7 @@ struct Walker {
       if (has_above) av = (U & 128) ? mnnz_top(ui) : sh->cur.mnnz[ui];
     }
     const int pv = mnnz_prev(n);
-    const int t = ((sh->cur.is8x8 | (max > 32)) ? 1 : 0) + 2 * is_dc + c422 + 4 * cat;
+    const int t = (((cf & CF_8X8) || max > 32) ? 1 : 0) + 2 * is_dc + c422 + 4 * cat;
     if (MODE == MODE_COMPRESS) {
       // all bits at once, bit i in lane i (so_far = the count's bits below i)
       const int i = (int)__lane_id();
@@ -1021,10 +1037,10 @@ struct Walker {
       }
       PROF_END(6, t6);
       cur.mnnz[n] = (uint8_t)cnt;             // end_coding_type recount (recode.cpp:935-947)
-      if (max > 32) cur.is8x8 = 1;
+      if (max > 32) cf |= CF_8X8;
     }
     if (is_dc) {
-      if (cnt) cur.cbp |= (uint16_t)(cat == 3 ? (0x40 << (n - 49)) : (0x100 << (n - 48)));
+      if (cnt) cf |= (uint32_t)(cat == 3 ? (0x40 << (n - 49)) : (0x100 << (n - 48))) << 16;
     } else if (max == 64) {
       cur.nnz[p][y4 * 4 + x4] = cur.nnz[p][y4 * 4 + x4 + 1] = (uint8_t)cnt;
       cur.nnz[p][y4 * 4 + 4 + x4] = cur.nnz[p][y4 * 4 + 4 + x4 + 1] = (uint8_t)cnt;
@@ -1064,7 +1080,7 @@ struct Walker {
     }
     for (int i8 = 0; i8 < 4; i8++) {
       if (!(cbp & (1 << i8))) continue;
-      if (sh->cur.flags & F_T8) {
+      if (cf & F_T8) {
         blk_pos(16 * p + 4 * i8, &x4, &y4);
         nb = push_block(nb, cat_8, 16 * p + 4 * i8, 64, 0, 0, p, 4, x4, y4);
       } else {
@@ -1107,27 +1123,26 @@ struct Walker {
 
   // ------------------------------------------------------------------ prediction syntax
   AVR_FI int ref_gt0(int list, int x4, int y4, int use_left) const {
-    uint8_t fl, dir;
+    uint8_t dir;
     int r;
     if (use_left) {
       if (x4 > 0) {
         int b8 = (y4 >> 1) * 2 + ((x4 - 1) >> 1);
-        fl = sh->cur.flags | F_DEC; dir = sh->cur.direct8[b8]; r = sh->cur.ref[list][b8];
+        dir = sh->cur.direct8[b8]; r = sh->cur.ref[list][b8];
       } else {
         if (!left_ok) return 0;
         int b8 = (y4 >> 1) * 2 + 1;
-        fl = sh->left.flags; dir = sh->left.direct8[b8]; r = sh->left.ref[list][b8];
+        dir = sh->left.direct8[b8]; r = sh->left.ref[list][b8];
       }
     } else {
       if (y4 > 0) {
         int b8 = ((y4 - 1) >> 1) * 2 + (x4 >> 1);
-        fl = sh->cur.flags | F_DEC; dir = sh->cur.direct8[b8]; r = sh->cur.ref[list][b8];
+        dir = sh->cur.direct8[b8]; r = sh->cur.ref[list][b8];
       } else {
         if (!top_ok) return 0;
-        fl = ring[mb_x].flags; dir = ring[mb_x].direct8[x4 >> 1]; r = ring[mb_x].ref[list][x4 >> 1];
+        dir = ring[mb_x].direct8[x4 >> 1]; r = ring[mb_x].ref[list][x4 >> 1];
       }
     }
-    (void)fl;
     if (is_b && dir) return 0;
     return r > 0;
   }
@@ -1185,8 +1200,8 @@ struct Walker {
     // returns 0 = I_NxN, 1 = I_16x16, 2 = I_PCM
     int ctx = 0;
     if (intra_slice) {
-      if (left_ok && (sh->left.flags & F_I16)) ctx++;
-      if (top_ok && (ring[mb_x].flags & F_I16)) ctx++;
+      if (left_ok && (lf & F_I16)) ctx++;
+      if (top_ok && (tf & F_I16)) ctx++;
       if (!bin(SE_OTHER, 0, base + ctx)) return 0;
       base += 2;
     } else {
@@ -1206,20 +1221,24 @@ struct Walker {
   AVR_FI void decode_mb() {
     MbRec& cur = sh->cur;
     const int nlists = is_b ? 2 : 1;
+    PROF_BEGIN(ps1);
     if (slice_type != 2) {
-      int ctx = (left_ok && !(sh->left.flags & F_SKIP)) + (top_ok && !(ring[mb_x].flags & F_SKIP));
+      int ctx = (left_ok && !(lf & F_SKIP)) + (top_ok && !(tf & F_SKIP));
       if (bin(SE_OTHER, 0, (is_b ? 24 : 11) + ctx)) {
-        cur.flags |= F_SKIP;
+        cf |= F_SKIP;
         if (is_b) {
-          cur.flags |= F_D16;
+          cf |= F_D16;
           cur.direct8[0] = cur.direct8[1] = cur.direct8[2] = cur.direct8[3] = 1;
         } else {
           cur.ref[0][0] = cur.ref[0][1] = cur.ref[0][2] = cur.ref[0][3] = 0;
         }
         last_dqp_nz = 0;
+        SPROF_END(1, ps1);
         return;
       }
     }
+    SPROF_END(1, ps1);
+    PROF_BEGIN(ps2);
     // mb_type
     int intra = 0, kind = 0, i16_cbp = 0, nparts = 0, vertical = 0, pred0 = 0, pred1 = 0, direct16 = 0;
     if (slice_type == 2) {
@@ -1239,7 +1258,7 @@ struct Walker {
         kind = intra_mb_type(17, 0, &i16_cbp);
       }
     } else {
-      int ctx = (left_ok && !(sh->left.flags & F_D16)) + (top_ok && !(ring[mb_x].flags & F_D16));
+      int ctx = (left_ok && !(lf & F_D16)) + (top_ok && !(tf & F_D16));
       if (!bin(SE_OTHER, 0, 27 + ctx)) {
         direct16 = 1;
         nparts = 4;
@@ -1270,17 +1289,19 @@ struct Walker {
         }
       }
     }
+    SPROF_END(2, ps2);
     if (err) return;
     if (intra && kind == 2) { err = -2; return; }  // I_PCM (skip_bytes hook, recode.cpp:161-163)
     int no_sub_lt8x8 = 1;
     int t8 = 0;
+    PROF_BEGIN(ps3);
     if (intra) {
-      cur.flags |= F_INTRA;
-      if (kind == 1) cur.flags |= F_I16;
+      cf |= F_INTRA;
+      if (kind == 1) cf |= F_I16;
       if (kind == 0) {
         if (t8mode) {
-          t8 = bin(SE_OTHER, 0, 399 + (left_ok && (sh->left.flags & F_T8)) + (top_ok && (ring[mb_x].flags & F_T8)));
-          if (t8) cur.flags |= F_T8;
+          t8 = bin(SE_OTHER, 0, 399 + (left_ok && (lf & F_T8)) + (top_ok && (tf & F_T8)));
+          if (t8) cf |= F_T8;
         }
         const int nmodes = t8 ? 4 : 16;
         for (int i = 0; i < nmodes; i++)
@@ -1291,16 +1312,17 @@ struct Walker {
           }
       }
       if (cat_ == 1 || cat_ == 2) {
-        int ctx = (left_ok && (sh->left.flags & F_INTRA) && (sh->left.flags & F_CPRED)) +
-                  (top_ok && (ring[mb_x].flags & F_INTRA) && (ring[mb_x].flags & F_CPRED));
+        int ctx = (left_ok && (lf & F_INTRA) && (lf & F_CPRED)) +
+                  (top_ok && (tf & F_INTRA) && (tf & F_CPRED));
         if (bin(SE_OTHER, 0, 64 + ctx)) {
-          cur.flags |= F_CPRED;
+          cf |= F_CPRED;
           if (bin(SE_OTHER, 0, 67)) bin(SE_OTHER, 0, 67);
         }
       }
+      SPROF_END(3, ps3);
     } else if (nparts == 4) {
       if (direct16) {
-        cur.flags |= F_D16;
+        cf |= F_D16;
         cur.direct8[0] = cur.direct8[1] = cur.direct8[2] = cur.direct8[3] = 1;
         if (!d8x8inf) no_sub_lt8x8 = 0;
       } else {
@@ -1345,6 +1367,8 @@ struct Walker {
             no_sub_lt8x8 = 0;
           }
         }
+        SPROF_END(2, ps3);
+        PROF_BEGIN(ps4);
         for (int list = 0; list < nlists; list++)
           for (int i = 0; i < 4; i++) {
             const int sp = (sub >> (8 * i)) & 7, spr = (sub >> (8 * i + 4)) & 3;
@@ -1352,6 +1376,8 @@ struct Walker {
             int nref = list ? nref1 : nref0;
             cur.ref[list][i] = (int8_t)(nref > 1 ? decode_ref(list, 2 * (i & 1), 2 * (i >> 1)) : 0);
           }
+        SPROF_END(4, ps4);
+        PROF_BEGIN(ps5);
         for (int list = 0; list < nlists; list++)
           for (int i = 0; i < 4; i++) {
             const int sp = (sub >> (8 * i)) & 7, sv = (sub >> (8 * i + 3)) & 1, spr = (sub >> (8 * i + 4)) & 3;
@@ -1364,8 +1390,11 @@ struct Walker {
               else mvd_part(list, x0 + j, y0, 1, 2);
             }
           }
+        SPROF_END(5, ps5);
       }
     } else {
+      SPROF_END(4, ps3);
+      PROF_BEGIN(ps4);
       for (int list = 0; list < nlists; list++)
         for (int i = 0; i < nparts; i++) {
           const int pr = i ? pred1 : pred0;
@@ -1377,6 +1406,8 @@ struct Walker {
           else if (!vertical) cur.ref[list][2 * i] = cur.ref[list][2 * i + 1] = (int8_t)ref;
           else cur.ref[list][i] = cur.ref[list][i + 2] = (int8_t)ref;
         }
+      SPROF_END(4, ps4);
+      PROF_BEGIN(ps5);
       for (int list = 0; list < nlists; list++)
         for (int i = 0; i < nparts; i++) {
           const int pr = i ? pred1 : pred0;
@@ -1385,8 +1416,10 @@ struct Walker {
           else if (vertical) mvd_part(list, 2 * i, 0, 2, 4);
           else mvd_part(list, 0, 2 * i, 4, 2);
         }
+      SPROF_END(5, ps5);
     }
     if (err) return;
+    PROF_BEGIN(ps6);
     int cbp;
     if (intra && kind == 1) {
       cbp = i16_cbp;
@@ -1404,11 +1437,11 @@ struct Walker {
       }
       cbp = c;
       if ((cbp & 15) && t8mode && !intra && no_sub_lt8x8 && (!direct16 || d8x8inf)) {
-        if (bin(SE_OTHER, 0, 399 + (left_ok && (sh->left.flags & F_T8)) + (top_ok && (ring[mb_x].flags & F_T8))))
-          cur.flags |= F_T8;
+        if (bin(SE_OTHER, 0, 399 + (left_ok && (lf & F_T8)) + (top_ok && (tf & F_T8))))
+          cf |= F_T8;
       }
     }
-    cur.cbp = (uint16_t)cbp;
+    cf |= (uint32_t)cbp << 16;
     if ((cbp & 0x3f) || (intra && kind == 1)) {
       int ctx = last_dqp_nz ? 1 : 0, val = 0;
       while (bin(SE_QPDELTA, val, 60 + ctx)) {
@@ -1416,9 +1449,11 @@ struct Walker {
         if (++val > 102) { err = -6; return; }
       }
       last_dqp_nz = val != 0;
+      SPROF_END(6, ps6);
       residual(intra && kind == 1, cbp);
     } else {
       last_dqp_nz = 0;
+      SPROF_END(6, ps6);
     }
   }
 };
@@ -1478,68 +1513,80 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
   w.mbs_done = 0;
   int addr = d->first_mb;
   const int lane = threadIdx.x;
+  const int npic = w.W * w.H;
+  w.mb_x = addr % w.W;   // then stepped: no integer division per macroblock
+  w.mb_y = addr / w.W;
+  {
+    const int j = lane, ph_c = (w.cat_ == 2 || w.cat_ == 3) ? 4 : 2;
+    int src = 0;
+    if (j >= 1 && j < 4) src = 1 + (j - 1) * 4 + (j == 1 ? 3 : ph_c - 1);   // nnz: bottom row of plane j - 1
+    else if (j >= 4 && j < 8) src = 13 + ((j - 4) >> 1) * 8 + 6 + ((j - 4) & 1);   // mvd[l][12..15]
+    else if (j == 8) src = 29;                       // ref[0][2..3] (| ref[1][2..3] from dword 30)
+    else if (j == 9) src = 31;                       // direct8[2..3]
+    else if (j >= 10 && j < 23) src = 32 + (j - 10); // mnnz[52]
+    w.edge_src = (uint32_t)src;
+  }
   for (;;) {
-    if (addr >= w.W * w.H) { w.err = -7; break; }
-    w.mb_x = addr % w.W;
-    w.mb_y = addr / w.W;
+    if (addr >= npic) { w.err = -7; break; }
+    PROF_BEGINW(ps0);
     w.left_ok = w.mb_x > 0 && addr - 1 >= w.first_mb;
-    w.top_ok = (w.ring[w.mb_x].flags & F_DEC) != 0;
-    // clear the current record (64 lanes)
+    {   // the upper neighbour's flags + cbp: the first dword of its edge record
+      w.tf = *(const uint32_t*)&w.ring[w.mb_x];
+      w.top_ok = (w.tf & F_DEC) != 0;
+      w.cf = 0;
+    }
+    // clear the current record (one dword per lane; ref[2][4] = dwords 29-30 to -1)
     {
       uint32_t* c32 = (uint32_t*)&w.sh->cur;
-      for (int i = lane; i < (int)sizeof(MbRec) / 4; i += 64) c32[i] = 0;
-      wave_sync();
-      for (int i = lane; i < 8; i += 64) ((int8_t*)w.sh->cur.ref)[i] = -1;
+      if (lane < (int)sizeof(MbRec) / 4) c32[lane] = (lane == 29 || lane == 30) ? 0xffffffffu : 0u;
       wave_sync();
     }
+    SPROF_ENDW(0, ps0);
+#ifdef AVR_PROFILE
+    w.sprofb[0]++;   // sub-section 0 counts macroblocks
+#endif
     PROF_BEGINW(t1);
     w.decode_mb();
     PROF_ENDW(1, t1);
     PROF_BEGINW(t7);
     if (w.err) break;
-    w.sh->cur.flags |= F_DEC;
+    w.cf |= F_DEC;
     w.mbs_done++;
-    w.last_mb = addr + 1 >= w.W * w.H;
-    // publish: bottom edge to the ring, full record to `left`, model bytes to the frame (RM)
+    w.last_mb = addr + 1 >= npic;
+    // publish: bottom edge to the ring, full record to `left`, model bytes to the frame (RM) --
+    // two lane-parallel LDS reads of the record (whole, and the edge's dwords), then the stores
     wave_sync();
     {
-      const MbRec& c = w.sh->cur;
-      EdgeRec& e = w.ring[w.mb_x];
-      const int ph_c = w.cat_ == 2 ? 4 : w.cat_ == 3 ? 4 : 2;
-      if (lane < 52) e.mnnz[lane] = c.mnnz[lane];
-      if (lane < 12) {
-        int p = lane / 4, x = lane % 4;
-        int ph = p == 0 ? 4 : ph_c;
-        e.nnz[p][x] = c.nnz[p][(ph - 1) * 4 + x];
-      }
-      if (lane < 16) {
-        int l = lane / 8, x = (lane / 2) % 4, comp = lane % 2;
-        e.mvd[l][x][comp] = c.mvd[l][12 + x][comp];
-      }
-      if (lane < 4) e.ref[lane / 2][lane % 2] = c.ref[lane / 2][2 + lane % 2];
-      if (lane < 2) e.direct8[lane] = c.direct8[2 + lane];
-      if (lane == 0) {
-        e.flags = c.flags;
-        e.cbp = c.cbp;
-      }
-      if (RM) {
-        uint8_t* f = w.frames + w.cur_off + ((int64_t)w.mb_y * w.W + w.mb_x) * 52;
-        if (lane < 52) f[lane] = c.mnnz[lane];
-      }
-      wave_sync();
-      uint32_t* l32 = (uint32_t*)&w.sh->left;
       const uint32_t* c32 = (const uint32_t*)&w.sh->cur;
-      for (int i = lane; i < (int)sizeof(MbRec) / 4; i += 64) l32[i] = c32[i];
+      const uint32_t v = c32[lane < 45 ? lane : 44];
+      const uint32_t ve = c32[w.edge_src], ref1 = c32[30];
+      uint32_t* l32 = (uint32_t*)&w.sh->left;
+      if (lane < 45) l32[lane] = v;
+      uint32_t* e32 = (uint32_t*)&w.ring[w.mb_x];
+      const uint32_t ev = lane == 8 ? (ve >> 16) | (ref1 & 0xffff0000u) : lane == 9 ? ve >> 16 : ve;
+      if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff007fu) : ev;   // dword 0: flags, pad, cbp
+      w.lf = w.cf;
+      if (RM) {   // MbRec dwords 32-44 are the 52 model bytes
+        uint32_t* f32 = (uint32_t*)(w.frames + w.cur_off + ((int64_t)w.mb_y * w.W + w.mb_x) * 52);
+        if (lane >= 32 && lane < 45) f32[lane - 32] = v;
+      }
       wave_sync();
     }
     PROF_ENDW(7, t7);
+    PROF_BEGINW(ps7);
     if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) {
       w.publish();
       if (!RM) w.update_prio();
     }
-    if (w.terminate(SE_EOS)) break;
+    const int eos = w.terminate(SE_EOS);
+    SPROF_ENDW(7, ps7);
+    if (eos) break;
     if (Walker<MODE, RM>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
     addr++;
+    if (++w.mb_x == w.W) {
+      w.mb_x = 0;
+      w.mb_y++;
+    }
   }
 }
 
@@ -1577,7 +1624,7 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
     w.target_mbs = d->payload_size ? (int)d->payload_size : 1 << 30;
   }
 #ifdef AVR_PROFILE
-  for (int i = 0; i < 8; i++) w.prof[i] = 0, w.profb[i] = 0;
+  for (int i = 0; i < 8; i++) w.prof[i] = 0, w.profb[i] = 0, w.sprof[i] = 0, w.sprofb[i] = 0;
 #endif
 }
 
@@ -1593,6 +1640,8 @@ AVR_FI void profile_slice(Walker<MODE, RM>& w) {
     for (int i = 0; i < 8; i++) {
       atomicAdd(&avr_prof[i], (unsigned long long)w.prof[i]);
       atomicAdd(&avr_prof[8 + i], (unsigned long long)w.profb[i]);
+      atomicAdd(&avr_prof[32 + i], (unsigned long long)w.sprof[i]);
+      atomicAdd(&avr_prof[40 + i], (unsigned long long)w.sprofb[i]);
     }
   }
 #else

@@ -32,7 +32,7 @@ def main():
     ps = avr.parse_stream(data)
     b = DeviceBatch(ctx, ps)
     L = avr.lib()
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * 64)()
     L.avr_debug_profile(2, buf)   # clear the generator's counters
     out = {}
     for mode, name in ((0, "compress"), (1, "decompress")):
