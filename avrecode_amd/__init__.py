@@ -56,7 +56,7 @@ SLICE_DESC = np.dtype([
     ("slice_type", "<i4"), ("slice_qp", "<i4"), ("cabac_init_idc", "<i4"), ("first_mb", "<i4"),
     ("mb_width", "<i4"), ("mb_height", "<i4"), ("num_ref_idx_l0", "<i4"), ("num_ref_idx_l1", "<i4"),
     ("chroma_array_type", "<i4"), ("transform_8x8_mode", "<i4"), ("direct_8x8_inference", "<i4"),
-    ("x264_build", "<i4"), ("picture_id", "<i4"), ("coded", "<i4"),
+    ("x264_build", "<i4"), ("picture_id", "<i4"), ("coded", "<i4"), ("structure", "<i4"),
 ], align=True)
 SLICE_RESULT = np.dtype([("out_len", "<u4"), ("status", "<i4"), ("bins", "<u4"), ("mbs", "<u4"),
                          ("bill", "<u4", (6,))], align=True)
@@ -84,7 +84,7 @@ class _SynthParams(ctypes.Structure):
                 ("mb_width", "mb_height", "slice_type", "slice_qp", "chroma_format_idc", "transform_8x8_mode",
                  "num_ref_idx_l0", "num_ref_idx_l1")] + [("seed", ctypes.c_uint64)] + \
                [("slices_per_picture", ctypes.c_int32), ("gop_length", ctypes.c_int32), ("repeat", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("structure", ctypes.c_int32)]
 
 
 @dataclass
@@ -102,6 +102,7 @@ class SynthParams:
     slices_per_picture: int = 1
     gop_length: int = 0          # > 0: IDR I picture every gop_length pictures, slice_type between
     repeat: int = 1              # > 1: the pictures written this many times (frame numbers advance)
+    structure: int = 0           # 0 progressive, 1 field pictures (PAFF), 2 MBAFF frames
 
 
 _lib = None
@@ -361,7 +362,7 @@ class Context:
         sp = _SynthParams(params.mb_width, params.mb_height, params.slice_type, params.slice_qp,
                           params.chroma_format_idc, params.transform_8x8_mode, params.num_ref_idx_l0,
                           params.num_ref_idx_l1, params.seed, params.slices_per_picture, params.gop_length,
-                          params.repeat, 0)
+                          params.repeat, params.structure)
         out, olen = ctypes.c_void_p(), ctypes.c_size_t()
         self._check(lib().avr_synthesize_stream(self._h, ctypes.byref(sp), int(n), ctypes.byref(out),
                                                 ctypes.byref(olen)), "synthesize")

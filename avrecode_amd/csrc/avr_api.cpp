@@ -174,6 +174,18 @@ void build_tables(avr::EngineTables* t) {
     t->hot.sig8x8[i] = sig8[i];
     t->hot.last8x8[i] = last8[i];
   }
+  // field coded (FFmpeg significant_coeff_flag_offset[1], last_coeff_flag_offset[1],
+  // significant_coeff_flag_offset_8x8[1] == recode.cpp:691-694)
+  static const int16_t sig_f[14] = {277, 292, 306, 321, 324, 436, 776, 791, 805, 675, 820, 835, 849, 733};
+  static const int16_t last_f[14] = {338, 353, 367, 382, 385, 451, 864, 879, 893, 699, 908, 923, 937, 757};
+  static const uint8_t sig8_f[63] = {
+    0, 1, 1, 2, 2, 3, 3, 4, 5, 6, 7, 7, 7, 8, 4, 5, 6, 9, 10, 10, 8, 11, 12, 11, 9, 9, 10, 10, 8, 11, 12, 11,
+    9, 9, 10, 10, 8, 11, 12, 11, 9, 9, 10, 10, 8, 13, 13, 9, 9, 10, 10, 8, 13, 13, 9, 9, 10, 10, 14, 14, 14, 14, 14};
+  for (int c = 0; c < 14; c++) {
+    t->sig_base_fld[c] = sig_f[c];
+    t->last_base_fld[c] = last_f[c];
+  }
+  for (int i = 0; i < 63; i++) t->sig8x8_fld[i] = sig8_f[i];
   const double alpha = std::pow(0.01875 / 0.5, 1.0 / 63.0);
   for (int s = 0; s < 64; s++) t->gen_plps[s] = (uint16_t)std::lround(65536.0 * 0.5 * std::pow(alpha, s));
 }
@@ -233,6 +245,8 @@ avr_slice_desc desc_from_header(const avr::SliceInfo& s) {
   d.x264_build = s.h.x264_build;
   d.picture_id = s.picture_id;
   d.coded = 1;
+  d.structure = s.h.field_pic ? (s.h.bottom_field ? AVR_STRUCT_BOTTOM_FIELD : AVR_STRUCT_TOP_FIELD)
+              : s.h.mbaff ? AVR_STRUCT_MBAFF : AVR_STRUCT_FRAME;
   return d;
 }
 
@@ -247,6 +261,7 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
   const int nf = plan.n_files();
   if (nf > avr::rmode_max_files_per_pass()) return kRModeFallback;
   struct Fb { int gen = -1, w = 0, h = 0, fid = 0; } fb[2];
+  std::vector<uint8_t> gen_parity;   // field parities (1 top, 2 bottom) seen per frame generation
   int cur = 0;
   std::vector<int64_t> gen_off, goff(2 * (size_t)n);
   int64_t fbytes = 0;
@@ -267,6 +282,7 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
       const bool reinit_other = (nw.w != W || nw.h != H) && (ot.w != W || ot.h != H);
       nw.gen = (int)gen_off.size();
       gen_off.push_back(fbytes);
+      gen_parity.push_back(0);
       fbytes += (int64_t)W * H * 52;
       if (reinit_other) {
         ot.gen = -1;
@@ -281,6 +297,13 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
     if (ot.gen >= 0 && (ot.w != W || ot.h != H)) return kRModeFallback;
     goff[2 * k] = gen_off[fb[cur].gen];
     goff[2 * k + 1] = ot.gen < 0 ? -1 : gen_off[ot.gen];
+    // a field whose frame has no slice of the other parity yet (its rows are still zero in the
+    // sequential model, but filled in the buffer the parallel scan reads): offsets are 4-aligned
+    if (d.structure == AVR_STRUCT_TOP_FIELD || d.structure == AVR_STRUCT_BOTTOM_FIELD) {
+      uint8_t& seen = gen_parity[fb[cur].gen];
+      if (!(seen & (d.structure == AVR_STRUCT_TOP_FIELD ? 2 : 1))) goff[2 * k] |= 1;
+      seen |= (uint8_t)(d.structure == AVR_STRUCT_TOP_FIELD ? 1 : 2);
+    }
   }
   if (fbytes > ((int64_t)4 << 30)) return kRModeFallback;
   const size_t lds = avr::shared_bytes(plan.max_w);
@@ -1133,16 +1156,21 @@ int avr_container_describe(const uint8_t* in, size_t n, char** json, uint8_t** r
 int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t** out, size_t* out_len) {
   if (!c || !p || n <= 0 || !out || !out_len || p->mb_width <= 0 || p->mb_height <= 0 || p->slice_type < 0 ||
       p->slice_type > 2 || p->chroma_format_idc < 1 || p->chroma_format_idc > 3 || p->gop_length < 0 ||
-      p->repeat < 0)
+      p->repeat < 0 || p->structure < 0 || p->structure > 2 || (p->structure && (p->mb_height & 1)))
     return AVR_ERR_INVALID_ARGUMENT;
   HIP_TRY(c, hipSetDevice(c->device));
   Plan plan;
-  const int mbs = p->mb_width * p->mb_height;
-  const int spp = std::max(1, std::min(p->slices_per_picture, mbs));
+  // a coded picture: the frame, or (field pictures) each of its two fields in turn
+  const int fields = p->structure == 1 ? 2 : 1;
+  const int mbs = p->mb_width * p->mb_height / fields;
+  // MBAFF slices start on a macroblock pair
+  const int unit = p->structure == 2 ? 2 : 1;
+  const int spp = std::max(1, std::min(p->slices_per_picture, mbs / unit));
   std::vector<int> pic_of, first_of;
-  for (int i = 0; i < n * spp; i++) {
-    const int pic = i / spp, j = i % spp;
-    const int first = (int)((int64_t)j * mbs / spp), next = (int)((int64_t)(j + 1) * mbs / spp);
+  for (int i = 0; i < n * fields * spp; i++) {
+    const int pic = i / (spp * fields), fi = (i / spp) % fields, j = i % spp;
+    const int first = unit * (int)((int64_t)j * (mbs / unit) / spp);
+    const int next = unit * (int)((int64_t)(j + 1) * (mbs / unit) / spp);
     pic_of.push_back(pic);
     first_of.push_back(first);
     avr_slice_desc d;
@@ -1165,6 +1193,8 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
     d.picture_id = pic;
     d.first_mb = first;
     d.coded = 1;
+    d.structure = p->structure == 1 ? (fi ? AVR_STRUCT_BOTTOM_FIELD : AVR_STRUCT_TOP_FIELD)
+                : p->structure == 2 ? AVR_STRUCT_MBAFF : AVR_STRUCT_FRAME;
     d.payload_offset = p->seed * 0x100000001B3ull + (uint64_t)i;  // generator seed
     d.payload_size = (uint32_t)(next - first);                    // generator: macroblocks to emit
     d.out_capacity = (uint32_t)std::min<uint64_t>((uint64_t)mbs * 384 + 4096, 0x7fffffffu);
@@ -1186,7 +1216,7 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
   stream.reserve(bytes * reps + 256);
   for (int t = 0; t < reps; t++)
     for (int i = 0; i < (int)plan.descs.size(); i++)
-      avr::synth_write_slice(&stream, *p, plan.descs[i].slice_type, t * n + pic_of[i], first_of[i],
+      avr::synth_write_slice(&stream, *p, plan.descs[i].slice_type, t * n + pic_of[i], plan.descs[i].structure, first_of[i],
                              outb.data() + plan.descs[i].out_offset, res[i].out_len);
   *out = (uint8_t*)malloc(stream.size());
   if (!*out) return AVR_ERR_OUT_OF_MEMORY;

@@ -47,6 +47,11 @@ static_assert(sizeof(HotTables) % 16 == 0, "HotTables is copied in 16-byte units
 
 struct EngineTables {
   HotTables hot;
+  // field-coded macroblocks (field pictures, MBAFF field pairs): Table 9-34's field ctxIdxOffsets of
+  // significant / last_significant_coeff_flag per ctxBlockCat and Table 9-43's 8x8 field ctxIdxInc
+  // of significant_coeff_flag (last is shared); patched into the walker's LDS copy of `hot`
+  int16_t sig_base_fld[16], last_base_fld[16];
+  uint8_t sig8x8_fld[64];
   int8_t mn[4][1024][2];  // init (m,n): [0] I, [1..3] cabac_init_idc 0..2
   uint16_t gen_plps[64];  // generator: p_LPS(pStateIdx) * 65536
 };

@@ -229,9 +229,11 @@ bool parse_slice_header(const Sps* sps_table, const Pps* pps_table, const uint8_
   h->frame_num = (int)b.u(sps.log2_max_frame_num);
   if (!sps.frame_mbs_only) {
     h->field_pic = (int)b.u1();
-    if (h->field_pic) b.u1();
+    if (h->field_pic) h->bottom_field = (int)b.u1();
   }
   h->mbaff = sps.mb_aff && !h->field_pic;
+  // first_mb_in_slice counts macroblock pairs in an MBAFF frame (7.4.3)
+  if (h->mbaff) h->first_mb *= 2;
   if (type == 5) h->idr_pic_id = (int)b.ue();
   if (sps.poc_type == 0) {
     h->poc_lsb = (int)b.u(sps.log2_max_poc_lsb);
@@ -303,9 +305,11 @@ bool parse_slice_header(const Sps* sps_table, const Pps* pps_table, const uint8_
   h->direct_8x8_inference = sps.direct_8x8_inference;
   h->mb_width = sps.mb_width;
   h->mb_height = sps.mb_height;
-  h->supported = pps.entropy_coding_mode && !h->field_pic && !h->mbaff && !sps.separate_colour_plane &&
+  // macroblocks in this picture: a field has half the frame's rows
+  const int pic_mbs = sps.mb_width * (h->field_pic ? sps.mb_height / 2 : sps.mb_height);
+  h->supported = pps.entropy_coding_mode && !h->mbaff && !sps.separate_colour_plane &&
                  (is_p || is_b || h->slice_type == 2) && h->cabac_init_idc <= 2 &&
-                 h->first_mb < sps.mb_width * sps.mb_height && h->num_ref_idx[0] <= 32 && h->num_ref_idx[1] <= 32 &&
+                 h->first_mb < pic_mbs && h->num_ref_idx[0] <= 32 && h->num_ref_idx[1] <= 32 &&
                  sps.mb_width <= 1024;
   return true;
 }
@@ -489,8 +493,15 @@ bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s) {
   const bool new_pic = !have_prev_ || h.first_mb == 0 || h.first_mb <= p.first_mb || h.frame_num != p.frame_num ||
                        h.pps_id != p.pps_id || h.poc_lsb != p.poc_lsb ||
                        (h.nal_unit_type == 5) != (p.nal_unit_type == 5) || h.idr_pic_id != p.idr_pic_id ||
-                       (h.nal_ref_idc == 0) != (p.nal_ref_idc == 0);
-  if (new_pic) picture_id_++;
+                       (h.nal_ref_idc == 0) != (p.nal_ref_idc == 0) || h.field_pic != p.field_pic ||
+                       h.bottom_field != p.bottom_field;
+  // picture_id stands in for the frame_num the fork hands frame_spec: the second
+  // field of a field pair shares its frame_num with the first, so it keeps the first's id and the
+  // model keeps filling the same frame (the fields interleave in its frame-sized buffer)
+  const bool second_field = new_pic && have_prev_ && h.field_pic && p.field_pic && h.frame_num == p.frame_num &&
+                            h.bottom_field != p.bottom_field && !second_field_;
+  if (new_pic && !second_field) picture_id_++;
+  if (new_pic) second_field_ = second_field;
   prev_ = h;
   have_prev_ = true;
   s->h = h;

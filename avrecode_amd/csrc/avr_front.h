@@ -24,7 +24,7 @@ struct Pps {
 
 struct SliceHeader {
   int nal_unit_type = 0, nal_ref_idc = 0, first_mb = 0, slice_type = 0, pps_id = 0, frame_num = 0;
-  int field_pic = 0, mbaff = 0, idr_pic_id = 0, poc_lsb = 0, num_ref_idx[2] = {0, 0}, cabac_init_idc = -1;
+  int field_pic = 0, bottom_field = 0, mbaff = 0, idr_pic_id = 0, poc_lsb = 0, num_ref_idx[2] = {0, 0}, cabac_init_idc = -1;
   int slice_qp = 26, chroma_array_type = 1, transform_8x8_mode = 0, direct_8x8_inference = 0;
   int mb_width = 0, mb_height = 0, x264_build = -1, entropy_coding_mode = 0;
   size_t cabac_start = 0;   // byte offset of slice_data() in the RBSP
@@ -62,6 +62,7 @@ class StreamParser {
   bool have_prev_ = false;
   SliceHeader prev_;
   int picture_id_ = 0;
+  bool second_field_ = false;   // the current picture is the second field of a pair
 };
 
 // recode.proto

@@ -71,9 +71,11 @@ void synth_write_parameter_sets(std::vector<uint8_t>* out, const avr_synth_param
   s.ue(4);               // max_num_ref_frames
   s.u(0, 1);
   s.ue(p.mb_width - 1);
-  s.ue(p.mb_height - 1);
-  s.u(1, 1);             // frame_mbs_only
-  s.u(1, 1);             // direct_8x8_inference
+  const bool frames_only = p.structure == 0;
+  s.ue((frames_only ? p.mb_height : p.mb_height / 2) - 1);   // pic_height_in_map_units_minus1
+  s.u(frames_only ? 1 : 0, 1);                              // frame_mbs_only
+  if (!frames_only) s.u(p.structure == 2 ? 1 : 0, 1);        // mb_adaptive_frame_field_flag
+  s.u(1, 1);             // direct_8x8_inference (required without frame_mbs_only)
   s.u(0, 1);             // no cropping
   s.u(0, 1);             // no VUI
   s.trailing();
@@ -102,13 +104,19 @@ void synth_write_parameter_sets(std::vector<uint8_t>* out, const avr_synth_param
 }
 
 void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int slice_type, int index,
-                       int first_mb, const uint8_t* payload, size_t payload_len) {
-  const bool idr = slice_type == 2;
+                       int structure, int first_mb, const uint8_t* payload, size_t payload_len) {
+  const bool idr = slice_type == 2 && structure != AVR_STRUCT_BOTTOM_FIELD;
+  const bool field = structure == AVR_STRUCT_TOP_FIELD || structure == AVR_STRUCT_BOTTOM_FIELD;
   BitWriter h;
-  h.ue((uint32_t)first_mb);      // first_mb_in_slice
+  h.ue((uint32_t)(structure == AVR_STRUCT_MBAFF ? first_mb / 2 : first_mb));   // first_mb_in_slice (pairs in MBAFF)
   h.ue((uint32_t)slice_type + 5);
   h.ue(0);                       // pps id
-  h.u(idr ? 0 : (uint32_t)(index & 0xffff), 16);
+  // frame_num: an IDR frame's is 0, and both fields of a frame carry the same one
+  h.u(slice_type == 2 && (idr || structure == AVR_STRUCT_BOTTOM_FIELD) ? 0 : (uint32_t)(index & 0xffff), 16);
+  if (p.structure != 0) {
+    h.u(field ? 1 : 0, 1);       // field_pic_flag
+    if (field) h.u(structure == AVR_STRUCT_BOTTOM_FIELD ? 1 : 0, 1);   // bottom_field_flag
+  }
   if (idr) h.ue((uint32_t)(index & 0xffff));
   if (slice_type == 1) h.u(1, 1);           // direct_spatial_mv_pred_flag
   if (slice_type != 2) {

@@ -486,6 +486,14 @@ struct Walker {
   uint64_t rng;
   // slice state
   int W, H, mb_x, mb_y, slice_type, is_b, cat_, t8mode;
+  // field coding: fld = the current macroblocks are field coded (their significance contexts use
+  // the field tables); my = the model's row of the current macroblock, FFmpeg's sl->mb_y (frame
+  // rows: a field picture's row r is frame row 2 r + bottom), stepped by ystep per parse row
+  int fld, fld_pic, my, ystep;
+  // RM parallel compress (rscan_kernel): this slice belongs to the first-coded field of its frame,
+  // so the other field's rows -- already in the frame buffer, which that kernel fills before it
+  // reads -- must read as the zeros the sequential model still sees there
+  int top_pending;
   int left_ok, top_ok, last_dqp_nz;
   // flags (bits 0-6, F_*) and coded_block_pattern (bits 16-31) of the current macroblock and of
   // its left / upper neighbours, in one scalar register each for the whole macroblock (the
@@ -527,12 +535,17 @@ struct Walker {
   uint32_t byp_e;         // decompress: the estimator of &bypass_context (recode.cpp:1049), Shared::est[1024] while walking
   AVR_FI static uint32_t wlane(uint32_t v, uint32_t L, uint32_t x) { return __lane_id() == L ? x : v; }
   AVR_FI int rc_addr(int cat, uint32_t j) const {
-    // 8x8 categories (5, 9, 13) use sig ctxIdxInc 0-14 and last 0-8 only: the other lanes would
-    // alias the next syntax element's contexts, so they hold nothing
+    // Only the contexts the category can use: a lane past them would alias another syntax
+    // element's context and write a stale copy back over it at rc_writeback -- within the
+    // category (8x8 sig ctxIdxInc 0-14 / last 0-8 then the next element) or, with the field
+    // offsets, transform_size_8x8_flag (ctxIdx 399-400 = chroma AC's last lanes 30-31), which
+    // bin() updates in LDS while the category stays loaded across macroblocks.
     const bool c8 = cat == 5 || cat == 9 || cat == 13;
-    if (c8 && (j == 15 || (j >= 25 && j < 32))) return -1;
-    return j < 16 ? T->sig_base[cat] + (int)j : j < 32 ? T->last_base[cat] + (int)j - 16
-         : j < 42 ? T->abs_base[cat] + (int)j - 32 : j < 46 ? T->cbf_base[cat] + (int)j - 42 : -1;
+    const int ns = c8 ? 15 : cat == 3 ? 3 : (cat == 1 || cat == 4 || cat == 7 || cat == 11) ? 14 : 15;
+    const int nl = c8 ? 9 : ns;
+    if (j < 16) return (int)j < ns ? T->sig_base[cat] + (int)j : -1;
+    if (j < 32) return (int)j - 16 < nl ? T->last_base[cat] + (int)j - 16 : -1;
+    return j < 42 ? T->abs_base[cat] + (int)j - 32 : j < 46 ? T->cbf_base[cat] + (int)j - 42 : -1;
   }
   AVR_FI void rc_writeback() {
     if (rc_cat < 0) return;
@@ -631,6 +644,24 @@ struct Walker {
   uint64_t prof[8], sprof[8];
   uint32_t profb[8], sprofb[8];
 #endif
+
+  // Frame or field significance contexts for the macroblocks that follow: the walker's LDS copy of
+  // the ctxIdx bases (rc_addr, sig_map) and the 8x8 ctxIdxInc map in sig8_v (for decompress also
+  // the frame map in bits 8-15: the model keys 8x8 positions by the frame map, recode.cpp:703-704,
+  // as does T->sig8x8, which is never patched).  Only this wave reads the patched entries.
+  AVR_FI void set_fld(int f) {
+    if (f == fld) return;
+    rc_writeback();
+    fld = f;
+    const uint32_t L = __lane_id();
+    HotTables* t = &sh->tab;
+    if (L < 16) t->sig_base[L] = f ? G->sig_base_fld[L] : G->hot.sig_base[L];
+    else if (L < 32) t->last_base[L - 16] = f ? G->last_base_fld[L - 16] : G->hot.last_base[L - 16];
+    const uint32_t fr = T->sig8x8[L];
+    const uint32_t cm = f ? (uint32_t)G->sig8x8_fld[L] : fr;
+    sig8_v = MODE == MODE_DECOMPRESS ? (cm | fr << 8) : cm;
+    wave_sync();
+  }
 
   // ------------------------------------------------------------------ bins through the model
   // Macroblock-layer contexts kMcBase .. kMcBase + 63 (sub_mb_type, B mb_type, mvd, ref_idx,
@@ -790,15 +821,17 @@ struct Walker {
   // ------------------------------------------------------------------ model neighbours
   // model num_nonzeros of a neighbouring macroblock (get_neighbor_sub_mb, recode.cpp:419-471)
   AVR_FI int mnnz_left(int idx) const {
-    if (RM) return frames[cur_off + ((int64_t)mb_y * W + mb_x - 1) * 52 + idx];
+    if (RM) return frames[cur_off + ((int64_t)my * W + mb_x - 1) * 52 + idx];
     return left_ok ? sh->left.mnnz[idx] : 0;
   }
   AVR_FI int mnnz_top(int idx) const {
-    if (RM) return frames[cur_off + ((int64_t)(mb_y - 1) * W + mb_x) * 52 + idx];
+    if (RM) return top_pending ? 0 : frames[cur_off + ((int64_t)(my - 1) * W + mb_x) * 52 + idx];
+    // fresh model per slice: in a field picture the model's upper row belongs to the other field
+    if (fld_pic) return 0;
     return top_ok ? ring[mb_x].mnnz[idx] : 0;
   }
   AVR_FI int mnnz_prev(int idx) const {
-    if (RM) return prev_off < 0 ? 0 : frames[prev_off + ((int64_t)mb_y * W + mb_x) * 52 + idx];
+    if (RM) return prev_off < 0 ? 0 : frames[prev_off + ((int64_t)my * W + mb_x) * 52 + idx];
     return 0;
   }
 
@@ -808,7 +841,7 @@ struct Walker {
     int has_left, has_above, lv = 0, av = 0;
     if (n >= 48) {
       has_left = mb_x > 0;
-      has_above = mb_y > 0;
+      has_above = my > 0;
       if (has_left) lv = mnnz_left(n);
       if (has_above) av = mnnz_top(n);
     } else {
@@ -816,7 +849,7 @@ struct Walker {
       int li = L & 63, ui = U & 63;
       if (max >= 32) { li &= ~3; ui &= ~3; }
       has_left = !(L & 128) || mb_x > 0;
-      has_above = !(U & 128) || mb_y > 0;
+      has_above = !(U & 128) || my > 0;
       if (has_left) lv = (L & 128) ? mnnz_left(li) : sh->cur.mnnz[li];
       if (has_above) av = (U & 128) ? mnnz_top(ui) : sh->cur.mnnz[ui];
     }
@@ -941,14 +974,16 @@ struct Walker {
       PROF_BEGIN(t3);
       int pos;
       for (pos = 0; pos < max - 1; pos++) {
-        int sc, lc;
+        int sc, lc, zk = 0;
         if (max == 64) {
-          sc = (int)__builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);
+          const uint32_t v = __builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);   // CABAC inc | key inc << 8
+          sc = (int)(v & 0xff);
+          zk = (int)(v >> 8);
           lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
         }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
         else sc = lc = pos;
-        const int zo = max == 64 ? sc : (is_dc && c422) ? (pos < 2 ? 0 : pos < 4 ? 1 : 2) : pos;
+        const int zo = max == 64 ? zk : (is_dc && c422) ? (pos < 2 ? 0 : pos < 4 ? 1 : 2) : pos;
         const int idx = seb + (zo * (max == 64 ? 64 : 16) + nnz_m) * (max == 64 ? 64 : 16) + cnt;   // sig_est_index
         uint32_t slot;
         uint32_t e = est_load(sh, est_g, idx, &slot);
@@ -1496,7 +1531,8 @@ template <int MODE, bool RM>
 AVR_FI void walk_slice(Walker<MODE, RM>& w) {
   const avr_slice_desc* d = w.d;
   w.W = d->mb_width;
-  w.H = d->mb_height;
+  // a field picture is a picture of half the frame's rows (d->mb_height is the frame's)
+  w.H = w.fld_pic ? d->mb_height >> 1 : d->mb_height;
   w.slice_type = d->slice_type;
   w.is_b = d->slice_type == 1;
   w.cat_ = d->chroma_array_type;
@@ -1516,6 +1552,8 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
   const int npic = w.W * w.H;
   w.mb_x = addr % w.W;   // then stepped: no integer division per macroblock
   w.mb_y = addr / w.W;
+  w.ystep = w.fld_pic ? 2 : 1;
+  w.my = w.mb_y * w.ystep + (d->structure == AVR_STRUCT_BOTTOM_FIELD ? 1 : 0);
   {
     const int j = lane, ph_c = (w.cat_ == 2 || w.cat_ == 3) ? 4 : 2;
     int src = 0;
@@ -1567,7 +1605,7 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
       if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff007fu) : ev;   // dword 0: flags, pad, cbp
       w.lf = w.cf;
       if (RM) {   // MbRec dwords 32-44 are the 52 model bytes
-        uint32_t* f32 = (uint32_t*)(w.frames + w.cur_off + ((int64_t)w.mb_y * w.W + w.mb_x) * 52);
+        uint32_t* f32 = (uint32_t*)(w.frames + w.cur_off + ((int64_t)w.my * w.W + w.mb_x) * 52);
         if (lane >= 32 && lane < 45) f32[lane - 32] = v;
       }
       wave_sync();
@@ -1586,6 +1624,7 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
     if (++w.mb_x == w.W) {
       w.mb_x = 0;
       w.mb_y++;
+      w.my += w.ystep;
     }
   }
 }
@@ -1606,7 +1645,10 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   vtab_load(w.vt, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
-  w.sig8_v = w.T->sig8x8[__lane_id()];
+  w.fld_pic = d->structure == AVR_STRUCT_TOP_FIELD || d->structure == AVR_STRUCT_BOTTOM_FIELD;
+  w.fld = -1;
+  w.set_fld(w.fld_pic);
+  w.top_pending = 0;
   w.last8_v = w.T->last8x8[__lane_id()];
   if (MODE == MODE_DECOMPRESS) w.byp_e = w.sh->est[1024];
   w.mc_load();

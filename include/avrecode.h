@@ -109,7 +109,10 @@ typedef struct {
   int32_t chroma_array_type, transform_8x8_mode, direct_8x8_inference, x264_build;
   int32_t picture_id;        /* decode-order picture counter (frame_spec, recode.cpp:824-843) */
   int32_t coded;             /* 0: skip_coded slice (reference mode only calls frame_spec) */
+  int32_t structure;         /* AVR_STRUCT_*: frame, top / bottom field picture (PAFF), MBAFF frame;
+                              * mb_height is the FRAME height in macroblocks in every case */
 } avr_slice_desc;
+enum { AVR_STRUCT_FRAME = 0, AVR_STRUCT_TOP_FIELD = 1, AVR_STRUCT_BOTTOM_FIELD = 2, AVR_STRUCT_MBAFF = 3 };
 
 typedef struct {
   uint32_t out_len;          /* bytes written at out_offset */
@@ -244,7 +247,9 @@ typedef struct {
   int32_t repeat;                /* 0 or 1: once; r > 1: the n generated pictures are written r
                                   * times, copy t with frame_num / idr_pic_id advanced by t n (a
                                   * long stream tiled from one GOP; the payloads repeat) */
-  int32_t reserved;
+  int32_t structure;             /* 0 progressive frames; 1 field pictures (PAFF: each picture a
+                                  * top then a bottom field, mb_height even); 2 MBAFF frames (every
+                                  * macroblock pair field or frame coded at random, mb_height even) */
 } avr_synth_params;
 /* Generate n pictures on the device (each slices_per_picture slices, in decode order) and return
  * them as one Annex-B stream (SPS/PPS + the slice NAL units) in host memory.  Pictures are

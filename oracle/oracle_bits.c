@@ -245,6 +245,7 @@ int avr_parse_slice_header(const avr_param_sets_t *ps, const uint8_t *rbsp, size
     if (h->field_pic) h->bottom_field = (int)br_u1(&b);
   }
   h->mbaff = sps->mb_aff && !h->field_pic;
+  if (h->mbaff) h->first_mb *= 2; /* first_mb_in_slice counts macroblock pairs (7.4.3) */
   if (nal_unit_type == 5) h->idr_pic_id = (int)br_ue(&b);
   if (sps->poc_type == 0) {
     h->poc_lsb = (int)br_u(&b, sps->log2_max_poc_lsb);
@@ -329,9 +330,11 @@ int avr_parse_slice_header(const avr_param_sets_t *ps, const uint8_t *rbsp, size
   h->constrained_intra_pred = pps->constrained_intra_pred;
   h->mb_width = sps->mb_width;
   h->mb_height = sps->mb_height;
-  h->supported = pps->entropy_coding_mode && !h->field_pic && !h->mbaff && !sps->separate_colour_plane &&
+  /* macroblocks in this picture: a field has half the frame's rows */
+  int pic_mbs = sps->mb_width * (h->field_pic ? sps->mb_height / 2 : sps->mb_height);
+  h->supported = pps->entropy_coding_mode && !h->mbaff && !sps->separate_colour_plane &&
                  h->slice_type != AVR_SLICE_SP && h->slice_type != AVR_SLICE_SI &&
-                 (h->cabac_init_idc <= 2) && h->first_mb < sps->mb_width * sps->mb_height &&
+                 (h->cabac_init_idc <= 2) && h->first_mb < pic_mbs &&
                  h->num_ref_idx_active[0] <= 32 && h->num_ref_idx_active[1] <= 32;
   return 0;
 }

@@ -401,7 +401,7 @@ typedef struct {
 typedef struct {
   avr_param_sets_t ps;
   int x264_build;
-  int have_prev, picture_id;
+  int have_prev, picture_id, second_field;
   avr_slice_hdr_t prev;
 } stream_state_t;
 
@@ -431,8 +431,14 @@ static int nal_to_slice(stream_state_t *st, const uint8_t *nal, size_t n, slice_
   int new_pic = !st->have_prev || s->h.first_mb == 0 || s->h.first_mb <= p->first_mb ||
                 s->h.frame_num != p->frame_num || s->h.pps_id != p->pps_id || s->h.poc_lsb != p->poc_lsb ||
                 (s->h.nal_unit_type == 5) != (p->nal_unit_type == 5) || s->h.idr_pic_id != p->idr_pic_id ||
-                (s->h.nal_ref_idc == 0) != (p->nal_ref_idc == 0);
-  if (new_pic) st->picture_id++;
+                (s->h.nal_ref_idc == 0) != (p->nal_ref_idc == 0) || s->h.field_pic != p->field_pic ||
+                s->h.bottom_field != p->bottom_field;
+  /* frame_spec receives the fork's frame_num, which the two fields of a pair share: the second
+   * field keeps the first's picture id, so the model fills one frame with both */
+  int second_field = new_pic && st->have_prev && s->h.field_pic && p->field_pic && s->h.frame_num == p->frame_num &&
+                     s->h.bottom_field != p->bottom_field && !st->second_field;
+  if (new_pic && !second_field) st->picture_id++;
+  if (new_pic) st->second_field = second_field;
   st->prev = s->h;
   st->have_prev = 1;
   s->picture_id = st->picture_id;

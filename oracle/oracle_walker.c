@@ -13,7 +13,7 @@
  *   significant_coeff_flag and end_coding_type(SIG_MAP) right after the map.
  * frame_spec is called once per slice with a decode-order picture counter.
  *
- * Supported: progressive frames (no MBAFF / field pictures), CABAC, ChromaArrayType 0..3,
+ * Supported: progressive frames and field pictures (no MBAFF yet), CABAC, ChromaArrayType 0..3,
  * 8x8 transform, I/P/B slices.  I_PCM returns an error (the reference throws, recode.cpp:161-163).
  */
 #include <stdio.h>
@@ -49,6 +49,16 @@ static const int16_t last_base[14] = {166 + 0, 166 + 15, 166 + 29, 166 + 44, 166
                                       572 + 15, 572 + 29, 690, 616 + 0, 616 + 15, 616 + 29, 748};
 static const int16_t abs_base[14] = {227 + 0, 227 + 10, 227 + 20, 227 + 30, 227 + 39, 426, 952 + 0,
                                      952 + 10, 952 + 20, 708, 982 + 0, 982 + 10, 982 + 20, 766};
+/* field-coded macroblocks (field pictures, MBAFF field pairs): Table 9-34's field ctxIdxOffsets
+ * (FFmpeg h264_cabac.c significant_coeff_flag_offset[1] / last_coeff_flag_offset[1]) */
+static const int16_t sig_base_fld[14] = {277 + 0, 277 + 15, 277 + 29, 277 + 44, 277 + 47, 436, 776 + 0,
+                                         776 + 15, 776 + 29, 675, 820 + 0, 820 + 15, 820 + 29, 733};
+static const int16_t last_base_fld[14] = {338 + 0, 338 + 15, 338 + 29, 338 + 44, 338 + 47, 451, 864 + 0,
+                                          864 + 15, 864 + 29, 699, 908 + 0, 908 + 15, 908 + 29, 757};
+/* Table 9-43 ctxIdxInc of significant_coeff_flag in 8x8 field blocks (== recode.cpp:691-694) */
+static const uint8_t sig8x8_fld[63] = {
+  0, 1, 1, 2, 2, 3, 3, 4, 5, 6, 7, 7, 7, 8, 4, 5, 6, 9, 10, 10, 8, 11, 12, 11, 9, 9, 10, 10, 8, 11, 12, 11,
+  9, 9, 10, 10, 8, 11, 12, 11, 9, 9, 10, 10, 8, 13, 13, 9, 9, 10, 10, 8, 13, 13, 9, 9, 10, 10, 14, 14, 14, 14, 14};
 /* Table 9-43 ctxIdxInc for significant / last in 8x8 frame blocks (== recode.cpp:686-690) */
 static const uint8_t sig8x8[63] = {
   0, 1, 2, 3, 4, 5, 5, 4, 4, 3, 3, 4, 4, 4, 5, 5, 4, 4, 4, 4, 3, 3, 6, 7, 7, 7, 8, 9, 10, 9, 8, 7,
@@ -76,6 +86,7 @@ typedef struct {
   int last_dqp_nz;
   int is_b;
   int err;
+  int fld;           /* the current macroblock is field coded (field picture, or an MBAFF field pair) */
 } walker_t;
 
 static inline int bin(walker_t *w, int se, int k, int ctx) {
@@ -346,12 +357,12 @@ static void residual_block(walker_t *w, int cat, int n, int max, int is_dc, int 
     int last;
     for (last = 0; last < max - 1; last++) {
       int sctx, lctx;
-      if (max == 64) { sctx = sig8x8[last]; lctx = last8x8[last]; }
+      if (max == 64) { sctx = w->fld ? sig8x8_fld[last] : sig8x8[last]; lctx = last8x8[last]; }
       else if (cat == 3) { sctx = lctx = imin(last / numc8x8, 2); }
       else sctx = lctx = last;
-      if (bin(w, SE_SIG, last, sig_base[cat] + sctx)) {
+      if (bin(w, SE_SIG, last, (w->fld ? sig_base_fld : sig_base)[cat] + sctx)) {
         idx[cnt++] = last;
-        if (bin(w, SE_LAST, last, last_base[cat] + lctx)) { last = max; break; }
+        if (bin(w, SE_LAST, last, (w->fld ? last_base_fld : last_base)[cat] + lctx)) { last = max; break; }
       }
     }
     if (last == max - 1) idx[cnt++] = last;
@@ -612,12 +623,16 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
   w.h = h;
   w.hk = hooks;
   w.W = h->mb_width;
-  w.H = h->mb_height;
+  /* a field picture is its own picture of half the frame's rows (FFmpeg PAFF); the model hooks
+   * still see the frame (h->mb_height) and FFmpeg's frame row of each macroblock,
+   * sl->mb_y = 2 * field row + bottom_field_flag (h264_slice.c, decode_slice) */
+  w.H = h->field_pic ? h->mb_height / 2 : h->mb_height;
+  w.fld = h->field_pic;
   w.is_b = h->slice_type == AVR_SLICE_B;
   w.mbs = (wmb_t *)calloc((size_t)w.W * w.H, sizeof(wmb_t));
   if (!w.mbs) return -1;
   avr_cabac_init_states(w.state, h->slice_type == AVR_SLICE_I ? -1 : h->cabac_init_idc, h->slice_qp);
-  hooks->frame_spec(hooks->opaque, picture_id, w.W, w.H);
+  hooks->frame_spec(hooks->opaque, picture_id, w.W, h->mb_height);
   int addr = h->first_mb;
   int ret = 0;
   avr_walk_mbs_done = 0;
@@ -627,7 +642,7 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
     w.cur = &w.mbs[addr];
     w.left = x > 0 && w.mbs[addr - 1].decoded ? &w.mbs[addr - 1] : NULL;
     w.top = y > 0 && w.mbs[addr - w.W].decoded ? &w.mbs[addr - w.W] : NULL;
-    hooks->mb_xy(hooks->opaque, x, y);
+    hooks->mb_xy(hooks->opaque, x, h->field_pic ? 2 * y + h->bottom_field : y);
     decode_mb(&w);
     if (getenv("AVR_WALK_DEBUG"))
       fprintf(stderr, "mb %d skip %d intra %d i16 %d t8 %d cbp %03x d16 %d nnz0 %d %d %d %d\n", addr, w.cur->skip, w.cur->intra,

@@ -1,0 +1,119 @@
+"""Field-coded H.264: field pictures (PAFF) and MBAFF frames, from the device
+generator (avr_synthesize_stream, structure 1 / 2), against the oracle.
+
+What the fork does for these (FFmpeg h264_cabac.c / h264_slice.c, restated in oracle_walker.c):
+field-coded macroblocks take the field ctxIdx offsets of significant / last_significant_coeff_flag
+and the field 8x8 significance map (recode.cpp:691-694 holds that map); the model keys of those
+bins do not change (recode.cpp:686-704 uses the frame map and frame offsets), the model hooks see
+FFmpeg's frame row of each macroblock (a field picture's row r is frame row 2 r + bottom) and the
+frame's size, and the two fields of a frame share frame_num, so frame_spec keeps one model frame
+for both.  No interlaced stream of the reference or of a real encoder is present:
+parity here is product against oracle, both restating the published algorithm."""
+import os
+import tempfile
+from pathlib import Path
+
+import pytest
+
+from _oracle import oracle_cli
+
+torch = pytest.importorskip("torch")
+import avrecode_amd as avr  # noqa: E402
+from test_gpu_parity import _check_batch_against_oracle  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = avr.Context(0)
+    yield c
+    c.close()
+
+
+def _paff(ctx, n, **kw):
+    args = dict(mb_width=14, mb_height=10, slice_type=0, slice_qp=26, seed=5, structure=1)
+    args.update(kw)
+    return ctx.synthesize(avr.SynthParams(**args), n)
+
+
+def test_field_pictures_structure(ctx):
+    data = _paff(ctx, 4, gop_length=2, slices_per_picture=2)
+    d = avr.parse_stream(data).descs
+    assert len(d) == 4 * 2 * 2
+    assert [int(x) for x in d["structure"]] == [1, 1, 2, 2] * 4
+    # the two fields of a frame share the model's frame (frame_num), frames advance
+    assert [int(x) for x in d["picture_id"]] == [k // 4 + 1 for k in range(16)]
+    assert (d["mb_height"] == 10).all() and [int(x) for x in d["first_mb"]] == [0, 35] * 8
+    assert [int(t) for t in d["slice_type"]] == [2] * 4 + [0] * 4 + [2] * 4 + [0] * 4
+
+
+CASES = [
+    # (slice_type, chroma, t8, l0, l1, gop, spp)
+    (2, 1, 1, 1, 1, 0, 1),
+    (0, 1, 1, 2, 1, 3, 1),
+    (1, 1, 1, 2, 2, 4, 2),
+    (0, 2, 1, 1, 1, 2, 1),
+    (1, 3, 1, 1, 3, 3, 1),
+    (0, 3, 0, 3, 1, 0, 3),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c)))
+def test_field_picture_slices_match_oracle(ctx, case):
+    st, cf, t8, l0, l1, gop, spp = case
+    data = _paff(ctx, 3, slice_type=st, chroma_format_idc=cf, transform_8x8_mode=t8, num_ref_idx_l0=l0,
+                 num_ref_idx_l1=l1, gop_length=gop, slices_per_picture=spp, seed=40 + st + 3 * cf)
+    ps, verdict = _check_batch_against_oracle(ctx, data, require_all=True)
+    assert len(ps.descs) == 3 * 2 * spp
+
+
+@pytest.mark.parametrize("case", CASES[1:5], ids=lambda c: "x".join(map(str, c)))
+def test_field_picture_files_match_oracle(ctx, case):
+    """Whole files in both model modes: the reference model's frame-row coordinates, shared
+    frame per field pair and previous-frame contexts, against the oracle; the parallel
+    reference-model compress against the sequential kernel."""
+    st, cf, t8, l0, l1, gop, spp = case
+    data = _paff(ctx, 4, slice_type=st, chroma_format_idc=cf, transform_8x8_mode=t8, num_ref_idx_l0=l0,
+                 num_ref_idx_l1=l1, gop_length=gop, slices_per_picture=spp, seed=70 + st + 3 * cf)
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / "paff.264"
+        f.write_bytes(data)
+        for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+            avrc = ctx.compress(data, model)
+            assert avrc == oracle_cli("compress", f, mode=mode), mode
+            assert ctx.decompress(avrc) == data
+    os.environ["AVR_RMODE_SEQUENTIAL"] = "1"
+    try:
+        seq = ctx.compress(data, avr.MODEL_REFERENCE)
+    finally:
+        del os.environ["AVR_RMODE_SEQUENTIAL"]
+    assert seq == ctx.compress(data, avr.MODEL_REFERENCE)
+
+
+def test_field_and_frame_pictures_mixed(ctx):
+    """A progressive stream followed by a field stream of the same size (two SPS): frame and field
+    context tables alternate in one reference-model walk."""
+    a = ctx.synthesize(avr.SynthParams(mb_width=12, mb_height=8, slice_type=0, slice_qp=27, seed=8), 2)
+    b = _paff(ctx, 2, mb_width=12, mb_height=8, slice_type=0, seed=9, gop_length=2)
+    data = a + b + a
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / "mix.264"
+        f.write_bytes(data)
+        for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+            avrc = ctx.compress(data, model)
+            assert avrc == oracle_cli("compress", f, mode=mode), mode
+            assert ctx.decompress(avrc) == data
+
+
+def test_field_fixture_matches_golden(ctx):
+    """The committed field-picture stream (tests/golden/fields.json) compresses to the oracle's
+    pinned containers in both model modes and decompresses back."""
+    import hashlib
+    import json
+    g = json.loads((Path(__file__).parent / "golden" / "fields.json").read_text())
+    data = (Path(__file__).parent / "fixtures" / g["file"]).read_bytes()
+    for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+        avrc = ctx.compress(data, model)
+        assert hashlib.sha256(avrc).hexdigest() == g[mode]["avrc_sha256"], mode
+        assert ctx.decompress(avrc) == data

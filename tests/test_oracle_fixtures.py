@@ -40,3 +40,21 @@ def test_reference_8x8_ordering_cannot_roundtrip(monkeypatch):
     env = dict(**__import__("os").environ, AVR_REFERENCE_8X8_BUG="1")
     r = subprocess.run([str(cli), "roundtrip", str(FIX / "realshort.mp4")], capture_output=True, env=env)
     assert r.returncode != 0
+
+
+FIELDS = json.loads((ROOT / "tests/golden/fields.json").read_text())
+
+
+def test_field_fixture_regenerates_and_roundtrips():
+    """Field pictures (PAFF, tests/golden/fields.json): every field slice parses to end_of_slice
+    and regenerates its payload (field ctxIdx offsets and 8x8 field map, oracle_walker.c), and
+    whole-file compress in both model modes round-trips to the pinned containers."""
+    _, cli = build_oracle()
+    f = FIX / FIELDS["file"]
+    r = subprocess.run([str(cli), "slices", str(f)], capture_output=True, text=True)
+    assert r.returncode == 0 and f"slices ok {FIELDS['slices']} bad 0" in r.stdout, r.stdout[-2000:]
+    for mode in ("R", "P"):
+        assert b"roundtrip succeeded" in oracle_cli("roundtrip", f, mode=mode)
+        avrc = oracle_cli("compress", f, mode=mode)
+        assert len(avrc) == FIELDS[mode]["avrc_len"]
+        assert hashlib.sha256(avrc).hexdigest() == FIELDS[mode]["avrc_sha256"]
