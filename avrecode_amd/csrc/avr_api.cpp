@@ -228,6 +228,10 @@ void append_aligned(std::vector<uint8_t>* arena, const uint8_t* p, size_t n, siz
   *off = o;
 }
 
+// EdgeRec slots of the LDS ring a slice needs (launch max_mb_width): an MBAFF slice keeps its pair
+// edges and records there too (Walker::pair_edge)
+int ring_cols(const avr_slice_desc& d) { return d.structure == AVR_STRUCT_MBAFF ? 3 * d.mb_width + 7 : d.mb_width; }
+
 avr_slice_desc desc_from_header(const avr::SliceInfo& s) {
   avr_slice_desc d;
   memset(&d, 0, sizeof(d));
@@ -573,7 +577,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
       d.payload_size = (uint32_t)s.size;
       d.read_limit = (uint32_t)s.read_limit;
       d.out_capacity = (uint32_t)(s.size * 2 + 256);
-      plan.max_w = std::max(plan.max_w, d.mb_width);
+      plan.max_w = std::max(plan.max_w, ring_cols(d));
       cand_of[f][i] = (int)plan.descs.size();
       plan.descs.push_back(d);
     }
@@ -617,7 +621,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
             d.read_limit = (uint32_t)s.read_limit;
             d.out_capacity = (uint32_t)(s.size * 4 + 4096);
           }
-          rp.max_w = std::max(rp.max_w, d.mb_width);
+          rp.max_w = std::max(rp.max_w, ring_cols(d));
           idx.push_back({f, (int)i});
           rp.descs.push_back(d);
         }
@@ -752,7 +756,7 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
     avr_slice_desc d = descs[k];
     const avr::PbBlock& b = j->blocks[block_of[k]];
     if (d.coded) append_aligned(&plan->arena, b.cabac, b.cabac_len, 16, &d.payload_offset);
-    plan->max_w = std::max(plan->max_w, d.mb_width);
+    plan->max_w = std::max(plan->max_w, ring_cols(d));
     j->desc_of_block[block_of[k]] = (int)plan->descs.size();
     plan->descs.push_back(d);
   }
@@ -1071,7 +1075,7 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
     d.out_offset = work;
     d.out_capacity = (uint32_t)(s.size * 2 + 256);
     work += ((uint64_t)d.out_capacity + 15) & ~15ull;
-    plan.max_w = std::max(plan.max_w, d.mb_width);
+    plan.max_w = std::max(plan.max_w, ring_cols(d));
     mh = std::max(mh, d.mb_height);
     plan.descs.push_back(d);
   }
@@ -1200,7 +1204,7 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
     d.out_capacity = (uint32_t)std::min<uint64_t>((uint64_t)mbs * 384 + 4096, 0x7fffffffu);
     plan.descs.push_back(d);
   }
-  plan.max_w = p->mb_width;
+  plan.max_w = p->structure == 2 ? 3 * p->mb_width + 7 : p->mb_width;
   plan.arena.assign(16, 0);
   std::vector<avr_slice_result> res;
   std::vector<uint8_t> outb;
@@ -1308,7 +1312,7 @@ int run_traces(avr_hooks_session* hs) {
     // 2 bytes per bin; H.264 bounds the bins of a slice by ~32/3 per payload byte plus a
     // per-macroblock allowance (7.4.2.2), well inside this
     d.out_capacity = (uint32_t)std::min<uint64_t>(0xfffffff0ull, 2ull * (16ull * s.size + 2048ull * d.mb_width * d.mb_height / 8 + 4096));
-    plan.max_w = std::max(plan.max_w, d.mb_width);
+    plan.max_w = std::max(plan.max_w, ring_cols(d));
     slice_of.push_back((int)i);
     plan.descs.push_back(d);
   }

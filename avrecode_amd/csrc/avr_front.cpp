@@ -307,7 +307,7 @@ bool parse_slice_header(const Sps* sps_table, const Pps* pps_table, const uint8_
   h->mb_height = sps.mb_height;
   // macroblocks in this picture: a field has half the frame's rows
   const int pic_mbs = sps.mb_width * (h->field_pic ? sps.mb_height / 2 : sps.mb_height);
-  h->supported = pps.entropy_coding_mode && !h->mbaff && !sps.separate_colour_plane &&
+  h->supported = pps.entropy_coding_mode && !sps.separate_colour_plane &&
                  (is_p || is_b || h->slice_type == 2) && h->cabac_init_idc <= 2 &&
                  h->first_mb < pic_mbs && h->num_ref_idx[0] <= 32 && h->num_ref_idx[1] <= 32 &&
                  sps.mb_width <= 1024;

@@ -22,6 +22,9 @@ constexpr int kEstGlobal = kEstLog + 2 * kEstLogCap;
 static_assert(kEstGlobal % 8 == 0 && kEstTable % 8 == 0, "16-byte clears");
 
 constexpr uint32_t kFlagBill = 1;   // launch flag: the coders bill per CodingType (avr_slice_result.bill)
+// launch flags bits 16-31: EdgeRec slots of the LDS ring (max_mb_width of shared_bytes), set by
+// launch_slices; an MBAFF slice needs 3 mb_width + 7 (Walker::pair_edge)
+constexpr int kFlagRingShift = 16;
 size_t shared_bytes(int max_mb_width);
 // does workgroup b of a 4G-workgroup launch land on CU group b mod G (schedule_kernel's assumption)?
 hipError_t probe_round_robin(size_t lds, bool* ok);

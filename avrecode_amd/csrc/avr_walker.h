@@ -494,6 +494,10 @@ struct Walker {
   // so the other field's rows -- already in the frame buffer, which that kernel fills before it
   // reads -- must read as the zeros the sequential model still sees there
   int top_pending;
+  // MBAFF frame (AVR_STRUCT_MBAFF): macroblock pairs; pst = the pair's state (PST_*); ring_cols =
+  // EdgeRec slots the launch gave the LDS ring (an MBAFF slice needs 3 W + 7, see pair_edge)
+  int mbaff;
+  uint32_t pst, ring_cols;
   int left_ok, top_ok, last_dqp_nz;
   // flags (bits 0-6, F_*) and coded_block_pattern (bits 16-31) of the current macroblock and of
   // its left / upper neighbours, in one scalar register each for the whole macroblock (the
@@ -807,7 +811,9 @@ struct Walker {
     if (x4 > 0) return sh->cur.nnz[p][y4 * 4 + x4 - 1];
     if (!left_ok) return (cf & F_INTRA) ? 64 : 0;
     int v;
-    if (nnz_override(lf, &v)) return v;
+    // MBAFF: rows of one left macroblock come from both macroblocks of the left pair; the view's
+    // flags byte holds each row's source 8x8-transform flag
+    if (nnz_override(mbaff ? (((uint32_t)sh->left.flags >> y4) & 1u) * (uint32_t)F_T8 : lf, &v)) return v;
     return sh->left.nnz[p][y4 * 4 + pw - 1];
   }
   AVR_FI int nnz_top(int p, int x4, int y4) const {
@@ -816,6 +822,196 @@ struct Walker {
     int v;
     if (nnz_override(tf, &v)) return v;
     return ring[mb_x].nnz[p][x4];
+  }
+
+  // ------------------------------------------------------------------ MBAFF (field / frame pairs)
+  // The per-bin code reads its neighbours from sh->left (the left macroblock), ring[mb_x] (the
+  // bottom edge of the upper one) and lf / tf / left_ok / top_ok.  In an MBAFF frame the
+  // neighbours of a macroblock follow ITU-T H.264 Table 6-4 (6.4.12.2): rows of the left one may
+  // come from either macroblock of the left pair, the upper one depends on the field / frame
+  // coding of both pairs, and vertical mvd / ref_idx of a neighbour of the other kind are scaled
+  // (9.3.3.1.1.6-7, FFmpeg fill_decode_caches MAP_F2F).  mbaff_view writes exactly that view into
+  // sh->left and ring[mb_x] before each coded macroblock, so the per-bin code is the same.
+  // LDS of an MBAFF launch (ring_cols >= 3 W + 7): ring[0, W) the views, ring[W + x] /
+  // ring[2 W + x] the bottom edges of the last top / bottom macroblock of column x, then three
+  // MbRec (this pair's top, the left pair's top and bottom, dword 0 = their cf) and four words:
+  // the dword 0 of the left pair's top / bottom and of the upper pair's top / bottom edges.
+  static constexpr uint32_t F_FLD = 0x100;   // cf: field macroblock
+  static constexpr uint32_t PST_FLD = 1, PST_SKIPT = 2, PST_SKIPB = 4, PST_BOT = 8;
+  AVR_FI EdgeRec* pair_edge(int bot) const { return ring + (1 + bot) * W; }
+  AVR_FI MbRec* pair_rec() const { return (MbRec*)(ring + 3 * W); }
+  AVR_FI uint32_t* pair_nb() const { return (uint32_t*)(pair_rec() + 3); }
+  AVR_FI uint32_t lds_u32(const uint32_t* p) const { return __builtin_amdgcn_readfirstlane(*p); }
+
+  // top macroblock of a pair: the neighbour pairs' words and the inferred field flag (7.4.4: the
+  // left pair's in the slice, else the upper pair's, else frame)
+  AVR_FI void mbaff_pair_start() {
+    const uint32_t L = __lane_id();
+    uint32_t v = 0;
+    if (L < 2) v = mb_x > 0 ? *(const uint32_t*)&pair_rec()[1 + L] : 0u;
+    else if (L < 4) v = *(const uint32_t*)&pair_edge((int)L - 2)[mb_x];
+    if (L < 4) pair_nb()[L] = v;
+    wave_sync();
+    const uint32_t lt = __builtin_amdgcn_readlane(v, 0), at = __builtin_amdgcn_readlane(v, 2);
+    pst = ((lt & F_DEC) ? (lt & F_FLD) : (at & F_DEC) ? (at & F_FLD) : 0u) ? PST_FLD : 0u;
+  }
+  // mb_skip_flag ctxIdx (FFmpeg decode_cabac_mb_skip); top_d0 = this pair's top macroblock's cf
+  AVR_FI int mbaff_skip_ctx(int bottom, uint32_t fld, uint32_t top_d0) const {
+    const uint32_t* nb = pair_nb();
+    const uint32_t lt = lds_u32(nb), lb = lds_u32(nb + 1), at = lds_u32(nb + 2), ab = lds_u32(nb + 3);
+    uint32_t a = 0, b = 0;
+    if (lt & F_DEC) a = (bottom && fld == ((lt & F_FLD) ? 1u : 0u)) ? lb : lt;
+    if (fld) {
+      if (at & F_DEC) b = (!bottom && (at & F_FLD)) ? at : ab;
+    } else {
+      b = bottom ? top_d0 : ab;
+    }
+    return (is_b ? 24 : 11) + ((a & F_DEC) && !(a & F_SKIP)) + ((b & F_DEC) && !(b & F_SKIP));
+  }
+  // mb_field_decoding_flag, ctxIdx 70-72 (FFmpeg decode_cabac_field_decoding_flag)
+  AVR_FI uint32_t mbaff_field_flag(uint32_t inferred) {
+    const uint32_t at = lds_u32(pair_nb() + 2);
+    return (uint32_t)bin(SE_OTHER, 0, 70 + (mb_x > 0 && inferred) + ((at & F_DEC) && (at & F_FLD)));
+  }
+  // FFmpeg's order: a skipped top macroblock takes the bottom's skip flag next and, when the bottom
+  // is coded, the pair's field flag; a coded top reads the field flag after its skip flag
+  AVR_FI int mbaff_skip() {
+    const int bottom = (pst & PST_BOT) != 0;
+    uint32_t fld = pst & PST_FLD;
+    int skip;
+    if (bottom && (pst & PST_SKIPT)) skip = (pst & PST_SKIPB) != 0;
+    else skip = bin(SE_OTHER, 0, mbaff_skip_ctx(bottom, fld, lds_u32((const uint32_t*)&pair_rec()[0])));
+    if (skip && !bottom) {
+      pst |= PST_SKIPT;
+      if (bin(SE_OTHER, 0, mbaff_skip_ctx(1, fld, F_DEC | F_SKIP))) {
+        pst |= PST_SKIPB;
+      } else {
+        fld = mbaff_field_flag(fld);
+        pst = (pst & ~PST_FLD) | fld;
+      }
+    }
+    if (skip && fld) cf |= F_FLD;
+    return skip;
+  }
+  // Table 6-4, xN < 0: the left pair's macroblock (s: 0 top, 1 bottom) and 4x4 row r holding row y4
+  // of a plane maxH samples high, for a field (fld) or frame current macroblock and a frame
+  // (afrm) or field left pair
+  AVR_FI static void left_src(uint32_t fld, int afrm, int bottom, int y4, int maxH, int* s, int* r) {
+    const int yN = 4 * y4;
+    if (!fld) {
+      if (afrm) { *s = bottom; *r = y4; return; }
+      *s = 0;
+      *r = (bottom ? (yN + maxH) >> 1 : yN >> 1) >> 2;
+      return;
+    }
+    if (afrm) {
+      const int y2 = 2 * yN + bottom;
+      if (yN < maxH / 2) { *s = 0; *r = y2 >> 2; }
+      else { *s = 1; *r = (y2 - maxH) >> 2; }
+      return;
+    }
+    *s = bottom;
+    *r = y4;
+  }
+  // vertical |mvd| bytes (1, 3) and ref_idx bytes of a neighbour of the other coding: a field
+  // neighbour of a frame macroblock counts double motion and half the references, and vice versa
+  AVR_FI static uint32_t scale_mvd(uint32_t v, uint32_t fld) {
+    return fld ? ((v & 0x00ff00ffu) | ((v >> 1) & 0x7f007f00u)) : ((v & 0x00ff00ffu) | ((v & 0xff00ff00u) << 1));
+  }
+  AVR_FI static uint32_t scale_ref(uint32_t v, uint32_t fld) {
+    uint32_t o = 0;
+    for (int k = 0; k < 4; k++) {
+      int r = (int8_t)(v >> (8 * k));
+      if (r >= 0) r = fld ? r * 2 : r >> 1;
+      o |= (uint32_t)(uint8_t)r << (8 * k);
+    }
+    return o;
+  }
+  AVR_FI void mbaff_view(int bottom, uint32_t fld) {
+    set_fld((int)fld);
+    nref0 = d->num_ref_idx_l0 << fld;   // a field macroblock addresses fields: twice the references
+    nref1 = d->num_ref_idx_l1 << fld;
+    const uint32_t L = __lane_id();
+    const uint32_t* nb = pair_nb();
+    const uint32_t lt = lds_u32(nb), lb = lds_u32(nb + 1), at = lds_u32(nb + 2);
+    // ---- left: sh->left, lane j = dword j, gathered from the left pair's records
+    left_ok = (lt & F_DEC) != 0;
+    if (left_ok) {
+      const int afrm = !(lt & F_FLD);
+      const MbRec* lp = pair_rec() + 1;
+      int s0, r0, s2, r2;
+      left_src(fld, afrm, bottom, 0, 16, &s0, &r0);
+      left_src(fld, afrm, bottom, 2, 16, &s2, &r2);
+      const uint32_t A = s0 ? lb : lt, C = s2 ? lb : lt;
+      const uint32_t cbpA = A >> 16, cbpC = C >> 16;
+      const uint32_t cbp = (cbpA & 0x7F0u) | (((cbpA >> ((r0 >> 1) * 2 + 1)) & 1u) << 1) |
+                           (((cbpC >> ((r2 >> 1) * 2 + 1)) & 1u) << 3);
+      lf = (A & 0xffffu) | cbp << 16;
+      uint32_t t8rows = 0;
+      for (int y4 = 0; y4 < 4; y4++) {
+        int sy, ry;
+        left_src(fld, afrm, bottom, y4, 16, &sy, &ry);
+        t8rows |= (((sy ? lb : lt) & F_T8) ? 1u : 0u) << y4;
+      }
+      int s = 0, dw = 0;
+      if (L >= 1 && L < 13) {          // nnz rows
+        const int p = ((int)L - 1) >> 2;
+        int r;
+        left_src(fld, afrm, bottom, ((int)L - 1) & 3, (cat_ == 1 && p) ? 8 : 16, &s, &r);
+        dw = 1 + p * 4 + min(r, 3);
+      } else if (L >= 13 && L < 29) {  // mvd rows (two dwords per row)
+        const int k = ((int)L - 13) & 7;
+        int r;
+        left_src(fld, afrm, bottom, k >> 1, 16, &s, &r);
+        dw = 13 + (((int)L - 13) >> 3) * 8 + r * 2 + (k & 1);
+      } else if (L == 29 || L == 30 || L == 31) {
+        s = s0;
+        dw = (int)L;
+      } else if (L >= 32 && L < 45) {  // model bytes: the left macroblock in the same row
+        s = bottom;
+        dw = (int)L;
+      }
+      uint32_t v = L < 45 ? ((const uint32_t*)&lp[s])[dw] : 0u;
+      const uint32_t v2 = (L >= 29 && L < 32) ? ((const uint32_t*)&lp[s2])[L] : 0u;
+      if (L == 0) {
+        v = t8rows | cbp << 16;
+      } else if (L >= 13 && L < 29) {
+        if (fld != (uint32_t)(!afrm)) v = scale_mvd(v, fld);
+      } else if (L == 29 || L == 30 || L == 31) {
+        // b8 1 <- row 0's source, b8 3 <- row 2's (the only left 8x8 blocks read: ref_idx / direct
+        // of partitions at y4 = 0 and 2)
+        const uint32_t b1 = (v >> (8 * ((r0 >> 1) * 2 + 1))) & 0xff, b3 = (v2 >> (8 * ((r2 >> 1) * 2 + 1))) & 0xff;
+        v = (L == 31 ? 0u : 0xff00ffu) | b1 << 8 | b3 << 24;
+        if (L != 31 && fld != (uint32_t)(!afrm)) v = scale_ref(v, fld);
+      }
+      if (L < 45) ((uint32_t*)&sh->left)[L] = v;
+    }
+    // ---- upper: ring[mb_x] from the pair edges (parse neighbour B) + the model's upper macroblock
+    const int above = (at & F_DEC) != 0;
+    const int sel = !fld ? (bottom ? 1 : above ? 2 : 0) : above ? ((!bottom && (at & F_FLD)) ? 1 : 2) : 0;
+    const int msel = bottom ? 1 : above ? 2 : 0;
+    uint32_t v = 0;
+    if (L < 10 && sel) v = ((const uint32_t*)&pair_edge(sel - 1)[mb_x])[L];
+    else if (L >= 10 && L < 23 && msel) v = ((const uint32_t*)&pair_edge(msel - 1)[mb_x])[L];
+    const uint32_t t0 = __builtin_amdgcn_readlane(v, 0);
+    if (sel && ((t0 & F_FLD) ? 1u : 0u) != fld) {
+      if (L >= 4 && L < 8) v = scale_mvd(v, fld);
+      else if (L == 8) v = scale_ref(v, fld);
+    }
+    if (L < 23) ((uint32_t*)&ring[mb_x])[L] = v;
+    tf = t0;
+    top_ok = sel != 0;
+    wave_sync();
+  }
+  AVR_FI void mbaff_layer_begin() {
+    const int bottom = (pst & PST_BOT) != 0;
+    uint32_t fld = pst & PST_FLD;
+    if (!bottom) {
+      fld = mbaff_field_flag(fld);
+      pst = (pst & ~PST_FLD) | fld;
+    }
+    if (fld) cf |= F_FLD;
+    mbaff_view(bottom, fld);
   }
 
   // ------------------------------------------------------------------ model neighbours
@@ -828,7 +1024,7 @@ struct Walker {
     if (RM) return top_pending ? 0 : frames[cur_off + ((int64_t)(my - 1) * W + mb_x) * 52 + idx];
     // fresh model per slice: in a field picture the model's upper row belongs to the other field
     if (fld_pic) return 0;
-    return top_ok ? ring[mb_x].mnnz[idx] : 0;
+    return (top_ok | mbaff) ? ring[mb_x].mnnz[idx] : 0;   // MBAFF: the view holds the model's upper macroblock
   }
   AVR_FI int mnnz_prev(int idx) const {
     if (RM) return prev_off < 0 ? 0 : frames[prev_off + ((int64_t)my * W + mb_x) * 52 + idx];
@@ -1258,8 +1454,10 @@ struct Walker {
     const int nlists = is_b ? 2 : 1;
     PROF_BEGIN(ps1);
     if (slice_type != 2) {
-      int ctx = (left_ok && !(lf & F_SKIP)) + (top_ok && !(tf & F_SKIP));
-      if (bin(SE_OTHER, 0, (is_b ? 24 : 11) + ctx)) {
+      int skip;
+      if (mbaff) skip = mbaff_skip();
+      else skip = bin(SE_OTHER, 0, (is_b ? 24 : 11) + (left_ok && !(lf & F_SKIP)) + (top_ok && !(tf & F_SKIP)));
+      if (skip) {
         cf |= F_SKIP;
         if (is_b) {
           cf |= F_D16;
@@ -1272,6 +1470,7 @@ struct Walker {
         return;
       }
     }
+    if (mbaff) mbaff_layer_begin();
     SPROF_END(1, ps1);
     PROF_BEGIN(ps2);
     // mb_type
@@ -1519,7 +1718,9 @@ AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
       for (int i = lane; i < kEtabSize + 64; i += nt) w.sh->etab[i] = 0;
   }
   uint32_t* ring32 = (uint32_t*)w.ring;
-  for (int i = lane; i < w.W * (int)sizeof(EdgeRec) / 4; i += nt) ring32[i] = 0;
+  // MBAFF: the pair edges and records too (walk_slice refuses the slice when they do not fit)
+  const int cols = (d->structure == AVR_STRUCT_MBAFF && (int)w.ring_cols >= 3 * w.W + 7) ? 3 * w.W + 7 : w.W;
+  for (int i = lane; i < cols * (int)sizeof(EdgeRec) / 4; i += nt) ring32[i] = 0;
   if (lane < 2) {
     w.sh->fifo_head[lane] = 0;
     w.sh->fifo_tail[lane] = 0;
@@ -1554,6 +1755,15 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
   w.mb_y = addr / w.W;
   w.ystep = w.fld_pic ? 2 : 1;
   w.my = w.mb_y * w.ystep + (d->structure == AVR_STRUCT_BOTTOM_FIELD ? 1 : 0);
+  w.mbaff = d->structure == AVR_STRUCT_MBAFF;
+  w.pst = 0;
+  if (w.mbaff) {   // pairs in raster order: mb_y = pair row, my = 2 mb_y + bottom
+    if ((int)w.ring_cols < 3 * w.W + 7 || (addr & 1)) { w.err = -20; return; }
+    w.mb_x = (addr >> 1) % w.W;
+    w.mb_y = (addr >> 1) / w.W;
+    w.ystep = 2;
+    w.my = 2 * w.mb_y;
+  }
   {
     const int j = lane, ph_c = (w.cat_ == 2 || w.cat_ == 3) ? 4 : 2;
     int src = 0;
@@ -1567,12 +1777,15 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
   for (;;) {
     if (addr >= npic) { w.err = -7; break; }
     PROF_BEGINW(ps0);
-    w.left_ok = w.mb_x > 0 && addr - 1 >= w.first_mb;
-    {   // the upper neighbour's flags + cbp: the first dword of its edge record
+    if (!w.mbaff) {
+      w.left_ok = w.mb_x > 0 && addr - 1 >= w.first_mb;
+      // the upper neighbour's flags + cbp: the first dword of its edge record
       w.tf = *(const uint32_t*)&w.ring[w.mb_x];
       w.top_ok = (w.tf & F_DEC) != 0;
-      w.cf = 0;
+    } else if (!(w.pst & Walker<MODE, RM>::PST_BOT)) {
+      w.mbaff_pair_start();
     }
+    w.cf = 0;
     // clear the current record (one dword per lane; ref[2][4] = dwords 29-30 to -1)
     {
       uint32_t* c32 = (uint32_t*)&w.sh->cur;
@@ -1598,12 +1811,26 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
       const uint32_t* c32 = (const uint32_t*)&w.sh->cur;
       const uint32_t v = c32[lane < 45 ? lane : 44];
       const uint32_t ve = c32[w.edge_src], ref1 = c32[30];
-      uint32_t* l32 = (uint32_t*)&w.sh->left;
-      if (lane < 45) l32[lane] = v;
-      uint32_t* e32 = (uint32_t*)&w.ring[w.mb_x];
       const uint32_t ev = lane == 8 ? (ve >> 16) | (ref1 & 0xffff0000u) : lane == 9 ? ve >> 16 : ve;
-      if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff007fu) : ev;   // dword 0: flags, pad, cbp
-      w.lf = w.cf;
+      if (!w.mbaff) {
+        uint32_t* l32 = (uint32_t*)&w.sh->left;
+        if (lane < 45) l32[lane] = v;
+        uint32_t* e32 = (uint32_t*)&w.ring[w.mb_x];
+        if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
+        w.lf = w.cf;
+      } else {   // the pair edge of this macroblock; the pair's records move left after its bottom
+        const int bot = (w.pst & Walker<MODE, RM>::PST_BOT) != 0;
+        uint32_t* e32 = (uint32_t*)&w.pair_edge(bot)[w.mb_x];
+        if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;
+        uint32_t* pr = (uint32_t*)w.pair_rec();
+        const uint32_t t = pr[lane < 45 ? lane : 44];
+        if (!bot) {
+          if (lane < 45) pr[lane] = lane == 0 ? w.cf : v;
+        } else if (lane < 45) {
+          pr[45 + lane] = t;
+          pr[90 + lane] = lane == 0 ? w.cf : v;
+        }
+      }
       if (RM) {   // MbRec dwords 32-44 are the 52 model bytes
         uint32_t* f32 = (uint32_t*)(w.frames + w.cur_off + ((int64_t)w.my * w.W + w.mb_x) * 52);
         if (lane >= 32 && lane < 45) f32[lane - 32] = v;
@@ -1616,11 +1843,21 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
       w.publish();
       if (!RM) w.update_prio();
     }
-    const int eos = w.terminate(SE_EOS);
+    // MBAFF: end_of_slice_flag follows the bottom macroblock of a pair only (7.3.4)
+    const int eos = (!w.mbaff || (w.pst & Walker<MODE, RM>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
     SPROF_ENDW(7, ps7);
     if (eos) break;
     if (Walker<MODE, RM>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
     addr++;
+    if (w.mbaff && !(w.pst & Walker<MODE, RM>::PST_BOT)) {
+      w.pst |= Walker<MODE, RM>::PST_BOT;
+      w.my++;
+      continue;
+    }
+    if (w.mbaff) {
+      w.pst = 0;
+      w.my--;
+    }
     if (++w.mb_x == w.W) {
       w.mb_x = 0;
       w.mb_y++;
@@ -2076,6 +2313,7 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   w.gsink = nullptr;
   w.gcount = 0;
   w.est_g = est_scratch + (size_t)s * kEstGlobal;
+  w.ring_cols = flags >> kFlagRingShift;
   if (!d->coded) {
     if (threadIdx.x == 0) {
       res[s].out_len = 0;
@@ -2137,6 +2375,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
   w.G = G;
   w.est_g = est_g;
   w.frames = frames;
+  w.ring_cols = flags >> kFlagRingShift;
   // fresh global model
   {
     uint4* e4 = (uint4*)est_g;

@@ -129,7 +129,10 @@ typedef struct {
  * Compress: payload bytes -> re-coded bytes.  For each slice the kernel also checks that a
  * CABAC re-encode plus the decompressor's last-byte rule (recode.cpp:1345-1356, 1503-1505)
  * restores the payload, and reports status < 0 otherwise. */
-/* max_mb_width / max_mb_height bound every slice's picture size (LDS ring and frame sizing). */
+/* max_mb_width / max_mb_height bound every slice's picture size (LDS ring and frame sizing).
+ * max_mb_width is the LDS ring's width in macroblock records: mb_width, or 3 * mb_width + 7 for an
+ * AVR_STRUCT_MBAFF slice (its pair records live there too) -- the value avr_parse_stream reports.
+ * An MBAFF slice launched with less fails alone (status < 0). */
 int avr_compress_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, int n, int max_mb_width, int max_mb_height,
                         const uint8_t* d_in, uint8_t* d_out, avr_slice_result* d_res, int model, void* stream);
 /* Decompress: re-coded bytes (at payload_offset/payload_size = recoded stream) -> regenerated

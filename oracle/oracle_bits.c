@@ -332,7 +332,7 @@ int avr_parse_slice_header(const avr_param_sets_t *ps, const uint8_t *rbsp, size
   h->mb_height = sps->mb_height;
   /* macroblocks in this picture: a field has half the frame's rows */
   int pic_mbs = sps->mb_width * (h->field_pic ? sps->mb_height / 2 : sps->mb_height);
-  h->supported = pps->entropy_coding_mode && !h->mbaff && !sps->separate_colour_plane &&
+  h->supported = pps->entropy_coding_mode && !sps->separate_colour_plane &&
                  h->slice_type != AVR_SLICE_SP && h->slice_type != AVR_SLICE_SI &&
                  (h->cabac_init_idc <= 2) && h->first_mb < pic_mbs &&
                  h->num_ref_idx_active[0] <= 32 && h->num_ref_idx_active[1] <= 32;

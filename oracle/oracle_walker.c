@@ -13,7 +13,7 @@
  *   significant_coeff_flag and end_coding_type(SIG_MAP) right after the map.
  * frame_spec is called once per slice with a decode-order picture counter.
  *
- * Supported: progressive frames and field pictures (no MBAFF yet), CABAC, ChromaArrayType 0..3,
+ * Supported: progressive frames, field pictures and MBAFF frames, CABAC, ChromaArrayType 0..3,
  * 8x8 transform, I/P/B slices.  I_PCM returns an error (the reference throws, recode.cpp:161-163).
  */
 #include <stdio.h>
@@ -27,7 +27,7 @@ int avr_walk_se, avr_walk_se_bin, avr_walk_se_limit, avr_walk_mbs_done, avr_walk
 enum {
   SE_SKIP = 1, SE_MBTYPE, SE_SUBMBTYPE, SE_T8X8, SE_PREVINTRA, SE_REMINTRA, SE_CHROMAPRED, SE_REF,
   SE_MVD_PREFIX, SE_MVD_SUFFIX, SE_CBP, SE_QPDELTA, SE_CBF, SE_SIG, SE_LAST, SE_LEVEL_PREFIX,
-  SE_LEVEL_SUFFIX, SE_SIGN, SE_EOS, SE_PCM_FLAG
+  SE_LEVEL_SUFFIX, SE_SIGN, SE_EOS, SE_PCM_FLAG, SE_FIELD
 };
 
 /* scan8 (recode.cpp:263-277 == FFmpeg h264dec.h scan8) */
@@ -69,6 +69,7 @@ static const uint8_t last8x8[63] = {
 
 typedef struct {
   uint8_t decoded, skip, intra, i16, direct16, t8x8, chroma_pred;
+  uint8_t fld;             /* field macroblock (field picture, or a field pair of an MBAFF frame) */
   uint16_t cbp;            /* FFmpeg cbp_table: luma b0-3, chroma b4-5, chroma DC cbf b6-7, luma DC cbf b8-10 */
   uint8_t nnz[3][16];      /* coefficient count per 4x4 block, raster x4 + 4*y4 per plane */
   uint8_t mvd[2][16][2];   /* min(|mvd|,70) per list, raster 4x4, component */
@@ -87,7 +88,65 @@ typedef struct {
   int is_b;
   int err;
   int fld;           /* the current macroblock is field coded (field picture, or an MBAFF field pair) */
+  /* MBAFF (FFmpeg FRAME_MBAFF): mbs is indexed by frame macroblock (x + frame row * W), pairs of
+   * a top and a bottom macroblock; neighbours follow ITU-T H.264 Table 6-4 (6.4.12.2) */
+  int mbaff, x, pr, bottom;
+  wmb_t *lpair, *apair;   /* top macroblocks of the left / upper pair when in the slice, else NULL */
 } walker_t;
+
+/* ---------------------------------------------------------------- neighbours (6.4.11, 6.4.12) */
+/* The macroblock holding the left neighbour of row yN (luma or chroma samples, maxH rows) of the
+ * current macroblock, and that row (*yM) in it: mbAddrA of Table 6-4 for xN < 0.  Progressive
+ * and field pictures: the macroblock to the left, same row. */
+static wmb_t *nb_left(walker_t *w, int yN, int maxH, int *yM) {
+  *yM = yN;
+  if (!w->mbaff) return w->left;
+  if (!w->lpair) return NULL;
+  wmb_t *T = w->lpair, *B = w->lpair + w->W;
+  const int afrm = !T->fld;
+  if (!w->cur->fld) {   /* frame macroblock */
+    if (afrm) return w->bottom ? B : T;
+    *yM = w->bottom ? (yN + maxH) >> 1 : yN >> 1;
+    return (yN & 1) ? B : T;
+  }
+  if (afrm) {           /* field macroblock, frame pair to the left */
+    const int y2 = (yN << 1) + w->bottom;
+    if (yN < maxH / 2) { *yM = y2; return T; }
+    *yM = y2 - maxH;
+    return B;
+  }
+  return w->bottom ? B : T;
+}
+/* mbAddrB of Table 6-4 (yN < 0): the macroblock above; its bottom row is the neighbour row */
+static wmb_t *nb_above(walker_t *w) {
+  if (!w->mbaff) return w->top;
+  if (!w->cur->fld) {
+    if (w->bottom) return w->cur - w->W;   /* the top macroblock of this pair */
+    return w->apair ? w->apair + w->W : NULL;
+  }
+  if (!w->apair) return NULL;
+  if (w->bottom) return w->apair + w->W;
+  return w->apair->fld ? w->apair : w->apair + w->W;
+}
+/* the macroblock neighbours A / B of 6.4.11.1 (luma locations (-1, 0) and (0, -1)) */
+static wmb_t *mb_a(walker_t *w) {
+  int yM;
+  return nb_left(w, 0, 16, &yM);
+}
+/* A neighbour's ref_idx / vertical |mvd| as seen from the current macroblock (FFmpeg
+ * fill_decode_caches MAP_F2F: a frame neighbour of a field macroblock counts double references
+ * and half the vertical motion, a field neighbour of a frame macroblock the opposite;
+ * 9.3.3.1.1.6-7) */
+static int nb_ref(const walker_t *w, const wmb_t *m, int list, int b8) {
+  int r = m->ref[list][b8];
+  if (w->mbaff && r >= 0 && m->fld != w->cur->fld) r = w->cur->fld ? r * 2 : r >> 1;
+  return r;
+}
+static int nb_mvd(const walker_t *w, const wmb_t *m, int list, int idx, int comp) {
+  int v = m->mvd[list][idx][comp];
+  if (w->mbaff && comp == 1 && m->fld != w->cur->fld) v = w->cur->fld ? v >> 1 : v << 1;
+  return v;
+}
 
 static inline int bin(walker_t *w, int se, int k, int ctx) {
   avr_walk_se = se;
@@ -121,8 +180,9 @@ static int intra_mb_type(walker_t *w, int base, int intra_slice, mbtype_t *t) {
   t->intra = 1;
   int ctx = 0;
   if (intra_slice) {
-    if (w->left && w->left->i16) ctx++;  /* condTerm: available && mb_type != I_NxN */
-    if (w->top && w->top->i16) ctx++;
+    const wmb_t *a = mb_a(w), *b = nb_above(w);
+    if (a && a->i16) ctx++;  /* condTerm: available && mb_type != I_NxN */
+    if (b && b->i16) ctx++;
     if (!bin(w, SE_MBTYPE, 0, base + ctx)) return 0; /* I_NxN */
     base += 2;
   } else {
@@ -165,8 +225,9 @@ static void decode_mb_type(walker_t *w, mbtype_t *t) {
   }
   /* B */
   int ctx = 0;
-  if (w->left && !w->left->direct16) ctx++;  /* condTerm: available && not B_Skip/B_Direct_16x16 */
-  if (w->top && !w->top->direct16) ctx++;
+  const wmb_t *a = mb_a(w), *b = nb_above(w);
+  if (a && !a->direct16) ctx++;  /* condTerm: available && not B_Skip/B_Direct_16x16 */
+  if (b && !b->direct16) ctx++;
   if (!bin(w, SE_MBTYPE, 0, 27 + ctx)) { t->direct16 = 1; t->nparts = 4; return; }
   if (!bin(w, SE_MBTYPE, 1, 27 + 3)) {
     t->nparts = 1;
@@ -234,23 +295,25 @@ static void decode_sub_mb_type(walker_t *w, submb_t *s) {
 /* ------------------------------------------------------------------------ ref / mvd */
 static int ref_neighbor_gt0(walker_t *w, int list, int x4, int y4, int left) {
   const wmb_t *m;
-  int b8;
+  int b8, yM;
   if (left) {
     if (x4 > 0) { m = w->cur; b8 = (y4 >> 1) * 2 + ((x4 - 1) >> 1); }
-    else { m = w->left; b8 = (y4 >> 1) * 2 + 1; }
+    else { m = nb_left(w, 4 * y4, 16, &yM); b8 = (yM >> 3) * 2 + 1; }
   } else {
     if (y4 > 0) { m = w->cur; b8 = ((y4 - 1) >> 1) * 2 + (x4 >> 1); }
-    else { m = w->top; b8 = 2 + (x4 >> 1); }
+    else { m = nb_above(w); b8 = 2 + (x4 >> 1); }
   }
   if (!m) return 0;
   if (w->is_b && m->direct8[b8]) return 0;
-  return m->ref[list][b8] > 0;
+  return nb_ref(w, m, list, b8) > 0;
 }
 
 static int decode_ref(walker_t *w, int list, int x4, int y4) {
   int ctx = ref_neighbor_gt0(w, list, x4, y4, 1) + 2 * ref_neighbor_gt0(w, list, x4, y4, 0);
   int ref = 0;
-  avr_walk_se_limit = w->h->num_ref_idx_active[list] - 1;
+  /* an MBAFF field macroblock addresses each reference field: twice the references (FFmpeg
+   * ref_count << MB_MBAFF) */
+  avr_walk_se_limit = (w->h->num_ref_idx_active[list] << (w->mbaff && w->cur->fld)) - 1;
   while (bin(w, SE_REF, ref, 54 + ctx)) {
     ref++;
     ctx = (ctx >> 2) + 4;
@@ -262,10 +325,13 @@ static int decode_ref(walker_t *w, int list, int x4, int y4) {
 static int mvd_neighbor(walker_t *w, int list, int comp, int x4, int y4, int left) {
   if (left) {
     if (x4 > 0) return w->cur->mvd[list][y4 * 4 + x4 - 1][comp];
-    return w->left ? w->left->mvd[list][y4 * 4 + 3][comp] : 0;
+    int yM;
+    const wmb_t *m = nb_left(w, 4 * y4, 16, &yM);
+    return m ? nb_mvd(w, m, list, (yM >> 2) * 4 + 3, comp) : 0;
   }
   if (y4 > 0) return w->cur->mvd[list][(y4 - 1) * 4 + x4][comp];
-  return w->top ? w->top->mvd[list][12 + x4][comp] : 0;
+  const wmb_t *m = nb_above(w);
+  return m ? nb_mvd(w, m, list, 12 + x4, comp) : 0;
 }
 
 /* decode_cabac_mb_mvd: ctxIdxOffset 40 (x) / 47 (y); returns |mvd| clipped to 70 */
@@ -315,19 +381,30 @@ static int nnz_at(walker_t *w, int p, int pw, int ph, int x4, int y4, int left) 
   int v;
   if (left) {
     if (x4 > 0) return w->cur->nnz[p][y4 * 4 + x4 - 1];
-    if (!w->left) return w->cur->intra ? 64 : 0;
-    if (nnz_444_8x8_override(w, w->left, &v)) return v;
-    return w->left->nnz[p][y4 * 4 + pw - 1];
+    int yM;   /* rows of 4x4 blocks: 4 y4 samples of a plane 4 ph high */
+    const wmb_t *m = nb_left(w, 4 * y4, 4 * ph, &yM);
+    if (!m) return w->cur->intra ? 64 : 0;
+    if (nnz_444_8x8_override(w, m, &v)) return v;
+    return m->nnz[p][(yM >> 2) * 4 + pw - 1];
   }
   if (y4 > 0) return w->cur->nnz[p][(y4 - 1) * 4 + x4];
-  if (!w->top) return w->cur->intra ? 64 : 0;
-  if (nnz_444_8x8_override(w, w->top, &v)) return v;
-  return w->top->nnz[p][(ph - 1) * 4 + x4];
+  const wmb_t *m = nb_above(w);
+  if (!m) return w->cur->intra ? 64 : 0;
+  if (nnz_444_8x8_override(w, m, &v)) return v;
+  return m->nnz[p][(ph - 1) * 4 + x4];
 }
 
 static uint16_t nb_cbp(walker_t *w, const wmb_t *m) {
   if (m) return m->cbp;
   return w->cur->intra ? 0x7CF : 0x00F;
+}
+/* the left neighbours' coded_block_pattern as FFmpeg's left_cbp: chroma and DC bits of A, luma
+ * bit 1 from the 8x8 block left of the current 8x8 block 0, bit 3 left of block 2 (6.4.11.2) */
+static uint16_t nb_cbp_left(walker_t *w) {
+  int y0, y2;
+  const wmb_t *m0 = nb_left(w, 0, 16, &y0), *m2 = nb_left(w, 8, 16, &y2);
+  const uint16_t c0 = nb_cbp(w, m0), c2 = nb_cbp(w, m2);
+  return (uint16_t)((c0 & 0x7F0) | (((c0 >> ((y0 >> 3) * 2 + 1)) & 1) << 1) | (((c2 >> ((y2 >> 3) * 2 + 1)) & 1) << 3));
 }
 
 /* one residual_block_cabac(); n = FFmpeg block index (scan8 index), p/x4/y4 its position */
@@ -341,8 +418,8 @@ static void residual_block(walker_t *w, int cat, int n, int max, int is_dc, int 
     int nza, nzb;
     if (is_dc) {
       int bit = cat == 3 ? (0x40 << (n - 49)) : (0x100 << (n - 48));
-      nza = (nb_cbp(w, w->left) & bit) != 0;
-      nzb = (nb_cbp(w, w->top) & bit) != 0;
+      nza = (nb_cbp(w, mb_a(w)) & bit) != 0;
+      nzb = (nb_cbp(w, nb_above(w)) & bit) != 0;
     } else {
       nza = nnz_at(w, p, pw, ph, x4, y4, 1) > 0;
       nzb = nnz_at(w, p, pw, ph, x4, y4, 0) > 0;
@@ -465,24 +542,105 @@ static void residual(walker_t *w, const mbtype_t *t, int cbp) {
 }
 
 /* ------------------------------------------------------------------------ macroblock */
+/* a skipped macroblock (P_Skip / B_Skip) */
+static void mb_skipped(walker_t *w) {
+  wmb_t *cur = w->cur;
+  cur->skip = 1;
+  if (w->is_b) {
+    cur->direct16 = 1;
+    memset(cur->direct8, 1, 4);
+  } else {
+    memset(cur->ref[0], 0, 4);
+  }
+  w->last_dqp_nz = 0;
+}
+
+static void decode_mb_layer(walker_t *w);
 static void decode_mb(walker_t *w) {
   const avr_slice_hdr_t *h = w->h;
-  wmb_t *cur = w->cur;
-  memset(cur->ref, -1, sizeof(cur->ref));
+  memset(w->cur->ref, -1, sizeof(w->cur->ref));
   if (h->slice_type != AVR_SLICE_I) {
     int ctx = (w->left && !w->left->skip) + (w->top && !w->top->skip);
     if (bin(w, SE_SKIP, 0, (w->is_b ? 24 : 11) + ctx)) {
-      cur->skip = 1;
-      if (w->is_b) {
-        cur->direct16 = 1;
-        memset(cur->direct8, 1, 4);
-      } else {
-        memset(cur->ref[0], 0, 4);
-      }
-      w->last_dqp_nz = 0;
+      mb_skipped(w);
       return;
     }
   }
+  decode_mb_layer(w);
+}
+
+/* MBAFF (FFmpeg h264_cabac.c decode_cabac_mb_skip): mb_skip_flag's neighbours A / B of the top
+ * (bottom = 0) or bottom macroblock of the current pair when the pair is field (fld) or frame
+ * coded -- fld may still be the inferred value (7.4.4) */
+static int skip_ctx_mbaff(walker_t *w, int bottom, int fld) {
+  const wmb_t *a = NULL, *b = NULL;
+  const wmb_t *T = w->mbs + w->x + 2 * w->pr * w->W;
+  if (w->lpair) a = (bottom && fld == w->lpair->fld) ? w->lpair + w->W : w->lpair;
+  if (fld) {
+    if (w->apair) b = (!bottom && w->apair->fld) ? w->apair : w->apair + w->W;
+  } else {
+    b = bottom ? T : (w->apair ? w->apair + w->W : NULL);
+  }
+  return (w->is_b ? 24 : 11) + (a && !a->skip) + (b && !b->skip);
+}
+/* mb_field_decoding_flag (FFmpeg decode_cabac_field_decoding_flag): ctxIdx 70 + left pair
+ * field (the inferred flag, which is the left pair's within a row) + upper pair field */
+static int field_flag(walker_t *w, int inferred) {
+  return bin(w, SE_FIELD, 0, 70 + (w->x > 0 && inferred) + (w->apair && w->apair->fld));
+}
+
+/* one macroblock pair of an MBAFF frame, FFmpeg's order: top skip; a skipped top takes the bottom's
+ * skip flag next and, if the bottom is coded, the pair's field flag; a coded top reads the field
+ * flag after its skip flag; the bottom of a pair whose top was coded reads none */
+static void decode_pair_mbaff(walker_t *w, int *mbs_done) {
+  const avr_slice_hdr_t *h = w->h;
+  const avr_hooks_t *hooks = w->hk;
+  wmb_t *T = w->mbs + w->x + 2 * w->pr * w->W;
+  /* inference (7.4.4): the left pair's flag, else the upper pair's, else frame */
+  int fld = w->lpair ? w->lpair->fld : w->apair ? w->apair->fld : 0;
+  int skip_top = 0, skip_bottom = 0;
+  for (int bottom = 0; bottom < 2 && !w->err; bottom++) {
+    wmb_t *cur = T + bottom * w->W;
+    w->cur = cur;
+    w->bottom = bottom;
+    memset(cur->ref, -1, sizeof(cur->ref));
+    hooks->mb_xy(hooks->opaque, w->x, 2 * w->pr + bottom);
+    cur->fld = (uint8_t)fld;
+    w->fld = fld;
+    if (h->slice_type != AVR_SLICE_I) {
+      int skip;
+      if (bottom && skip_top) skip = skip_bottom;
+      else skip = bin(w, SE_SKIP, 0, skip_ctx_mbaff(w, bottom, fld));
+      if (skip) {
+        if (!bottom) {
+          skip_top = 1;
+          cur->skip = 1;
+          skip_bottom = bin(w, SE_SKIP, 0, skip_ctx_mbaff(w, 1, fld));
+          if (!skip_bottom) fld = field_flag(w, fld);
+          cur->fld = (uint8_t)fld;
+          w->fld = fld;
+        }
+        mb_skipped(w);
+        cur->decoded = 1;
+        (*mbs_done)++;
+        continue;
+      }
+    }
+    if (!bottom) {
+      fld = field_flag(w, fld);
+      cur->fld = (uint8_t)fld;
+      w->fld = fld;
+    }
+    decode_mb_layer(w);
+    if (w->err) return;
+    cur->decoded = 1;
+    (*mbs_done)++;
+  }
+}
+
+static void decode_mb_layer(walker_t *w) {
+  const avr_slice_hdr_t *h = w->h;
+  wmb_t *cur = w->cur;
   mbtype_t t;
   decode_mb_type(w, &t);
   if (w->err) return;
@@ -493,7 +651,7 @@ static void decode_mb(walker_t *w) {
     cur->intra = 1;
     cur->i16 = (uint8_t)t.i16;
     if (!t.i16) {
-      if (h->transform_8x8_mode) cur->t8x8 = (uint8_t)bin(w, SE_T8X8, 0, 399 + (w->left && w->left->t8x8) + (w->top && w->top->t8x8));
+      if (h->transform_8x8_mode) cur->t8x8 = (uint8_t)bin(w, SE_T8X8, 0, 399 + (mb_a(w) && mb_a(w)->t8x8) + (nb_above(w) && nb_above(w)->t8x8));
       int nmodes = cur->t8x8 ? 4 : 16;
       for (int i = 0; i < nmodes; i++) {
         if (!bin(w, SE_PREVINTRA, 0, 68)) {
@@ -504,7 +662,8 @@ static void decode_mb(walker_t *w) {
       }
     }
     if (h->chroma_array_type == 1 || h->chroma_array_type == 2) {
-      int ctx = (w->left && w->left->intra && w->left->chroma_pred) + (w->top && w->top->intra && w->top->chroma_pred);
+      const wmb_t *a = mb_a(w), *b = nb_above(w);
+      int ctx = (a && a->intra && a->chroma_pred) + (b && b->intra && b->chroma_pred);
       int mode = 0;
       if (bin(w, SE_CHROMAPRED, 0, 64 + ctx)) {
         mode = 1;
@@ -532,7 +691,7 @@ static void decode_mb(walker_t *w) {
       for (int list = 0; list < (w->is_b ? 2 : 1); list++) {
         for (int i = 0; i < 4; i++) {
           if (sub[i].direct || !(sub[i].pred & (1 << list))) continue;
-          int ref = h->num_ref_idx_active[list] > 1 ? decode_ref(w, list, 2 * (i & 1), 2 * (i >> 1)) : 0;
+          int ref = (h->num_ref_idx_active[list] << (w->mbaff && cur->fld)) > 1 ? decode_ref(w, list, 2 * (i & 1), 2 * (i >> 1)) : 0;
           cur->ref[list][i] = (int8_t)ref;
         }
       }
@@ -559,7 +718,7 @@ static void decode_mb(walker_t *w) {
       for (int i = 0; i < t.nparts; i++) {
         if (!(t.pred[i] & (1 << list))) continue;
         int px = t.nparts == 2 && t.vertical ? 2 * i : 0, py = t.nparts == 2 && !t.vertical ? 2 * i : 0;
-        int ref = h->num_ref_idx_active[list] > 1 ? decode_ref(w, list, px, py) : 0;
+        int ref = (h->num_ref_idx_active[list] << (w->mbaff && cur->fld)) > 1 ? decode_ref(w, list, px, py) : 0;
         if (t.nparts == 1) memset(cur->ref[list], ref, 4);
         else if (!t.vertical) { cur->ref[list][2 * i] = cur->ref[list][2 * i + 1] = (int8_t)ref; }
         else { cur->ref[list][i] = cur->ref[list][i + 2] = (int8_t)ref; }
@@ -583,7 +742,7 @@ static void decode_mb(walker_t *w) {
   if (t.i16) {
     cbp = t.i16_cbp;
   } else {
-    uint16_t ca = nb_cbp(w, w->left), cb = nb_cbp(w, w->top);
+    uint16_t ca = nb_cbp_left(w), cb = nb_cbp(w, nb_above(w));
     int c = 0;
     c |= bin(w, SE_CBP, 0, 73 + !(ca & 0x02) + 2 * !(cb & 0x04));
     c |= bin(w, SE_CBP, 1, 73 + !(c & 0x01) + 2 * !(cb & 0x08)) << 1;
@@ -600,7 +759,7 @@ static void decode_mb(walker_t *w) {
     cbp = c;
     if ((cbp & 15) && h->transform_8x8_mode && !t.intra && no_sub_lt8x8 &&
         (!cur->direct16 || h->direct_8x8_inference))
-      cur->t8x8 = (uint8_t)bin(w, SE_T8X8, 0, 399 + (w->left && w->left->t8x8) + (w->top && w->top->t8x8));
+      cur->t8x8 = (uint8_t)bin(w, SE_T8X8, 0, 399 + (mb_a(w) && mb_a(w)->t8x8) + (nb_above(w) && nb_above(w)->t8x8));
   }
   cur->cbp = (uint16_t)cbp;
   if ((cbp & 0x3f) || t.i16) {
@@ -627,7 +786,7 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
    * still see the frame (h->mb_height) and FFmpeg's frame row of each macroblock,
    * sl->mb_y = 2 * field row + bottom_field_flag (h264_slice.c, decode_slice) */
   w.H = h->field_pic ? h->mb_height / 2 : h->mb_height;
-  w.fld = h->field_pic;
+  w.fld = h->field_pic;   /* MBAFF: per pair */
   w.is_b = h->slice_type == AVR_SLICE_B;
   w.mbs = (wmb_t *)calloc((size_t)w.W * w.H, sizeof(wmb_t));
   if (!w.mbs) return -1;
@@ -636,7 +795,23 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
   int addr = h->first_mb;
   int ret = 0;
   avr_walk_mbs_done = 0;
-  for (;;) {
+  w.mbaff = h->mbaff;
+  /* MBAFF: first_mb is the top macroblock of the first pair (2 * first_mb_in_slice); macroblock
+   * pairs in raster order, the model hooks see FFmpeg's frame row 2 * pair row + bottom */
+  for (int pair = addr / 2; w.mbaff;) {
+    w.x = pair % w.W;
+    w.pr = pair / w.W;
+    if (2 * w.pr + 1 >= w.H) { ret = -7; break; }
+    wmb_t *T = w.mbs + w.x + 2 * w.pr * w.W;
+    w.lpair = w.x > 0 && T[-1].decoded ? T - 1 : NULL;
+    w.apair = w.pr > 0 && T[-2 * w.W].decoded ? T - 2 * w.W : NULL;
+    decode_pair_mbaff(&w, &avr_walk_mbs_done);
+    if (w.err) { ret = w.err; break; }
+    avr_walk_last_mb = 2 * (pair + 1) >= w.W * w.H;
+    if (term(&w, SE_EOS)) break;
+    pair++;
+  }
+  for (; !w.mbaff;) {
     if (addr >= w.W * w.H) { ret = -7; break; }
     int x = addr % w.W, y = addr / w.W;
     w.cur = &w.mbs[addr];

@@ -42,19 +42,21 @@ def test_reference_8x8_ordering_cannot_roundtrip(monkeypatch):
     assert r.returncode != 0
 
 
-FIELDS = json.loads((ROOT / "tests/golden/fields.json").read_text())
+FIELDS = json.loads((ROOT / "tests/golden/fields.json").read_text())["files"]
 
 
-def test_field_fixture_regenerates_and_roundtrips():
-    """Field pictures (PAFF, tests/golden/fields.json): every field slice parses to end_of_slice
-    and regenerates its payload (field ctxIdx offsets and 8x8 field map, oracle_walker.c), and
-    whole-file compress in both model modes round-trips to the pinned containers."""
+@pytest.mark.parametrize("g", FIELDS, ids=lambda g: g["file"])
+def test_field_fixture_regenerates_and_roundtrips(g):
+    """Field pictures (PAFF) and MBAFF frames (tests/golden/fields.json): every slice parses to
+    end_of_slice and regenerates its payload (field ctxIdx offsets, 8x8 field map, macroblock-pair
+    neighbours of Table 6-4, oracle_walker.c), and whole-file compress in both model modes
+    round-trips to the pinned containers."""
     _, cli = build_oracle()
-    f = FIX / FIELDS["file"]
+    f = FIX / g["file"]
     r = subprocess.run([str(cli), "slices", str(f)], capture_output=True, text=True)
-    assert r.returncode == 0 and f"slices ok {FIELDS['slices']} bad 0" in r.stdout, r.stdout[-2000:]
+    assert r.returncode == 0 and f"slices ok {g['slices']} bad 0" in r.stdout, r.stdout[-2000:]
     for mode in ("R", "P"):
         assert b"roundtrip succeeded" in oracle_cli("roundtrip", f, mode=mode)
         avrc = oracle_cli("compress", f, mode=mode)
-        assert len(avrc) == FIELDS[mode]["avrc_len"]
-        assert hashlib.sha256(avrc).hexdigest() == FIELDS[mode]["avrc_sha256"]
+        assert len(avrc) == g[mode]["avrc_len"]
+        assert hashlib.sha256(avrc).hexdigest() == g[mode]["avrc_sha256"]
