@@ -219,6 +219,12 @@ struct Plan {
   int n_files() const { return file_first.empty() ? 1 : (int)file_first.size() - 1; }
   int file_begin(int f) const { return file_first.empty() ? 0 : file_first[f]; }
   int file_end(int f) const { return file_first.empty() ? (int)descs.size() : file_first[f + 1]; }
+  // field pictures / MBAFF frames present: launches add the field-capable kernels (kFlagFields)
+  bool fields() const {
+    for (const auto& d : descs)
+      if (d.structure != AVR_STRUCT_FRAME) return true;
+    return false;
+  }
 };
 
 void append_aligned(std::vector<uint8_t>* arena, const uint8_t* p, size_t n, size_t extra, uint64_t* off) {
@@ -322,7 +328,7 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
   HIP_TRY(c, avr::launch_rscan(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, lds,
                                c->in.as<uint8_t>(), c->frames.as<uint8_t>(), c->rm_goff.as<int64_t>(),
                                c->rm_counts.as<uint32_t>(), nullptr, nullptr, c->res.as<avr_slice_result>(),
-                               c->rm_stop.as<int32_t>(), c->stream));
+                               c->rm_stop.as<int32_t>(), plan.fields(), c->stream));
   std::vector<uint32_t> counts(n);
   HIP_TRY(c, hipMemcpyAsync(counts.data(), c->rm_counts.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -349,7 +355,7 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
   HIP_TRY(c, avr::launch_rscan(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, lds,
                                c->in.as<uint8_t>(), c->frames.as<uint8_t>(), c->rm_goff.as<int64_t>(),
                                c->rm_counts.as<uint32_t>(), ops, c->rm_off.as<uint64_t>(),
-                               c->res.as<avr_slice_result>(), c->rm_stop.as<int32_t>(), c->stream));
+                               c->res.as<avr_slice_result>(), c->rm_stop.as<int32_t>(), plan.fields(), c->stream));
   HIP_TRY(c, avr::launch_rmode_estimators(ops, N, c->file_op_off.as<uint64_t>(), nf, keys, vals, skeys, svals, temp,
                                           tb, rops, c->stream));
   HIP_TRY(c, avr::launch_rcode(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, rops,
@@ -368,6 +374,7 @@ constexpr int32_t kStatusNoRoundtrip = -20;
 int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_slice_result>* res,
              std::vector<uint8_t>* out_host, bool verify = false, uint32_t flags = 0) {
   const int n = (int)plan.descs.size();
+  if (plan.fields()) flags |= avr::kFlagFields;
   res->assign(n, avr_slice_result{0, 0, 0, 0, {0, 0, 0, 0, 0, 0}});
   uint64_t out_total = 0;
   for (auto& d : plan.descs) {
@@ -438,7 +445,8 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
       const int m = std::min(chunk, n - s0);
       HIP_TRY(c, avr::launch_slices(1, false, c->tables.as<avr::EngineTables>(), dd + s0, m, plan.max_w,
                                     c->out.as<uint8_t>(), c->regen.as<uint8_t>(), rd + s0, c->est.as<uint16_t>(),
-                                    nullptr, nullptr, c->order_or_null(), c->stream));
+                                    nullptr, nullptr, c->order_or_null(), c->stream, avr::SeqFiles(),
+                                    plan.fields() ? avr::kFlagFields : 0u));
     }
     HIP_TRY(c, avr::launch_verify(c->descs.as<avr_slice_desc>(), c->res.as<avr_slice_result>(), rd, n,
                                   c->in.as<uint8_t>(), c->regen.as<uint8_t>(), c->verdict.as<int32_t>(), c->stream));
@@ -1001,7 +1009,8 @@ static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int 
     HIP_TRY(c, c->frames.reserve((size_t)2 * max_w * max_h * 52 + 64));
     HIP_TRY(c, c->frame_meta.reserve(64));
     HIP_TRY(c, avr::launch_slices(mode, true, c->tables.as<avr::EngineTables>(), d_desc, n, max_w, d_in, d_out, d_res,
-                                  c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), nullptr, s));
+                                  c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), nullptr, s,
+                                  avr::SeqFiles(), avr::kFlagFields));
     return AVR_OK;
   }
   const int chunk = std::max(1, std::min(n, kMaxSlicesPerLaunch));
@@ -1010,7 +1019,8 @@ static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int 
   for (int s0 = 0; s0 < n; s0 += chunk) {
     const int m = std::min(chunk, n - s0);
     HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), d_desc + s0, m, max_w, d_in, d_out,
-                                  d_res + s0, c->est.as<uint16_t>(), nullptr, nullptr, c->order_or_null(), s));
+                                  d_res + s0, c->est.as<uint16_t>(), nullptr, nullptr, c->order_or_null(), s,
+                                  avr::SeqFiles(), avr::kFlagFields));
   }
   return AVR_OK;
 }

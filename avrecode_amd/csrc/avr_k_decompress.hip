@@ -8,7 +8,14 @@ hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_des
   // the per-CU priority board of this kernel starts empty on every launch (cu_cell's slot counter
   // must not carry a previous launch's residue)
   if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
-  hipLaunchKernelGGL(slices_parallel_kernel<MODE_DECOMPRESS>, dim3(n), dim3(slice_threads<MODE_DECOMPRESS>()), lds, stream, T, descs, n, in, out, res, est, order, flags);
+  hipLaunchKernelGGL((slices_parallel_kernel<MODE_DECOMPRESS, false>), dim3(n), dim3(slice_threads<MODE_DECOMPRESS>()), lds, stream, T, descs, n, in, out, res, est, order, flags);
+  // field pictures / MBAFF frames: a second launch over the batch (its workgroups for progressive
+  // slices return at once)
+  if (flags & kFlagFields) {
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
+    hipLaunchKernelGGL((slices_parallel_kernel<MODE_DECOMPRESS, true>), dim3(n), dim3(slice_threads<MODE_DECOMPRESS>()), lds, stream, T, descs, n, in, out, res, est, order, flags);
+  }
   return hipGetLastError();
 }
 

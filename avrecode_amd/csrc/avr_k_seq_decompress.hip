@@ -7,7 +7,11 @@ hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_d
                     uint8_t* out, avr_slice_result* res, uint16_t* est, uint8_t* frames, int* frame_meta,
                     const int* file_first, int n_files, uint64_t frame_stride, uint32_t flags,
                     hipStream_t stream) {
-  hipLaunchKernelGGL(slices_sequential_kernel<MODE_DECOMPRESS>, dim3(n_files), dim3(slice_threads<MODE_DECOMPRESS>()), lds, stream, T, descs, n, in, out, res, est,
+  if (flags & kFlagFields)
+    hipLaunchKernelGGL((slices_sequential_kernel<MODE_DECOMPRESS, true>), dim3(n_files), dim3(slice_threads<MODE_DECOMPRESS>()), lds, stream, T, descs, n, in, out, res, est,
+                     frames, frame_meta, file_first, frame_stride, flags);
+  else
+    hipLaunchKernelGGL((slices_sequential_kernel<MODE_DECOMPRESS, false>), dim3(n_files), dim3(slice_threads<MODE_DECOMPRESS>()), lds, stream, T, descs, n, in, out, res, est,
                      frames, frame_meta, file_first, frame_stride, flags);
   return hipGetLastError();
 }

@@ -25,6 +25,9 @@ constexpr uint32_t kFlagBill = 1;   // launch flag: the coders bill per CodingTy
 // launch flags bits 16-31: EdgeRec slots of the LDS ring (max_mb_width of shared_bytes), set by
 // launch_slices; an MBAFF slice needs 3 mb_width + 7 (Walker::pair_edge)
 constexpr int kFlagRingShift = 16;
+// launch flag: the batch may hold field pictures / MBAFF frames -- the parallel launches add a
+// launch of the field-capable kernel for them, the sequential ones use it for every file
+constexpr uint32_t kFlagFields = 2;
 size_t shared_bytes(int max_mb_width);
 // does workgroup b of a 4G-workgroup launch land on CU group b mod G (schedule_kernel's assumption)?
 hipError_t probe_round_robin(size_t lds, bool* ok);
@@ -67,7 +70,7 @@ hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_d
 // estimator chains over the op stream, per-slice coder
 hipError_t launch_rscan(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
                         uint8_t* frames, const int64_t* goff, uint32_t* counts, uint32_t* ops,
-                        const uint64_t* op_off, avr_slice_result* res, int32_t* stop_ok, hipStream_t stream);
+                        const uint64_t* op_off, avr_slice_result* res, int32_t* stop_ok, bool fields, hipStream_t stream);
 // Several files in one pass (a corpus): file f's ops are [file_op_off[f], file_op_off[f + 1]) (device,
 // n_files + 1 entries; ignored for one file), each file with estimators of its own.
 size_t rmode_sort_temp_bytes(uint64_t N, int n_files);

@@ -461,7 +461,10 @@ AVR_FI void est_table_reset(uint16_t* est_g, Shared* sh) {
   __syncthreads();
 }
 
-template <int MODE, bool RM>
+// FLD: field-coded slices (PAFF, MBAFF) -- a second instantiation (kernels of their own, launched
+// only when a batch may hold such slices: kFlagFields), so that the progressive walker carries no
+// field tests in its per-bin and per-macroblock code
+template <int MODE, bool RM, bool FLD = false>
 struct Walker {
   static constexpr bool DEC = MODE == MODE_COMPRESS || MODE == MODE_TRACE;  // CABAC decoding side
   const HotTables* T;     // LDS copy
@@ -494,6 +497,7 @@ struct Walker {
   // so the other field's rows -- already in the frame buffer, which that kernel fills before it
   // reads -- must read as the zeros the sequential model still sees there
   int top_pending;
+  AVR_FI int mrow() const { return FLD ? my : mb_y; }   // the model's row (progressive: the parse row)
   // MBAFF frame (AVR_STRUCT_MBAFF): macroblock pairs; pst = the pair's state (PST_*); ring_cols =
   // EdgeRec slots the launch gave the LDS ring (an MBAFF slice needs 3 W + 7, see pair_edge)
   int mbaff;
@@ -545,6 +549,11 @@ struct Walker {
     // offsets, transform_size_8x8_flag (ctxIdx 399-400 = chroma AC's last lanes 30-31), which
     // bin() updates in LDS while the category stays loaded across macroblocks.
     const bool c8 = cat == 5 || cat == 9 || cat == 13;
+    if (!FLD) {   // frame offsets: only the 8x8 categories' lanes alias (within the category)
+      if (c8 && (j == 15 || (j >= 25 && j < 32))) return -1;
+      return j < 16 ? T->sig_base[cat] + (int)j : j < 32 ? T->last_base[cat] + (int)j - 16
+           : j < 42 ? T->abs_base[cat] + (int)j - 32 : j < 46 ? T->cbf_base[cat] + (int)j - 42 : -1;
+    }
     const int ns = c8 ? 15 : cat == 3 ? 3 : (cat == 1 || cat == 4 || cat == 7 || cat == 11) ? 14 : 15;
     const int nl = c8 ? 9 : ns;
     if (j < 16) return (int)j < ns ? T->sig_base[cat] + (int)j : -1;
@@ -663,7 +672,7 @@ struct Walker {
     else if (L < 32) t->last_base[L - 16] = f ? G->last_base_fld[L - 16] : G->hot.last_base[L - 16];
     const uint32_t fr = T->sig8x8[L];
     const uint32_t cm = f ? (uint32_t)G->sig8x8_fld[L] : fr;
-    sig8_v = MODE == MODE_DECOMPRESS ? (cm | fr << 8) : cm;
+    sig8_v = (MODE == MODE_DECOMPRESS && FLD) ? (cm | fr << 8) : cm;
     wave_sync();
   }
 
@@ -813,7 +822,7 @@ struct Walker {
     int v;
     // MBAFF: rows of one left macroblock come from both macroblocks of the left pair; the view's
     // flags byte holds each row's source 8x8-transform flag
-    if (nnz_override(mbaff ? (((uint32_t)sh->left.flags >> y4) & 1u) * (uint32_t)F_T8 : lf, &v)) return v;
+    if (nnz_override((FLD && mbaff) ? (((uint32_t)sh->left.flags >> y4) & 1u) * (uint32_t)F_T8 : lf, &v)) return v;
     return sh->left.nnz[p][y4 * 4 + pw - 1];
   }
   AVR_FI int nnz_top(int p, int x4, int y4) const {
@@ -1017,17 +1026,17 @@ struct Walker {
   // ------------------------------------------------------------------ model neighbours
   // model num_nonzeros of a neighbouring macroblock (get_neighbor_sub_mb, recode.cpp:419-471)
   AVR_FI int mnnz_left(int idx) const {
-    if (RM) return frames[cur_off + ((int64_t)my * W + mb_x - 1) * 52 + idx];
+    if (RM) return frames[cur_off + ((int64_t)mrow() * W + mb_x - 1) * 52 + idx];
     return left_ok ? sh->left.mnnz[idx] : 0;
   }
   AVR_FI int mnnz_top(int idx) const {
-    if (RM) return top_pending ? 0 : frames[cur_off + ((int64_t)(my - 1) * W + mb_x) * 52 + idx];
+    if (RM) return (FLD && top_pending) ? 0 : frames[cur_off + ((int64_t)(mrow() - 1) * W + mb_x) * 52 + idx];
     // fresh model per slice: in a field picture the model's upper row belongs to the other field
-    if (fld_pic) return 0;
-    return (top_ok | mbaff) ? ring[mb_x].mnnz[idx] : 0;   // MBAFF: the view holds the model's upper macroblock
+    if (FLD && fld_pic) return 0;
+    return (top_ok | (FLD && mbaff)) ? ring[mb_x].mnnz[idx] : 0;   // MBAFF: the view holds the model's upper macroblock
   }
   AVR_FI int mnnz_prev(int idx) const {
-    if (RM) return prev_off < 0 ? 0 : frames[prev_off + ((int64_t)my * W + mb_x) * 52 + idx];
+    if (RM) return prev_off < 0 ? 0 : frames[prev_off + ((int64_t)mrow() * W + mb_x) * 52 + idx];
     return 0;
   }
 
@@ -1037,7 +1046,7 @@ struct Walker {
     int has_left, has_above, lv = 0, av = 0;
     if (n >= 48) {
       has_left = mb_x > 0;
-      has_above = my > 0;
+      has_above = mrow() > 0;
       if (has_left) lv = mnnz_left(n);
       if (has_above) av = mnnz_top(n);
     } else {
@@ -1045,7 +1054,7 @@ struct Walker {
       int li = L & 63, ui = U & 63;
       if (max >= 32) { li &= ~3; ui &= ~3; }
       has_left = !(L & 128) || mb_x > 0;
-      has_above = !(U & 128) || my > 0;
+      has_above = !(U & 128) || mrow() > 0;
       if (has_left) lv = (L & 128) ? mnnz_left(li) : sh->cur.mnnz[li];
       if (has_above) av = (U & 128) ? mnnz_top(ui) : sh->cur.mnnz[ui];
     }
@@ -1172,9 +1181,9 @@ struct Walker {
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc, zk = 0;
         if (max == 64) {
-          const uint32_t v = __builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);   // CABAC inc | key inc << 8
-          sc = (int)(v & 0xff);
-          zk = (int)(v >> 8);
+          const uint32_t v = __builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);   // CABAC inc | key inc << 8 (FLD)
+          sc = FLD ? (int)(v & 0xff) : (int)v;
+          zk = FLD ? (int)(v >> 8) : (int)v;
           lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
         }
         else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
@@ -1455,7 +1464,7 @@ struct Walker {
     PROF_BEGIN(ps1);
     if (slice_type != 2) {
       int skip;
-      if (mbaff) skip = mbaff_skip();
+      if (FLD && mbaff) skip = mbaff_skip();
       else skip = bin(SE_OTHER, 0, (is_b ? 24 : 11) + (left_ok && !(lf & F_SKIP)) + (top_ok && !(tf & F_SKIP)));
       if (skip) {
         cf |= F_SKIP;
@@ -1470,7 +1479,7 @@ struct Walker {
         return;
       }
     }
-    if (mbaff) mbaff_layer_begin();
+    if (FLD && mbaff) mbaff_layer_begin();
     SPROF_END(1, ps1);
     PROF_BEGIN(ps2);
     // mb_type
@@ -1693,8 +1702,8 @@ struct Walker {
 };
 
 // ---------------------------------------------------------------------------------------
-template <int MODE, bool RM>
-AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
+template <int MODE, bool RM, bool FLD>
+AVR_FI void init_slice_state(Walker<MODE, RM, FLD>& w, const EngineTables* T) {
   const int lane = threadIdx.x, nt = blockDim.x;  // every wave of the workgroup takes part
   const avr_slice_desc* d = w.d;
   // cabac contexts: 9.3.1.1
@@ -1719,7 +1728,7 @@ AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
   }
   uint32_t* ring32 = (uint32_t*)w.ring;
   // MBAFF: the pair edges and records too (walk_slice refuses the slice when they do not fit)
-  const int cols = (d->structure == AVR_STRUCT_MBAFF && (int)w.ring_cols >= 3 * w.W + 7) ? 3 * w.W + 7 : w.W;
+  const int cols = (FLD && d->structure == AVR_STRUCT_MBAFF && (int)w.ring_cols >= 3 * w.W + 7) ? 3 * w.W + 7 : w.W;
   for (int i = lane; i < cols * (int)sizeof(EdgeRec) / 4; i += nt) ring32[i] = 0;
   if (lane < 2) {
     w.sh->fifo_head[lane] = 0;
@@ -1728,12 +1737,12 @@ AVR_FI void init_slice_state(Walker<MODE, RM>& w, const EngineTables* T) {
   __syncthreads();
 }
 
-template <int MODE, bool RM>
-AVR_FI void walk_slice(Walker<MODE, RM>& w) {
+template <int MODE, bool RM, bool FLD>
+AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
   const avr_slice_desc* d = w.d;
   w.W = d->mb_width;
   // a field picture is a picture of half the frame's rows (d->mb_height is the frame's)
-  w.H = w.fld_pic ? d->mb_height >> 1 : d->mb_height;
+  w.H = (FLD && w.fld_pic) ? d->mb_height >> 1 : d->mb_height;
   w.slice_type = d->slice_type;
   w.is_b = d->slice_type == 1;
   w.cat_ = d->chroma_array_type;
@@ -1753,11 +1762,11 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
   const int npic = w.W * w.H;
   w.mb_x = addr % w.W;   // then stepped: no integer division per macroblock
   w.mb_y = addr / w.W;
-  w.ystep = w.fld_pic ? 2 : 1;
+  w.ystep = (FLD && w.fld_pic) ? 2 : 1;
   w.my = w.mb_y * w.ystep + (d->structure == AVR_STRUCT_BOTTOM_FIELD ? 1 : 0);
-  w.mbaff = d->structure == AVR_STRUCT_MBAFF;
+  w.mbaff = FLD && d->structure == AVR_STRUCT_MBAFF;
   w.pst = 0;
-  if (w.mbaff) {   // pairs in raster order: mb_y = pair row, my = 2 mb_y + bottom
+  if ((FLD && w.mbaff)) {   // pairs in raster order: mb_y = pair row, my = 2 mb_y + bottom
     if ((int)w.ring_cols < 3 * w.W + 7 || (addr & 1)) { w.err = -20; return; }
     w.mb_x = (addr >> 1) % w.W;
     w.mb_y = (addr >> 1) / w.W;
@@ -1777,12 +1786,12 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
   for (;;) {
     if (addr >= npic) { w.err = -7; break; }
     PROF_BEGINW(ps0);
-    if (!w.mbaff) {
+    if (!(FLD && w.mbaff)) {
       w.left_ok = w.mb_x > 0 && addr - 1 >= w.first_mb;
       // the upper neighbour's flags + cbp: the first dword of its edge record
       w.tf = *(const uint32_t*)&w.ring[w.mb_x];
       w.top_ok = (w.tf & F_DEC) != 0;
-    } else if (!(w.pst & Walker<MODE, RM>::PST_BOT)) {
+    } else if (!(w.pst & Walker<MODE, RM, FLD>::PST_BOT)) {
       w.mbaff_pair_start();
     }
     w.cf = 0;
@@ -1812,14 +1821,14 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
       const uint32_t v = c32[lane < 45 ? lane : 44];
       const uint32_t ve = c32[w.edge_src], ref1 = c32[30];
       const uint32_t ev = lane == 8 ? (ve >> 16) | (ref1 & 0xffff0000u) : lane == 9 ? ve >> 16 : ve;
-      if (!w.mbaff) {
+      if (!(FLD && w.mbaff)) {
         uint32_t* l32 = (uint32_t*)&w.sh->left;
         if (lane < 45) l32[lane] = v;
         uint32_t* e32 = (uint32_t*)&w.ring[w.mb_x];
         if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
         w.lf = w.cf;
       } else {   // the pair edge of this macroblock; the pair's records move left after its bottom
-        const int bot = (w.pst & Walker<MODE, RM>::PST_BOT) != 0;
+        const int bot = (w.pst & Walker<MODE, RM, FLD>::PST_BOT) != 0;
         uint32_t* e32 = (uint32_t*)&w.pair_edge(bot)[w.mb_x];
         if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;
         uint32_t* pr = (uint32_t*)w.pair_rec();
@@ -1832,7 +1841,7 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
         }
       }
       if (RM) {   // MbRec dwords 32-44 are the 52 model bytes
-        uint32_t* f32 = (uint32_t*)(w.frames + w.cur_off + ((int64_t)w.my * w.W + w.mb_x) * 52);
+        uint32_t* f32 = (uint32_t*)(w.frames + w.cur_off + ((int64_t)w.mrow() * w.W + w.mb_x) * 52);
         if (lane >= 32 && lane < 45) f32[lane - 32] = v;
       }
       wave_sync();
@@ -1844,31 +1853,33 @@ AVR_FI void walk_slice(Walker<MODE, RM>& w) {
       if (!RM) w.update_prio();
     }
     // MBAFF: end_of_slice_flag follows the bottom macroblock of a pair only (7.3.4)
-    const int eos = (!w.mbaff || (w.pst & Walker<MODE, RM>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
+    const int eos = (!(FLD && w.mbaff) || (w.pst & Walker<MODE, RM, FLD>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
     SPROF_ENDW(7, ps7);
     if (eos) break;
-    if (Walker<MODE, RM>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
+    if (Walker<MODE, RM, FLD>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
     addr++;
-    if (w.mbaff && !(w.pst & Walker<MODE, RM>::PST_BOT)) {
-      w.pst |= Walker<MODE, RM>::PST_BOT;
+    if ((FLD && w.mbaff) && !(w.pst & Walker<MODE, RM, FLD>::PST_BOT)) {
+      w.pst |= Walker<MODE, RM, FLD>::PST_BOT;
       w.my++;
       continue;
     }
-    if (w.mbaff) {
+    if ((FLD && w.mbaff)) {
       w.pst = 0;
       w.my--;
     }
     if (++w.mb_x == w.W) {
       w.mb_x = 0;
       w.mb_y++;
-      w.my += w.ystep;
+      if (FLD) w.my += w.ystep;
     }
   }
 }
 
+// Run f on the walker instantiation of the slice's structure: w itself for a progressive frame,
+// a field-capable copy (FLD = true, set up from w) for field pictures and MBAFF frames.
 // --------------------------------------------------------------------------- kernel bodies
-template <int MODE, bool RM>
-AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out) {
+template <int MODE, bool RM, bool FLD>
+AVR_FI void begin_slice(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out) {
   w.d = d;
   w.in.g = in + d->payload_offset;
   w.in.limit = MODE == MODE_GENERATE ? 0 : d->read_limit;
@@ -1882,9 +1893,11 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
   vtab_load(w.vt, w.T);
   w.rc_cat = -1;
   w.rc_v = 0;
-  w.fld_pic = d->structure == AVR_STRUCT_TOP_FIELD || d->structure == AVR_STRUCT_BOTTOM_FIELD;
+  w.fld_pic = FLD && (d->structure == AVR_STRUCT_TOP_FIELD || d->structure == AVR_STRUCT_BOTTOM_FIELD);
   w.fld = -1;
-  w.set_fld(w.fld_pic);
+  // the progressive kernels never run a field slice: their LDS tables are the frame ones
+  if (FLD) w.set_fld(w.fld_pic);
+  else w.sig8_v = w.T->sig8x8[__lane_id()];
   w.top_pending = 0;
   w.last8_v = w.T->last8x8[__lane_id()];
   if (MODE == MODE_DECOMPRESS) w.byp_e = w.sh->est[1024];
@@ -1907,8 +1920,8 @@ AVR_FI void begin_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint
 #endif
 }
 
-template <int MODE, bool RM>
-AVR_FI void profile_slice(Walker<MODE, RM>& w) {
+template <int MODE, bool RM, bool FLD>
+AVR_FI void profile_slice(Walker<MODE, RM, FLD>& w) {
 #ifdef AVR_PROFILE
   w.bins = 0;
   const uint64_t t0 = PROF_T();
@@ -1930,8 +1943,8 @@ AVR_FI void profile_slice(Walker<MODE, RM>& w) {
 
 // The walker wave of a pipelined slice: parse + model, one op per bin into the ring, OP_END at
 // the end whatever happened.  Leaves its status in LDS for finish_slice.
-template <int MODE, bool RM>
-AVR_FI void walker_slice(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
+template <int MODE, bool RM, bool FLD>
+AVR_FI void walker_slice(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
   begin_slice(w, d, in, nullptr);
   profile_slice(w);
   if (!RM) cu_post(w.prio_cell, 0);   // leave the CU board
@@ -2257,8 +2270,8 @@ AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_re
 }
 
 // Single-wave slice (the generator: CABAC encode inline, no coder wave).
-template <int MODE, bool RM>
-AVR_FI void run_slice_inline(Walker<MODE, RM>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
+template <int MODE, bool RM, bool FLD>
+AVR_FI void run_slice_inline(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
                              avr_slice_result* res) {
   begin_slice(w, d, in, out);
   profile_slice(w);
@@ -2291,7 +2304,9 @@ constexpr int slice_threads() {
   return MODE == MODE_GENERATE || MODE == MODE_TRACE ? 64 : MODE == MODE_COMPRESS ? 192 : 128;
 }
 
-template <int MODE>
+// FLD = false: the progressive frames of the batch; FLD = true: its field pictures and MBAFF frames
+// (a second launch over the same batch: each kernel leaves the other's slices alone)
+template <int MODE, bool FLD>
 __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                 const uint8_t* in, uint8_t* out, avr_slice_result* res,
                                                                 uint16_t* est_scratch, const int* order,
@@ -2300,7 +2315,8 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   if ((int)blockIdx.x >= n) return;
   const int s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
   const avr_slice_desc* d = &descs[s];
-  Walker<MODE, false> w;
+  if ((d->structure != AVR_STRUCT_FRAME) != FLD) return;
+  Walker<MODE, false, FLD> w;
   w.sh = (Shared*)smem;
   w.ring = (EdgeRec*)(smem + sizeof(Shared));
   load_hot_tables(w.sh, G);
@@ -2352,7 +2368,9 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
 // the slices [file_first[f], file_first[f + 1]) (file_first == nullptr: one file, all n slices),
 // with its own estimator table (est_g + f kEstGlobal), frames (frames + f frame_stride) and
 // frame_meta[f] -- files share nothing, as separate runs of the reference would not.
-template <int MODE>
+// FLD = true when the files may hold field pictures or MBAFF frames (the field-capable walker
+// also walks progressive slices); FLD = false refuses such a slice (status -21)
+template <int MODE, bool FLD>
 __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                   const uint8_t* in, uint8_t* out,
                                                                   avr_slice_result* res, uint16_t* est_g,
@@ -2367,7 +2385,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
   est_g += (size_t)file * kEstGlobal;
   frames += (size_t)file * frame_stride;
   frame_meta += file;
-  Walker<MODE, true> w;
+  Walker<MODE, true, FLD> w;
   w.sh = (Shared*)smem;
   w.ring = (EdgeRec*)(smem + sizeof(Shared));
   load_hot_tables(w.sh, G);
@@ -2412,10 +2430,10 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
       __threadfence_block();
       __syncthreads();
     }
-    if (!d->coded) {
+    if (!d->coded || (!FLD && d->structure != AVR_STRUCT_FRAME)) {
       if (tid == 0) {
         res[s].out_len = 0;
-        res[s].status = 1;
+        res[s].status = d->coded ? -21 : 1;
         res[s].bins = 0;
         res[s].mbs = 0;
       for (int i = 0; i < 6; i++) res[s].bill[i] = 0;
