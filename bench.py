@@ -276,6 +276,37 @@ def corpus_section(ctx, args):
     return rec
 
 
+def rmode_files_section(ctx, args):
+    """The reference model (R-mode) as throughput: its unit of sequential work is a file
+    (DESIGN.md §2), so N independent files go through avr_compress_files / avr_decompress_files at
+    once -- every slice of every file in one parallel R-mode compress pass, one workgroup per file
+    for the decompress.  The files are N copies of realshort.mp4 (independent runs of the reference
+    model; replicas stand in for a corpus of small files).  MB/s = N x file bytes / (compress +
+    decompress wall time), every file checked byte-exact."""
+    import avrecode_amd as avr
+    data = (ROOT / "tests" / "fixtures" / "realshort.mp4").read_bytes()
+    datas = [data] * args.rfiles
+    total = len(data) * args.rfiles
+    walls, tc, td = [], [], []
+    for it in range(1 + args.file_reps):
+        t0 = time.perf_counter()
+        outs = ctx.compress_files(datas, avr.MODEL_REFERENCE)
+        t1 = time.perf_counter()
+        back = ctx.decompress_files(outs)
+        t2 = time.perf_counter()
+        assert back == datas, "R-mode files: decompress did not restore every file"
+        if it == 0:
+            continue   # warm-up (buffer allocation)
+        walls.append(t2 - t0)
+        tc.append(t1 - t0)
+        td.append(t2 - t1)
+    k = sorted(range(len(walls)), key=walls.__getitem__)[len(walls) // 2]
+    progress(f"R-mode files: {total / walls[k] / 1e6:.2f} MB/s")
+    return {"files": args.rfiles, "file": "realshort.mp4", "bytes": total, "model": "reference (R)",
+            "MB_s": total / walls[k] / 1e6, "wall_s": walls[k], "compress_s": tc[k], "decompress_s": td[k],
+            "bit_exact": True}
+
+
 def main_stream_shard(args):
     """BASELINE configs[3]: ONE 4K stream (1 slice per frame, a 1-s GOP I + 29 P tiled to
     --stream-seconds with rewritten frame numbers) cut by NAL unit into contiguous slice ranges
@@ -395,6 +426,7 @@ def main():
     ap.add_argument("--no-clip", action="store_true", help="skip the configs[1] clip in the file roundtrips")
     ap.add_argument("--no-corpus", action="store_true", help="skip the configs[4] corpus")
     ap.add_argument("--corpus-scale", type=float, default=1.0)
+    ap.add_argument("--rfiles", type=int, default=512, help="files in the R-mode many-files leg (0: skip)")
     ap.add_argument("--stream-shard", action="store_true",
                     help="configs[3]: one 4K stream sharded over the GPUs with the RCCL gather (strong scaling)")
     ap.add_argument("--stream-seconds", type=int, default=600)
@@ -518,6 +550,8 @@ def main():
             line["file_roundtrip"] = file_roundtrips(ctx, args)
         if world == 1 and not args.no_corpus:
             line["corpus"] = corpus_section(ctx, args)
+        if world == 1 and args.rfiles > 0 and not args.no_files:
+            line["rmode_files"] = rmode_files_section(ctx, args)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
