@@ -92,6 +92,33 @@ def test_sharded_compress_world1_rccl():
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_compress_multirank_gloo(world):
+    """The sharded compress with several ranks, each a process of its own running its slice range
+    on the device (all on cuda:0 here; one per GPU on a node), gathered to rank 0 over gloo: the
+    container equals the single-GPU compress (golden sha) for both fixtures."""
+    import subprocess
+    import sys
+    import tempfile
+
+    for name in ("realshort.mp4", "cockatoo.mp4"):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        with tempfile.TemporaryDirectory() as td:
+            out = Path(td) / "out.avrc"
+            procs = []
+            for r in range(world):
+                env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                           WORLD_SIZE=str(world), LOCAL_RANK="0")
+                procs.append(subprocess.Popen([sys.executable, str(Path(__file__).parent / "_shard_worker.py"),
+                                               str(FIX / name), str(out)], env=env))
+            rcs = [p.wait(timeout=100) for p in procs]
+            assert rcs == [0] * world, rcs
+            got = out.read_bytes()
+            assert hashlib.sha256(got).hexdigest() == GOLD[(name, "P")]["avrc_sha256"], name
+
+
 def _bills(stderr: str) -> dict:
     """The "Avrecode Bill" / "CABAC Bill" sections of ~h264_model's stderr print (recode.cpp:634-655)."""
     out, cur = {}, None
