@@ -10,7 +10,10 @@ import json
 import os
 from collections import defaultdict
 
-KERNELS = {"slices_parallel_kernel<0>": "compress", "slices_parallel_kernel<1>": "decompress"}
+# progressive-slice kernels ("<0, false>" since the field-capable instantiations, which return at
+# once on a progressive batch; "<0>" before)
+KERNELS = {"slices_parallel_kernel<0>": "compress", "slices_parallel_kernel<1>": "decompress",
+           "slices_parallel_kernel<0, false>": "compress", "slices_parallel_kernel<1, false>": "decompress"}
 
 
 def main():

@@ -26,7 +26,8 @@ def main():
     for p in glob.glob(os.path.join(a.src, "pass*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
             name = r["Kernel_Name"]
-            if "slices_parallel_kernel<" not in name:
+            # the field-capable kernels (", true>") return at once on a progressive batch
+            if "slices_parallel_kernel<" not in name or ", true>" in name:
                 continue
             k = "slices_parallel_kernel<%s>" % name.split("slices_parallel_kernel<")[1][0]
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
