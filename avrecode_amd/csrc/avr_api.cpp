@@ -556,8 +556,12 @@ void add_bill(Bill* b, const avr_slice_result& r) {
   for (int i = 0; i < 6; i++) (*b)[i] += r.bill[i];
 }
 
+// verify (parallel model): decompress every candidate slice on the device and code only those that
+// regenerate their payload.  avr_roundtrip_file skips it on a first attempt -- its own whole-file
+// decompress and compare check the same thing, as the reference's roundtrip() does with a
+// compressor that never verifies (recode.cpp:1594-1624) -- and repeats with it on a mismatch.
 int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* in_len, int model, uint8_t** out,
-                   size_t* out_len, int32_t* status, std::vector<Bill>* bills = nullptr) {
+                   size_t* out_len, int32_t* status, std::vector<Bill>* bills = nullptr, bool verify = true) {
   if (bills) bills->assign(nf, Bill{});
   HIP_TRY(c, hipSetDevice(c->device));
   std::vector<int32_t> st(nf, AVR_OK);
@@ -592,7 +596,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   }
   std::vector<avr_slice_result> res;
   std::vector<uint8_t> outb;
-  if (int r = run_plan(c, 0, false, plan, &res, &outb, /*verify=*/true,
+  if (int r = run_plan(c, 0, false, plan, &res, &outb, verify,
                        bills && model == AVR_MODEL_PARALLEL ? avr::kFlagBill : 0))
     return r;
   // 2) segmentation (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297)
@@ -953,20 +957,38 @@ int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8
   size_t cn = 0, dn = 0;
   std::vector<Bill> cbill, dbill;
   int32_t st = 0;
-  const double t0 = now_s();
-  if (int r = compress_files(c, 1, &in, &n, model, &comp, &cn, &st, &cbill)) return r;
-  if (st) return st;
-  const double t1 = now_s();
-  const uint8_t* cp = comp;
-  int r = decompress_files(c, 1, &cp, &cn, &dec, &dn, &st, &dbill);
-  if (!r) r = st;
-  const double t2 = now_s();
-  if (r) {
+  double t0 = 0, t1 = 0, t2 = 0;
+  bool same = false;
+  // the parallel model's per-slice device check is left to the whole-file compare below; a file
+  // that does not come back is compressed again with it (every slice that fails it stored as is)
+  for (int attempt = model == AVR_MODEL_PARALLEL ? 0 : 1; attempt < 2; attempt++) {
     free(comp);
-    return r;
+    comp = nullptr;
+    cn = 0;
+    t0 = now_s();
+    if (int r = compress_files(c, 1, &in, &n, model, &comp, &cn, &st, &cbill, /*verify=*/attempt > 0)) {
+      free(comp);
+      return r;
+    }
+    if (st) {
+      free(comp);
+      return st;
+    }
+    t1 = now_s();
+    const uint8_t* cp = comp;
+    int r = decompress_files(c, 1, &cp, &cn, &dec, &dn, &st, &dbill);
+    if (!r) r = st;
+    t2 = now_s();
+    same = !r && dn == n && memcmp(dec, in, n) == 0;
+    free(dec);
+    dec = nullptr;
+    if (attempt == 0 && getenv("AVR_ROUNDTRIP_FORCE_VERIFY")) continue;   // tests: the second path
+    if (same) break;
+    if (attempt == 1 && r) {
+      free(comp);
+      return r;
+    }
   }
-  const bool same = dn == n && memcmp(dec, in, n) == 0;
-  free(dec);
   if (stats) {
     memset(stats, 0, sizeof(*stats));
     stats->file_bytes = n;
