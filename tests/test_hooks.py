@@ -82,6 +82,23 @@ def test_hooks_compress_then_decompress(name, mode, model):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["paff_ipp.264", "mbaff_ib.264"])
+@pytest.mark.parametrize("mode,model", [("R", 0), ("P", 1)])
+def test_hooks_field_streams(name, mode, model):
+    """Field pictures and MBAFF frames through the hooks surface: the oracle's parser (field
+    contexts, macroblock pairs) driven by the device's bins gives the pinned containers
+    (tests/golden/fields.json) and the original file back."""
+    g = {e["file"]: e for e in json.loads((ROOT / "tests/golden/fields.json").read_text())["files"]}[name]
+    data = (FIX / name).read_bytes()
+    r, avrc, walked = _call("hooks_compress", data, len(data), model)
+    assert r == 0, r
+    assert hashlib.sha256(avrc).hexdigest() == g[mode]["avrc_sha256"]
+    r, back, walked_d = _call("hooks_decompress", avrc, len(avrc))
+    assert r == 0, r
+    assert walked_d == walked and back == data
+
+
+@pytest.mark.gpu
 def test_hooks_detect_a_diverging_caller():
     """A container whose re-coded stream was altered: the device decompress either fails or
     yields different bins; either way the session must not report success with wrong bytes."""
