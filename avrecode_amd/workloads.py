@@ -3,8 +3,9 @@
 (data/GOPR4542.MP4) is absent, so these seeded streams stand in, as SURVEY.md 8d specifies.
 
   clip(ctx)        configs[1]: 1080p High 4:2:0, 64 frames x 1 slice, GOP I + 31 P (twice), QP 26
-  corpus(ctx)      configs[4]: mixed I/P/B GOPs, 1/2/4/8/17 slices per frame, 720p/1080p/4K, plus
-                   the two real fixtures (tests/fixtures)
+  corpus(ctx)      configs[4]: mixed I/P/B GOPs, 1/2/4/8/17 slices per frame, 720p/1080p/4K,
+                   progressive plus two 1080i streams (field pictures and MBAFF), plus the two real
+                   fixtures (tests/fixtures)
   stream_4k(ctx)   configs[3]: one 4K stream, 1 slice per frame, 1-s GOP (I + 29 P) tiled with
                    rewritten frame numbers (avr_synthesize_stream's repeat)
 """
@@ -23,26 +24,35 @@ def clip(ctx, frames: int = 64, mb_width: int = 120, mb_height: int = 68, seed: 
                                       chroma_format_idc=1, transform_8x8_mode=1, seed=seed, gop_length=32), frames)
 
 
-# (name, mb_width, mb_height, slices per frame, frames, gop, slice type between I pictures, QP, chroma)
+# (name, mb_width, mb_height, slices per picture, frames, gop, slice type between I pictures, QP,
+#  chroma, structure: 0 progressive, 1 field pictures (two fields per frame), 2 MBAFF)
 CORPUS = [
-    ("720p_IBBP_2spf", 80, 45, 2, 24, 12, 1, 24, 1),
-    ("720p_IP_1spf", 80, 45, 1, 32, 16, 0, 28, 1),
-    ("1080p_IBBP_4spf", 120, 68, 4, 16, 8, 1, 26, 1),
-    ("1080p_IP_17spf", 120, 68, 17, 8, 8, 0, 22, 1),
-    ("1080p_I_8spf_422", 120, 68, 8, 4, 1, 2, 30, 2),
-    ("4K_IP_8spf", 240, 135, 8, 6, 6, 0, 27, 1),
-    ("4K_IBBP_1spf_444", 240, 135, 1, 4, 4, 1, 30, 3),
+    ("720p_IBBP_2spf", 80, 45, 2, 24, 12, 1, 24, 1, 0),
+    ("720p_IP_1spf", 80, 45, 1, 32, 16, 0, 28, 1, 0),
+    ("1080p_IBBP_4spf", 120, 68, 4, 16, 8, 1, 26, 1, 0),
+    ("1080p_IP_17spf", 120, 68, 17, 8, 8, 0, 22, 1, 0),
+    ("1080p_I_8spf_422", 120, 68, 8, 4, 1, 2, 30, 2, 0),
+    ("4K_IP_8spf", 240, 135, 8, 6, 6, 0, 27, 1, 0),
+    ("4K_IBBP_1spf_444", 240, 135, 1, 4, 4, 1, 30, 3, 0),
+    ("1080i_PAFF_IP_2spf", 120, 68, 2, 8, 8, 0, 26, 1, 1),
+    ("1080i_MBAFF_IBBP_2spf", 120, 68, 2, 8, 8, 1, 26, 1, 2),
 ]
+
+
+def slices_of(entry, frames: int) -> int:
+    """Slices the generator writes for `frames` frames of a CORPUS entry."""
+    spf, structure = entry[3], entry[9]
+    return frames * spf * (2 if structure == 1 else 1)
 
 
 def corpus(ctx, scale: float = 1.0, fixtures: bool = True) -> list[tuple[str, bytes]]:
     """configs[4]: [(name, file bytes)].  scale < 1 shortens every stream (tests)."""
     out = []
-    for k, (name, w, h, spf, frames, gop, st, qp, cf) in enumerate(CORPUS):
+    for k, (name, w, h, spf, frames, gop, st, qp, cf, structure) in enumerate(CORPUS):
         n = max(1, int(round(frames * scale)))
         p = SynthParams(mb_width=w, mb_height=h, slice_type=st, slice_qp=qp, chroma_format_idc=cf,
                         transform_8x8_mode=1, num_ref_idx_l0=2, num_ref_idx_l1=1, seed=4000 + k,
-                        slices_per_picture=spf, gop_length=gop)
+                        slices_per_picture=spf, gop_length=gop, structure=structure)
         out.append((name, ctx.synthesize(p, n)))
     if fixtures:
         for f in FIXTURES:

@@ -82,11 +82,14 @@ def test_mixed_models_and_error_isolation(ctx):
 def test_corpus_generator_structure(ctx):
     files = workloads.corpus(ctx, scale=0.25, fixtures=False)
     assert [n for n, _ in files] == [c[0] for c in workloads.CORPUS]
-    for (name, w, h, spf, frames, gop, st, qp, cf), (_, data) in zip(workloads.CORPUS, files):
+    for entry, (_, data) in zip(workloads.CORPUS, files):
+        name, w, h, spf, frames, gop, st, qp, cf, structure = entry
         d = avr.parse_stream(data).descs
         n = max(1, int(round(frames * 0.25)))
-        assert len(d) == n * spf, name
+        assert len(d) == workloads.slices_of(entry, n), name
         assert (d["mb_width"] == w).all() and (d["mb_height"] == h).all() and (d["chroma_array_type"] == cf).all()
+        want = {0: {0}, 1: {1, 2}, 2: {3}}[structure]
+        assert set(int(x) for x in d["structure"]) == want, name
         types = set(int(t) for t in d["slice_type"])
         assert 2 in types
     outs = ctx.compress_files([d for _, d in files], avr.MODEL_REFERENCE)
