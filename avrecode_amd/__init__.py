@@ -102,7 +102,7 @@ class SynthParams:
     slices_per_picture: int = 1
     gop_length: int = 0          # > 0: IDR I picture every gop_length pictures, slice_type between
     repeat: int = 1              # > 1: the pictures written this many times (frame numbers advance)
-    structure: int = 0           # 0 progressive, 1 field pictures (PAFF), 2 MBAFF frames
+    structure: int = 0           # 0 progressive, 1 field pictures (PAFF), 2 MBAFF frames, 3 PAFF bottom first
 
 
 _lib = None

@@ -1192,12 +1192,14 @@ int avr_container_describe(const uint8_t* in, size_t n, char** json, uint8_t** r
 int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t** out, size_t* out_len) {
   if (!c || !p || n <= 0 || !out || !out_len || p->mb_width <= 0 || p->mb_height <= 0 || p->slice_type < 0 ||
       p->slice_type > 2 || p->chroma_format_idc < 1 || p->chroma_format_idc > 3 || p->gop_length < 0 ||
-      p->repeat < 0 || p->structure < 0 || p->structure > 2 || (p->structure && (p->mb_height & 1)))
+      p->repeat < 0 || p->structure < 0 || p->structure > 3 || (p->structure && (p->mb_height & 1)))
     return AVR_ERR_INVALID_ARGUMENT;
   HIP_TRY(c, hipSetDevice(c->device));
   Plan plan;
-  // a coded picture: the frame, or (field pictures) each of its two fields in turn
-  const int fields = p->structure == 1 ? 2 : 1;
+  // a coded picture: the frame, or (field pictures) each of its two fields in turn, the top
+  // field first (structure 1) or the bottom field first (3)
+  const bool paff = p->structure == 1 || p->structure == 3;
+  const int fields = paff ? 2 : 1;
   const int mbs = p->mb_width * p->mb_height / fields;
   // MBAFF slices start on a macroblock pair
   const int unit = p->structure == 2 ? 2 : 1;
@@ -1229,7 +1231,7 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
     d.picture_id = pic;
     d.first_mb = first;
     d.coded = 1;
-    d.structure = p->structure == 1 ? (fi ? AVR_STRUCT_BOTTOM_FIELD : AVR_STRUCT_TOP_FIELD)
+    d.structure = paff ? ((fi ^ (p->structure == 3)) ? AVR_STRUCT_BOTTOM_FIELD : AVR_STRUCT_TOP_FIELD)
                 : p->structure == 2 ? AVR_STRUCT_MBAFF : AVR_STRUCT_FRAME;
     d.payload_offset = p->seed * 0x100000001B3ull + (uint64_t)i;  // generator seed
     d.payload_size = (uint32_t)(next - first);                    // generator: macroblocks to emit
@@ -1252,8 +1254,9 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
   stream.reserve(bytes * reps + 256);
   for (int t = 0; t < reps; t++)
     for (int i = 0; i < (int)plan.descs.size(); i++)
-      avr::synth_write_slice(&stream, *p, plan.descs[i].slice_type, t * n + pic_of[i], plan.descs[i].structure, first_of[i],
-                             outb.data() + plan.descs[i].out_offset, res[i].out_len);
+      avr::synth_write_slice(&stream, *p, plan.descs[i].slice_type, t * n + pic_of[i], plan.descs[i].structure,
+                             paff && (i / spp) % 2 == 1, first_of[i], outb.data() + plan.descs[i].out_offset,
+                             res[i].out_len);
   *out = (uint8_t*)malloc(stream.size());
   if (!*out) return AVR_ERR_OUT_OF_MEMORY;
   memcpy(*out, stream.data(), stream.size());

@@ -104,15 +104,17 @@ void synth_write_parameter_sets(std::vector<uint8_t>* out, const avr_synth_param
 }
 
 void synth_write_slice(std::vector<uint8_t>* out, const avr_synth_params& p, int slice_type, int index,
-                       int structure, int first_mb, const uint8_t* payload, size_t payload_len) {
-  const bool idr = slice_type == 2 && structure != AVR_STRUCT_BOTTOM_FIELD;
+                       int structure, bool second_field, int first_mb, const uint8_t* payload,
+                       size_t payload_len) {
+  // every I picture is an IDR picture; the second field of an IDR frame is a non-IDR I field
+  const bool idr = slice_type == 2 && !second_field;
   const bool field = structure == AVR_STRUCT_TOP_FIELD || structure == AVR_STRUCT_BOTTOM_FIELD;
   BitWriter h;
   h.ue((uint32_t)(structure == AVR_STRUCT_MBAFF ? first_mb / 2 : first_mb));   // first_mb_in_slice (pairs in MBAFF)
   h.ue((uint32_t)slice_type + 5);
   h.ue(0);                       // pps id
   // frame_num: an IDR frame's is 0, and both fields of a frame carry the same one
-  h.u(slice_type == 2 && (idr || structure == AVR_STRUCT_BOTTOM_FIELD) ? 0 : (uint32_t)(index & 0xffff), 16);
+  h.u(slice_type == 2 ? 0 : (uint32_t)(index & 0xffff), 16);
   if (p.structure != 0) {
     h.u(field ? 1 : 0, 1);       // field_pic_flag
     if (field) h.u(structure == AVR_STRUCT_BOTTOM_FIELD ? 1 : 0, 1);   // bottom_field_flag

@@ -252,7 +252,8 @@ typedef struct {
                                   * long stream tiled from one GOP; the payloads repeat) */
   int32_t structure;             /* 0 progressive frames; 1 field pictures (PAFF: each picture a
                                   * top then a bottom field, mb_height even); 2 MBAFF frames (every
-                                  * macroblock pair field or frame coded at random, mb_height even) */
+                                  * macroblock pair field or frame coded at random, mb_height even);
+                                  * 3 field pictures, bottom field first */
 } avr_synth_params;
 /* Generate n pictures on the device (each slices_per_picture slices, in decode order) and return
  * them as one Annex-B stream (SPS/PPS + the slice NAL units) in host memory.  Pictures are

@@ -91,6 +91,33 @@ def test_field_picture_files_match_oracle(ctx, case):
     assert seq == ctx.compress(data, avr.MODEL_REFERENCE)
 
 
+def test_bottom_field_first(ctx):
+    """Field pictures with the bottom field coded first (generator structure 3): the bottom field
+    is the IDR / first field, the top field the second field of the same frame_num, so the two
+    still share one picture id; the reference model's first-coded field is the bottom one (its
+    parallel compress must see the top rows as not yet written).  Batch, both file models, the
+    sequential reference-model compress, against the oracle."""
+    data = _paff(ctx, 4, structure=3, slice_type=1, gop_length=3, slices_per_picture=2, num_ref_idx_l0=2,
+                 transform_8x8_mode=1, seed=91)
+    d = avr.parse_stream(data).descs
+    assert [int(x) for x in d["structure"][:8]] == [2, 2, 1, 1] * 2
+    assert [int(x) for x in d["picture_id"]] == [k // 4 + 1 for k in range(16)]
+    _check_batch_against_oracle(ctx, data, require_all=True)
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / "bff.264"
+        f.write_bytes(data)
+        for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+            avrc = ctx.compress(data, model)
+            assert avrc == oracle_cli("compress", f, mode=mode), mode
+            assert ctx.decompress(avrc) == data
+    os.environ["AVR_RMODE_SEQUENTIAL"] = "1"
+    try:
+        seq = ctx.compress(data, avr.MODEL_REFERENCE)
+    finally:
+        del os.environ["AVR_RMODE_SEQUENTIAL"]
+    assert seq == ctx.compress(data, avr.MODEL_REFERENCE)
+
+
 def test_field_and_frame_pictures_mixed(ctx):
     """A progressive stream followed by a field stream of the same size (two SPS): frame and field
     context tables alternate in one reference-model walk."""
