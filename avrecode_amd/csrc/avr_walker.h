@@ -464,6 +464,9 @@ AVR_FI void est_table_reset(uint16_t* est_g, Shared* sh) {
 // FLD: field-coded slices (PAFF, MBAFF) -- a second instantiation (kernels of their own, launched
 // only when a batch may hold such slices: kFlagFields), so that the progressive walker carries no
 // field tests in its per-bin and per-macroblock code
+// v_writelane_b32 (clang has no builtin for it; the LLVM intrinsic by its name)
+extern "C" __device__ int avr_llvm_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 template <int MODE, bool RM, bool FLD = false>
 struct Walker {
   static constexpr bool DEC = MODE == MODE_COMPRESS || MODE == MODE_TRACE;  // CABAC decoding side
@@ -541,7 +544,12 @@ struct Walker {
   int rc_cat;
   uint32_t sig8_v, last8_v;   // 8x8 significant / last ctxIdxInc tables, lane = scan position
   uint32_t byp_e;         // decompress: the estimator of &bypass_context (recode.cpp:1049), Shared::est[1024] while walking
-  AVR_FI static uint32_t wlane(uint32_t v, uint32_t L, uint32_t x) { return __lane_id() == L ? x : v; }
+  // lane L of v := x (L and x wave-uniform).  Decompress: one v_writelane, no lane-mask compare
+  // to keep live (R-mode decompress -1 %); compress keeps the select (v_writelane there: +2 %).
+  AVR_FI static uint32_t wlane(uint32_t v, uint32_t L, uint32_t x) {
+    if (MODE == MODE_DECOMPRESS) return (uint32_t)avr_llvm_writelane((int)x, (int)L, (int)v);
+    return __lane_id() == L ? x : v;
+  }
   AVR_FI int rc_addr(int cat, uint32_t j) const {
     // Only the contexts the category can use: a lane past them would alias another syntax
     // element's context and write a stale copy back over it at rc_writeback -- within the
