@@ -549,9 +549,12 @@ __device__ __forceinline__ int rd_get(RecodedDecoder& d, InStream& in, uint64_t 
   const bool bin = (hi32(diff) >> 31) == 0;
   d.low = bin ? diff : d.low;
   d.range = bin ? r1 : r0;
+  // below min_range (2^51) the encoder shifts until range >= 2^55 (re_put).  A decision starts
+  // from range >= 2^51 and both outcomes keep at least range / 97 > 2^44 (pos, neg >= 1,
+  // pos + neg <= 97), never 0: one or two digits, straight-line instead of a loop
   if (hi32(d.range) < (1u << 19)) {
-    #pragma clang loop unroll(disable)
-    while (hi32(d.range) < (1u << 23) && d.range != 0) rd_consume(d, in);
+    rd_consume(d, in);
+    if (hi32(d.range) < (1u << 23)) rd_consume(d, in);
   }
   return bin;
 }
