@@ -428,7 +428,6 @@ static void residual_block(walker_t *w, int cat, int n, int max, int is_dc, int 
   }
   int cnt = 0;
   if (coded) {
-    int idx[64];
     int numc8x8 = w->h->chroma_array_type == 2 ? 2 : 1;
     hk->begin_coding_type(hk->opaque, PIP_SIGNIFICANCE_MAP, 0, 0, 0);
     int last;
@@ -438,11 +437,11 @@ static void residual_block(walker_t *w, int cat, int n, int max, int is_dc, int 
       else if (cat == 3) { sctx = lctx = imin(last / numc8x8, 2); }
       else sctx = lctx = last;
       if (bin(w, SE_SIG, last, (w->fld ? sig_base_fld : sig_base)[cat] + sctx)) {
-        idx[cnt++] = last;
+        cnt++;  /* only the count matters: levels are coded in reverse scan order */
         if (bin(w, SE_LAST, last, (w->fld ? last_base_fld : last_base)[cat] + lctx)) { last = max; break; }
       }
     }
-    if (last == max - 1) idx[cnt++] = last;
+    if (last == max - 1) cnt++;
     hk->end_coding_type(hk->opaque, PIP_SIGNIFICANCE_MAP);
     int gt1 = 0, eq1 = 0;
     for (int i = cnt - 1; i >= 0 && !w->err; i--) {
