@@ -21,7 +21,7 @@ import numpy as np
 
 __all__ = [
     "AvrError", "Context", "MODEL_REFERENCE", "MODEL_PARALLEL", "SLICE_DESC", "SLICE_RESULT",
-    "SynthParams", "lib", "parse_stream", "assemble_container", "library_path", "EXPORTED_SYMBOLS",
+    "SynthParams", "lib", "parse_stream", "assemble_container", "neighbor_tables", "library_path", "EXPORTED_SYMBOLS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "avr_hooks_compress_begin", "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
     "avr_hook_get_bypass", "avr_hook_get_terminate", "avr_hook_skip_bytes", "avr_hook_frame_spec", "avr_hook_mb_xy",
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
-    "avr_hooks_end", "avr_hooks_destroy",
+    "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables",
 )
 
 # avr_slice_desc / avr_slice_result (include/avrecode.h), C layout
@@ -142,6 +142,7 @@ def lib() -> ctypes.CDLL:
     L.avr_container_describe.argtypes = [vp, sz, pp, pp, psz]
     L.avr_compress_files.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
     L.avr_decompress_files.argtypes = [vp, i32, vp, vp, vp, vp, vp]
+    L.avr_neighbor_tables.argtypes = [vp, vp]
     for name in EXPORTED_SYMBOLS:   # fails here, not at first use, when the build is stale
         getattr(L, name)
     _lib = L
@@ -226,6 +227,17 @@ def describe_container(avrc) -> tuple[dict, bytes]:
     text = ctypes.string_at(js.value).decode()
     L.avr_free(js)
     return json.loads(text), _take(out, olen.value)
+
+
+def neighbor_tables(ctx=None) -> tuple[bytes, bytes]:
+    """(nb_left[48], nb_up[48]): the model's neighbour geometry as the kernels use it
+    (avr_neighbor_tables).  ctx None: the host-built table (no GPU); a Context: its device copy."""
+    L = lib()
+    out = ctypes.create_string_buffer(96)
+    r = L.avr_neighbor_tables(ctx._h if ctx is not None else None, out)
+    if r != AVR_OK:
+        raise AvrError(r, "avr_neighbor_tables failed")
+    return out.raw[:48], out.raw[48:96]
 
 
 class Context:

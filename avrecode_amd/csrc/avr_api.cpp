@@ -897,6 +897,21 @@ const char* avr_last_error(const avr_ctx* c) { return c ? c->err.c_str() : "no c
 
 void avr_free(void* p) { free(p); }
 
+int avr_neighbor_tables(avr_ctx* c, uint8_t out[96]) {
+  if (!out) return AVR_ERR_INVALID_ARGUMENT;
+  static_assert(offsetof(avr::HotTables, nb_up) == offsetof(avr::HotTables, nb_left) + 48, "nb_left, nb_up adjacent");
+  if (!c) {
+    std::unique_ptr<avr::EngineTables> t(new avr::EngineTables());
+    build_tables(t.get());
+    memcpy(out, t->hot.nb_left, 96);
+    return AVR_OK;
+  }
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t off = offsetof(avr::EngineTables, hot) + offsetof(avr::HotTables, nb_left);
+  HIP_TRY(c, hipMemcpy(out, c->tables.as<uint8_t>() + off, 96, hipMemcpyDeviceToHost));
+  return AVR_OK;
+}
+
 int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** out, size_t* out_len) {
   if (!c || !in || !out || !out_len || (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL))
     return AVR_ERR_INVALID_ARGUMENT;

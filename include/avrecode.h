@@ -191,6 +191,14 @@ int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const in
  * Both buffers are malloc'd (avr_free).  AVR_ERR_FORMAT when the bytes are not a Recoded message. */
 int avr_container_describe(const uint8_t* in, size_t n, char** json, uint8_t** reserialized, size_t* len);
 
+/* Model neighbour geometry (get_neighbor_sub_mb + reverse_scan_8, recode.cpp:279-312, 419-471) as the
+ * kernels use it (HotTables::nb_left / nb_up, loaded into every workgroup's LDS): out[n] (n < 48) =
+ * the 4x4 block left of block n, out[48 + n] = the block above it, | 128 when that block lies in
+ * the left / upper macroblock.  ctx NULL: the table the library builds on the host (no device
+ * needed); a context: read back from that device's copy.  Pinned against the reference compiled
+ * here by tests/test_oracle_geometry.py and tests/test_gpu_parity.py. */
+int avr_neighbor_tables(avr_ctx* ctx, uint8_t out[96]);
+
 /* ------------------------------------------------ libavcodec-hooks callback surface (AVCodecHooks) */
 /* For a caller that drives the recode path from its own H.264 decoder exactly as the reference's
  * libavcodec-hooks fork does (recode.cpp:137-228).  A session runs the whole file on the device up

@@ -70,6 +70,12 @@ static int get_neighbor_sub_mb(int above, int sub_mb_size, int mb_x, int mb_y, i
   *oy = mb_y;
   return 1;
 }
+/* exported for tests/test_oracle_geometry.py: compared with the reference's get_neighbor_sub_mb
+ * compiled from recode.cpp:419-471 (tests/golden/geometry.json) */
+int oracle_get_neighbor_sub_mb(int above, int sub_mb_size, int mb_x, int mb_y, int scan8_index, int *out3) {
+  return get_neighbor_sub_mb(above, sub_mb_size, mb_x, mb_y, scan8_index, &out3[0], &out3[1], &out3[2]);
+}
+const uint8_t *oracle_scan_8(void) { return scan_8; }
 
 /* ------------------------------------------------------------------------- FrameBuffer */
 static void fb_bzero(framebuf_t *f) {
