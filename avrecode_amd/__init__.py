@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "avr_hooks_compress_begin", "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
     "avr_hook_get_bypass", "avr_hook_get_terminate", "avr_hook_skip_bytes", "avr_hook_frame_spec", "avr_hook_mb_xy",
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
-    "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables",
+    "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables", "avr_last_phase_times",
 )
 
 # avr_slice_desc / avr_slice_result (include/avrecode.h), C layout
@@ -72,11 +72,24 @@ class AvrError(RuntimeError):
         self.code = code
 
 
+PHASES = ("demux_s", "upload_s", "kernel_s", "download_s", "container_s", "other_s")
+
+
+class _PhaseTimes(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in PHASES]
+
+
+def _phases(p: _PhaseTimes) -> dict:
+    return {n: getattr(p, n) for n in PHASES}
+
+
 class _FileStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
                 ("file_bytes", "slices", "coded_slices", "skipped_slices", "payload_bytes", "recoded_bytes", "bins")] + \
                [("compress_s", ctypes.c_double), ("decompress_s", ctypes.c_double),
-                ("bill", ctypes.c_uint64 * 6), ("cabac_bill", ctypes.c_uint64 * 6)]
+                ("bill", ctypes.c_uint64 * 6), ("cabac_bill", ctypes.c_uint64 * 6),
+                ("attempts", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("compress_phases", _PhaseTimes), ("decompress_phases", _PhaseTimes)]
 
 
 class _SynthParams(ctypes.Structure):
@@ -143,6 +156,7 @@ def lib() -> ctypes.CDLL:
     L.avr_compress_files.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
     L.avr_decompress_files.argtypes = [vp, i32, vp, vp, vp, vp, vp]
     L.avr_neighbor_tables.argtypes = [vp, vp]
+    L.avr_last_phase_times.argtypes = [vp, vp]
     for name in EXPORTED_SYMBOLS:   # fails here, not at first use, when the build is stale
         getattr(L, name)
     _lib = L
@@ -293,7 +307,9 @@ class Context:
         st = _FileStats()
         self._check(lib().avr_roundtrip_file(self._h, p, n, model, ctypes.byref(out), ctypes.byref(olen),
                                              ctypes.byref(st)), "roundtrip")
-        stats = {f: getattr(st, f) for f, _ in _FileStats._fields_}
+        stats = {f: getattr(st, f) for f, _ in _FileStats._fields_ if f != "reserved"}
+        for f in ("compress_phases", "decompress_phases"):
+            stats[f] = _phases(stats[f])
         for f in ("bill", "cabac_bill"):   # by CodingType name, nonzero entries (~h264_model's print)
             stats[f] = {CODING_TYPES[i]: int(v) for i, v in enumerate(stats[f]) if v}
         return _take(out, olen.value), stats
@@ -308,13 +324,22 @@ class Context:
         st = (ctypes.c_int32 * max(1, n))()
         self._check(fn(self._h, n, ptrs, lens, *extra, outs, olens, st), fn.__name__)
         res = []
+        failed = [k for k in range(n) if st[k] != AVR_OK]
+        # the context keeps one error message: it belongs to a failed file only when there is one
+        detail = lib().avr_last_error(self._h).decode(errors="replace") if len(failed) == 1 else ""
         for k in range(n):
             if st[k] != AVR_OK:
-                res.append(AvrError(st[k], f"file {k}: {lib().avr_last_error(self._h).decode(errors='replace')}"))
+                res.append(AvrError(st[k], f"file {k}" + (f": {detail}" if detail else "")))
             else:
                 res.append(_take(ctypes.c_void_p(outs[k]), olens[k]))
         del keep
         return res
+
+    def last_phase_times(self) -> dict:
+        """avr_last_phase_times: where the last whole-file call's wall time went (seconds)."""
+        p = _PhaseTimes()
+        self._check(lib().avr_last_phase_times(self._h, ctypes.byref(p)), "avr_last_phase_times")
+        return _phases(p)
 
     def compress_files(self, datas, model: int = MODEL_REFERENCE) -> list:
         """avr_compress_files: one container (bytes) or AvrError per input file."""

@@ -71,15 +71,39 @@ struct avr_ctx {
   DevBuf file_first, file_op_off;                        // reference model over several files
   bool round_robin = false;   // placement probe passed: the CU schedule (order) may be used
   int* order_or_null() { return round_robin ? order.as<int>() : nullptr; }
+  // phase breakdown of the current / last whole-file call (avr_phase_times): run_plan adds the
+  // device phases (HIP events ev[0..3] around its uploads, kernels and downloads) and its own wall
+  // time (plan_wall); the file paths add the host phases
+  avr_phase_times phase{};
+  double plan_wall = 0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  ~avr_ctx() {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
 };
 
 namespace {
 
 constexpr int kMaxSlicesPerLaunch = 4096;
+constexpr size_t kLdsBudget = 160 * 1024;   // LDS per workgroup (one slice) on gfx950
+constexpr uint64_t kMaxSynthBytes = (uint64_t)1 << 35;   // avr_synthesize_stream's output cap (32 GiB)
 
 int fail(avr_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
+}
+// No C++ exception crosses the C ABI: the entry points that build host containers run their body
+// through guarded(), which turns an allocation failure into AVR_ERR_OUT_OF_MEMORY.
+template <class F>
+int guarded(avr_ctx* c, F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return fail(c, AVR_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(c, AVR_ERR_DEVICE, std::string("internal error: ") + e.what());
+  }
 }
 #define HIP_TRY(c, expr)                                                                              \
   do {                                                                                                \
@@ -370,7 +394,7 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
 // last-byte rule and compare with the payload (avr_roundtrip_slices); a slice whose output does not
 // regenerate its payload gets status kStatusNoRoundtrip, so no container ever holds a block that
 // cannot be decompressed.
-constexpr int32_t kStatusNoRoundtrip = -20;
+constexpr int32_t kStatusNoRoundtrip = AVR_SLICE_NO_ROUNDTRIP;
 int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_slice_result>* res,
              std::vector<uint8_t>* out_host, bool verify = false, uint32_t flags = 0) {
   const int n = (int)plan.descs.size();
@@ -383,13 +407,18 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
   }
   out_host->assign(out_total, 0);
   if (!n) return AVR_OK;
+  const double t_wall = now_s();
   HIP_TRY(c, c->in.reserve(plan.arena.size() + 4096));
-  HIP_TRY(c, hipMemcpyAsync(c->in.p, plan.arena.data(), plan.arena.size(), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, c->out.reserve(out_total + 4096));
   HIP_TRY(c, c->descs.reserve(sizeof(avr_slice_desc) * n));
   HIP_TRY(c, c->res.reserve(sizeof(avr_slice_result) * n));
+  for (auto& e : c->ev)
+    if (!e) HIP_TRY(c, hipEventCreate(&e));
+  HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->in.p, plan.arena.data(), plan.arena.size(), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->descs.p, plan.descs.data(), sizeof(avr_slice_desc) * n, hipMemcpyHostToDevice,
                             c->stream));
+  HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   int rm = kRModeFallback;
   if (sequential && mode == 0 && !getenv("AVR_RMODE_SEQUENTIAL")) {
     rm = run_rmode_compress(c, plan, out_total, flags);
@@ -453,9 +482,17 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
     verdict.resize(n);
     HIP_TRY(c, hipMemcpyAsync(verdict.data(), c->verdict.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
   }
+  HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(c, hipMemcpyAsync(res->data(), c->res.p, sizeof(avr_slice_result) * n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipMemcpyAsync(out_host->data(), c->out.p, out_total, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  float ms[3] = {0, 0, 0};
+  for (int i = 0; i < 3; i++) HIP_TRY(c, hipEventElapsedTime(&ms[i], c->ev[i], c->ev[i + 1]));
+  c->phase.upload_s += 1e-3 * ms[0];
+  c->phase.kernel_s += 1e-3 * ms[1];
+  c->phase.download_s += 1e-3 * ms[2];
+  c->plan_wall += now_s() - t_wall;
   for (int k = 0; k < (int)verdict.size(); k++)
     if ((*res)[k].status == 0 && verdict[k] != 1) (*res)[k].status = kStatusNoRoundtrip;
   return AVR_OK;
@@ -480,7 +517,13 @@ int parse_file(avr_ctx* c, const uint8_t* in, size_t n, ParsedFile* pf) {
   return AVR_OK;
 }
 
-bool recodable_candidate(const avr::SliceInfo& s) { return s.h.supported && s.size >= (size_t)avr::kSurrogateMarkerBytes; }
+// A slice the device can take: supported syntax, at least a surrogate marker long, and an LDS ring
+// (ring_cols: 3 W + 7 records for an MBAFF slice) that fits a workgroup's LDS -- a very wide MBAFF
+// picture is stored skip_coded instead of failing the whole file's launch.
+bool recodable_candidate(const avr::SliceInfo& s) {
+  const int cols = s.h.mbaff && !s.h.field_pic ? 3 * s.h.mb_width + 7 : s.h.mb_width;
+  return s.h.supported && s.size >= (size_t)avr::kSurrogateMarkerBytes && avr::shared_bytes(cols) <= kLdsBudget;
+}
 
 // find_next_coded_block_and_emit_literal (recode.cpp:1275-1297): slice i becomes a cabac block when
 // it is recodable (ok[i]), at least a surrogate marker long, and its payload occurs verbatim after
@@ -551,6 +594,29 @@ int emit_container(const uint8_t* in, size_t n, const ParsedFile& pf, const std:
 // device roundtrip), and the reference model runs all files in one pass (the parallel R-mode
 // pipeline over all their slices with per-file estimators, or one workgroup per file).  out[f] is
 // malloc'd; status[f] (optional) is file f's result; the return value is the first failure.
+// Host side of avr_phase_times for one whole-file call: the time before the first device pass is
+// demux, the wall time inside run_plan is the device passes (split by their HIP events, the rest
+// of it overhead), everything else container work.
+struct PhaseClock {
+  avr_ctx* c;
+  double t0, t_demux = -1;
+  explicit PhaseClock(avr_ctx* ctx) : c(ctx), t0(now_s()) {
+    c->phase = avr_phase_times{};
+    c->plan_wall = 0;
+  }
+  void mark_demux() {
+    if (t_demux < 0) t_demux = now_s() - t0;
+  }
+  void finish() {
+    mark_demux();
+    avr_phase_times& p = c->phase;
+    const double wall = now_s() - t0, dev = p.upload_s + p.kernel_s + p.download_s;
+    p.demux_s = t_demux;
+    p.container_s = std::max(0.0, wall - t_demux - c->plan_wall);
+    p.other_s = std::max(0.0, c->plan_wall - dev);
+  }
+};
+
 typedef std::array<uint64_t, 6> Bill;   // h264_model::bill / cabac_bill by avr_pip_coding_type
 void add_bill(Bill* b, const avr_slice_result& r) {
   for (int i = 0; i < 6; i++) (*b)[i] += r.bill[i];
@@ -564,6 +630,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
                    size_t* out_len, int32_t* status, std::vector<Bill>* bills = nullptr, bool verify = true) {
   if (bills) bills->assign(nf, Bill{});
   HIP_TRY(c, hipSetDevice(c->device));
+  PhaseClock pc(c);
   std::vector<int32_t> st(nf, AVR_OK);
   std::vector<ParsedFile> pf(nf);
   for (int f = 0; f < nf; f++) {
@@ -596,6 +663,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   }
   std::vector<avr_slice_result> res;
   std::vector<uint8_t> outb;
+  pc.mark_demux();
   if (int r = run_plan(c, 0, false, plan, &res, &outb, verify,
                        bills && model == AVR_MODEL_PARALLEL ? avr::kFlagBill : 0))
     return r;
@@ -632,8 +700,8 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
             d.payload_size = (uint32_t)s.size;
             d.read_limit = (uint32_t)s.read_limit;
             d.out_capacity = (uint32_t)(s.size * 4 + 4096);
+            rp.max_w = std::max(rp.max_w, ring_cols(d));   // uncoded slices only flip frames
           }
-          rp.max_w = std::max(rp.max_w, ring_cols(d));
           idx.push_back({f, (int)i});
           rp.descs.push_back(d);
         }
@@ -692,6 +760,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
     if (status) status[f] = st[f];
     if (st[f] && !first_err) first_err = st[f];
   }
+  pc.finish();
   return status ? AVR_OK : first_err;
 }
 
@@ -767,8 +836,10 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
   for (size_t k = 0; k < descs.size(); k++) {
     avr_slice_desc d = descs[k];
     const avr::PbBlock& b = j->blocks[block_of[k]];
-    if (d.coded) append_aligned(&plan->arena, b.cabac, b.cabac_len, 16, &d.payload_offset);
-    plan->max_w = std::max(plan->max_w, ring_cols(d));
+    if (d.coded) {
+      append_aligned(&plan->arena, b.cabac, b.cabac_len, 16, &d.payload_offset);
+      plan->max_w = std::max(plan->max_w, ring_cols(d));
+    }
     j->desc_of_block[block_of[k]] = (int)plan->descs.size();
     plan->descs.push_back(d);
   }
@@ -778,6 +849,7 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
 int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* in_len, uint8_t** out,
                      size_t* out_len, int32_t* status, std::vector<Bill>* bills = nullptr) {
   HIP_TRY(c, hipSetDevice(c->device));
+  PhaseClock pc(c);
   if (bills) bills->assign(nf, Bill{});
   const uint32_t flags = bills ? avr::kFlagBill : 0;
   std::vector<int32_t> st(nf, AVR_OK);
@@ -800,6 +872,7 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
   }
   std::vector<avr_slice_result> pres, rres;
   std::vector<uint8_t> pout, rout;
+  pc.mark_demux();
   if (!pp.descs.empty())
     if (int r = run_plan(c, 1, false, pp, &pres, &pout, false, flags)) return r;
   if (!rp.file_first.empty()) {
@@ -856,6 +929,7 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
     if (status) status[f] = st[f];
     if (st[f] && !first_err) first_err = st[f];
   }
+  pc.finish();
   return status ? AVR_OK : first_err;
 }
 
@@ -897,6 +971,12 @@ const char* avr_last_error(const avr_ctx* c) { return c ? c->err.c_str() : "no c
 
 void avr_free(void* p) { free(p); }
 
+int avr_last_phase_times(const avr_ctx* c, avr_phase_times* out) {
+  if (!c || !out) return AVR_ERR_INVALID_ARGUMENT;
+  *out = c->phase;
+  return AVR_OK;
+}
+
 int avr_neighbor_tables(avr_ctx* c, uint8_t out[96]) {
   if (!out) return AVR_ERR_INVALID_ARGUMENT;
   static_assert(offsetof(avr::HotTables, nb_up) == offsetof(avr::HotTables, nb_left) + 48, "nb_left, nb_up adjacent");
@@ -916,7 +996,7 @@ int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_
   if (!c || !in || !out || !out_len || (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL))
     return AVR_ERR_INVALID_ARGUMENT;
   int32_t st = 0;
-  const int r = compress_files(c, 1, &in, &n, model, out, out_len, &st);
+  const int r = guarded(c, [&] { return compress_files(c, 1, &in, &n, model, out, out_len, &st); });
   return r ? r : st;
 }
 
@@ -927,7 +1007,7 @@ int avr_compress_files(avr_ctx* c, int n_files, const uint8_t* const* in, const 
     return AVR_ERR_INVALID_ARGUMENT;
   for (int f = 0; f < n_files; f++)
     if (!in[f]) return AVR_ERR_INVALID_ARGUMENT;
-  return compress_files(c, n_files, in, in_len, model, out, out_len, status);
+  return guarded(c, [&] { return compress_files(c, n_files, in, in_len, model, out, out_len, status); });
 }
 
 int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
@@ -952,7 +1032,7 @@ int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const in
 int avr_decompress_file(avr_ctx* c, const uint8_t* in, size_t n, uint8_t** out, size_t* out_len) {
   if (!c || !in || !out || !out_len) return AVR_ERR_INVALID_ARGUMENT;
   int32_t st = 0;
-  const int r = decompress_files(c, 1, &in, &n, out, out_len, &st);
+  const int r = guarded(c, [&] { return decompress_files(c, 1, &in, &n, out, out_len, &st); });
   return r ? r : st;
 }
 
@@ -961,18 +1041,30 @@ int avr_decompress_files(avr_ctx* c, int n_files, const uint8_t* const* in, cons
   if (!c || n_files < 0 || (n_files && (!in || !in_len || !out || !out_len))) return AVR_ERR_INVALID_ARGUMENT;
   for (int f = 0; f < n_files; f++)
     if (!in[f]) return AVR_ERR_INVALID_ARGUMENT;
-  return decompress_files(c, n_files, in, in_len, out, out_len, status);
+  return guarded(c, [&] { return decompress_files(c, n_files, in, in_len, out, out_len, status); });
 }
 
+static int roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** compressed,
+                          size_t* compressed_len, avr_file_stats* stats);
 int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** compressed,
                        size_t* compressed_len, avr_file_stats* stats) {
+  return guarded(c, [&] { return roundtrip_file(c, in, n, model, compressed, compressed_len, stats); });
+}
+static int roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** compressed,
+                          size_t* compressed_len, avr_file_stats* stats) {
   if (!c || !in) return AVR_ERR_INVALID_ARGUMENT;
   if (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL) return AVR_ERR_INVALID_ARGUMENT;
   uint8_t *comp = nullptr, *dec = nullptr;
   size_t cn = 0, dn = 0;
   std::vector<Bill> cbill, dbill;
   int32_t st = 0;
-  double t0 = 0, t1 = 0, t2 = 0;
+  double tc = 0, td = 0;
+  avr_phase_times pcomp{}, pdec{};
+  uint32_t attempts = 0;
+  auto add_phases = [](avr_phase_times* a, const avr_phase_times& b) {
+    a->demux_s += b.demux_s, a->upload_s += b.upload_s, a->kernel_s += b.kernel_s;
+    a->download_s += b.download_s, a->container_s += b.container_s, a->other_s += b.other_s;
+  };
   bool same = false;
   // the parallel model's per-slice device check is left to the whole-file compare below; a file
   // that does not come back is compressed again with it (every slice that fails it stored as is)
@@ -980,7 +1072,8 @@ int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8
     free(comp);
     comp = nullptr;
     cn = 0;
-    t0 = now_s();
+    attempts++;
+    const double t0 = now_s();
     if (int r = compress_files(c, 1, &in, &n, model, &comp, &cn, &st, &cbill, /*verify=*/attempt > 0)) {
       free(comp);
       return r;
@@ -989,11 +1082,15 @@ int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8
       free(comp);
       return st;
     }
-    t1 = now_s();
+    const double t1 = now_s();
+    add_phases(&pcomp, c->phase);
     const uint8_t* cp = comp;
     int r = decompress_files(c, 1, &cp, &cn, &dec, &dn, &st, &dbill);
     if (!r) r = st;
-    t2 = now_s();
+    const double t2 = now_s();
+    add_phases(&pdec, c->phase);
+    tc += t1 - t0;
+    td += t2 - t1;
     same = !r && dn == n && memcmp(dec, in, n) == 0;
     free(dec);
     dec = nullptr;
@@ -1007,8 +1104,11 @@ int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8
   if (stats) {
     memset(stats, 0, sizeof(*stats));
     stats->file_bytes = n;
-    stats->compress_s = t1 - t0;
-    stats->decompress_s = t2 - t1;
+    stats->compress_s = tc;
+    stats->decompress_s = td;
+    stats->attempts = attempts;
+    stats->compress_phases = pcomp;
+    stats->decompress_phases = pdec;
     for (int i = 0; i < 6; i++) {
       stats->bill[i] = cbill[0][i];
       stats->cabac_bill[i] = dbill[0][i];
@@ -1204,7 +1304,11 @@ int avr_container_describe(const uint8_t* in, size_t n, char** json, uint8_t** r
   return AVR_OK;
 }
 
+static int synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t** out, size_t* out_len);
 int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t** out, size_t* out_len) {
+  return guarded(c, [&] { return synthesize_stream(c, p, n, out, out_len); });
+}
+static int synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t** out, size_t* out_len) {
   if (!c || !p || n <= 0 || !out || !out_len || p->mb_width <= 0 || p->mb_height <= 0 || p->slice_type < 0 ||
       p->slice_type > 2 || p->chroma_format_idc < 1 || p->chroma_format_idc > 3 || p->gop_length < 0 ||
       p->repeat < 0 || p->structure < 0 || p->structure > 3 || (p->structure && (p->mb_height & 1)))
@@ -1263,19 +1367,33 @@ int avr_synthesize_stream(avr_ctx* c, const avr_synth_params* p, int n, uint8_t*
   for (int i = 0; i < (int)plan.descs.size(); i++)
     if (res[i].status != 0) return fail(c, AVR_ERR_DEVICE, "generator failed on slice " + std::to_string(i));
   const int reps = std::max(1, p->repeat);
+  // the tiled stream goes straight into the caller's buffer (one copy of it in host memory): each
+  // NAL unit is written to a scratch vector and appended; 64 B per slice bound its header and
+  // start code (checked at every append)
   size_t bytes = 0;
   for (int i = 0; i < (int)plan.descs.size(); i++) bytes += res[i].out_len + 64;
-  if ((uint64_t)bytes * reps > ((uint64_t)1 << 36)) return fail(c, AVR_ERR_INVALID_ARGUMENT, "stream too large");
-  stream.reserve(bytes * reps + 256);
+  if ((uint64_t)bytes * reps > kMaxSynthBytes) return fail(c, AVR_ERR_INVALID_ARGUMENT, "stream too large");
+  const size_t cap = stream.size() + bytes * reps;
+  uint8_t* o = (uint8_t*)malloc(cap);
+  if (!o) return fail(c, AVR_ERR_OUT_OF_MEMORY, "synthetic stream: host allocation failed");
+  memcpy(o, stream.data(), stream.size());
+  size_t at = stream.size();
+  std::vector<uint8_t> nal;
   for (int t = 0; t < reps; t++)
-    for (int i = 0; i < (int)plan.descs.size(); i++)
-      avr::synth_write_slice(&stream, *p, plan.descs[i].slice_type, t * n + pic_of[i], plan.descs[i].structure,
+    for (int i = 0; i < (int)plan.descs.size(); i++) {
+      nal.clear();
+      avr::synth_write_slice(&nal, *p, plan.descs[i].slice_type, t * n + pic_of[i], plan.descs[i].structure,
                              paff && (i / spp) % 2 == 1, first_of[i], outb.data() + plan.descs[i].out_offset,
                              res[i].out_len);
-  *out = (uint8_t*)malloc(stream.size());
-  if (!*out) return AVR_ERR_OUT_OF_MEMORY;
-  memcpy(*out, stream.data(), stream.size());
-  *out_len = stream.size();
+      if (at + nal.size() > cap) {
+        free(o);
+        return fail(c, AVR_ERR_DEVICE, "synthetic stream: slice header larger than its bound");
+      }
+      memcpy(o + at, nal.data(), nal.size());
+      at += nal.size();
+    }
+  *out = o;
+  *out_len = at;
   return AVR_OK;
 }
 

@@ -1272,7 +1272,7 @@ struct Walker {
           if (absl >= 15) {
             int k = 0;
             while (bypass(SE_LEVEL_SUFFIX, k)) {
-              if (++k > 30) { err = -5; break; }
+              if (++k > 30) { err = AVR_SLICE_BAD_LEVEL; break; }
             }
             int v = 1;
             while (k-- > 0) v += v + bypass(SE_LEVEL_SUFFIX, 100);
@@ -1401,7 +1401,7 @@ struct Walker {
     while (bin(SE_REF, ref, 54 + ctx)) {
       ref++;
       ctx = (ctx >> 2) + 4;
-      if (ref >= 32) { err = -3; return 0; }
+      if (ref >= 32) { err = AVR_SLICE_BAD_REF_IDX; return 0; }
     }
     return ref;
   }
@@ -1427,7 +1427,7 @@ struct Walker {
       int k = 3;
       while (bypass(SE_MVD_SUFFIX, k - 3)) {
         mvd += 1 << k;
-        if (++k > 24) { err = -4; return 0; }
+        if (++k > 24) { err = AVR_SLICE_BAD_MVD; return 0; }
       }
       while (k--) mvd += bypass(SE_MVD_SUFFIX, 100) << k;
     }
@@ -1542,7 +1542,7 @@ struct Walker {
     }
     SPROF_END(2, ps2);
     if (err) return;
-    if (intra && kind == 2) { err = -2; return; }  // I_PCM (skip_bytes hook, recode.cpp:161-163)
+    if (intra && kind == 2) { err = AVR_SLICE_PCM; return; }  // I_PCM (skip_bytes hook, recode.cpp:161-163)
     int no_sub_lt8x8 = 1;
     int t8 = 0;
     PROF_BEGIN(ps3);
@@ -1697,7 +1697,7 @@ struct Walker {
       int ctx = last_dqp_nz ? 1 : 0, val = 0;
       while (bin(SE_QPDELTA, val, 60 + ctx)) {
         ctx = ctx < 2 ? 2 : 3;
-        if (++val > 102) { err = -6; return; }
+        if (++val > 102) { err = AVR_SLICE_BAD_QP_DELTA; return; }
       }
       last_dqp_nz = val != 0;
       SPROF_END(6, ps6);
@@ -1775,7 +1775,7 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
   w.mbaff = FLD && d->structure == AVR_STRUCT_MBAFF;
   w.pst = 0;
   if ((FLD && w.mbaff)) {   // pairs in raster order: mb_y = pair row, my = 2 mb_y + bottom
-    if ((int)w.ring_cols < 3 * w.W + 7 || (addr & 1)) { w.err = -20; return; }
+    if ((int)w.ring_cols < 3 * w.W + 7 || (addr & 1)) { w.err = AVR_SLICE_MBAFF_RING; return; }
     w.mb_x = (addr >> 1) % w.W;
     w.mb_y = (addr >> 1) / w.W;
     w.ystep = 2;
@@ -1792,7 +1792,7 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
     w.edge_src = (uint32_t)src;
   }
   for (;;) {
-    if (addr >= npic) { w.err = -7; break; }
+    if (addr >= npic) { w.err = AVR_SLICE_BAD_MB_ADDR; break; }
     PROF_BEGINW(ps0);
     if (!(FLD && w.mbaff)) {
       w.left_ok = w.mb_x > 0 && addr - 1 >= w.first_mb;
@@ -1864,7 +1864,7 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
     const int eos = (!(FLD && w.mbaff) || (w.pst & Walker<MODE, RM, FLD>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
     SPROF_ENDW(7, ps7);
     if (eos) break;
-    if (Walker<MODE, RM, FLD>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = -8; break; }
+    if (Walker<MODE, RM, FLD>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = AVR_SLICE_OVERREAD; break; }
     addr++;
     if ((FLD && w.mbaff) && !(w.pst & Walker<MODE, RM, FLD>::PST_BOT)) {
       w.pst |= Walker<MODE, RM, FLD>::PST_BOT;
@@ -1965,7 +1965,7 @@ AVR_FI void walker_slice(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, cons
 #endif
   w.publish();
   int status = w.err;
-  if (!status && !w.finished) status = -9;
+  if (!status && !w.finished) status = AVR_SLICE_NO_END;
   int stop_ok = 1;
   if (MODE == MODE_COMPRESS && !status) {
     // predicted decompressor output (recode.cpp:1345-1356, 1503-1505): the regenerated CABAC
@@ -2267,9 +2267,9 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
 template <int MODE>
 AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_result* res) {
   int status = sh->p_status;
-  if (sh->c_err) status = -10;
-  if (MODE == MODE_COMPRESS && !status && !sh->p_stop_ok) status = -11;
-  if (sh->c_len > d->out_capacity) status = -12;
+  if (sh->c_err) status = AVR_SLICE_CODER;
+  if (MODE == MODE_COMPRESS && !status && !sh->p_stop_ok) status = AVR_SLICE_NO_STOP;
+  if (sh->c_len > d->out_capacity) status = AVR_SLICE_OVERFLOW;
   uint32_t len = sh->c_len;
   if (MODE == MODE_DECOMPRESS && !status && len && sh->c_last == 0x80) len--;  // recode.cpp:1503-1505
   res->out_len = len;
@@ -2286,9 +2286,9 @@ AVR_FI void run_slice_inline(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, 
   w.rc_writeback();
   w.mc_store();
   int status = w.err;
-  if (!status && !w.finished) status = -9;
-  if (MODE == MODE_GENERATE && w.ce.err) status = -10;
-  if (out_overflow(w.out)) status = -12;
+  if (!status && !w.finished) status = AVR_SLICE_NO_END;
+  if (MODE == MODE_GENERATE && w.ce.err) status = AVR_SLICE_CODER;
+  if (out_overflow(w.out)) status = AVR_SLICE_OVERFLOW;
   if (__lane_id() == 0) {
     res->out_len = out_total(w.out);
     res->status = status;

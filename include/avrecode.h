@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define AVRECODE_ABI_VERSION 2
+#define AVRECODE_ABI_VERSION 3
 
 typedef enum {
   AVR_OK = 0,
@@ -74,22 +74,46 @@ int avr_decompress_file(avr_ctx* ctx, const uint8_t* in, size_t n, uint8_t** out
  * workgroup (wavefront) per file; parallel-model slices of all files run one wavefront each.
  * out[f] / out_len[f]: file f's result (malloc'd, avr_free; NULL on failure).  status (optional,
  * n_files entries) receives each file's status and the call returns AVR_OK unless the batch as a
- * whole failed; without it the call returns the first file failure.  Output bytes equal
+ * whole failed; without it the call returns the first file failure -- and out[f] is still set for
+ * every file that succeeded, so the caller frees every non-NULL out[f] whatever the call returns.
+ * avr_last_error holds one message: the last failing file's.  Output bytes equal
  * avr_compress_file / avr_decompress_file on each file alone. */
 int avr_compress_files(avr_ctx* ctx, int n_files, const uint8_t* const* in, const size_t* in_len, int model,
                        uint8_t** out, size_t* out_len, int32_t* status);
 int avr_decompress_files(avr_ctx* ctx, int n_files, const uint8_t* const* in, const size_t* in_len, uint8_t** out,
                          size_t* out_len, int32_t* status);
 
+/* Where the wall time of a whole-file call goes (seconds).  Host phases by wall clock, device
+ * phases by HIP events on the context's stream (summed over the call's device passes):
+ *   demux_s      compress: demux, NAL unescape, parameter-set / slice-header parse, plan building;
+ *                decompress: container parse, surrogate stream, header parse, plan building
+ *   upload_s     host -> device copies of payloads / re-coded streams and descriptors
+ *   kernel_s     the device passes (slice kernels, schedule, R-mode scan / sort / coder, verify)
+ *   download_s   device -> host copies of results and outputs
+ *   container_s  compress: segmentation + Recoded protobuf (and the reference model's re-plans);
+ *                decompress: splicing literals + regenerated slices, last-byte patch
+ *   other_s      the rest of the call's wall time (allocation, launch and synchronisation
+ *                overhead) */
+typedef struct {
+  double demux_s, upload_s, kernel_s, download_s, container_s, other_s;
+} avr_phase_times;
+
 typedef struct {
   uint64_t file_bytes, slices, coded_slices, skipped_slices, payload_bytes, recoded_bytes, bins;
-  double compress_s, decompress_s;  /* wall time of the two halves (host + device) */
+  double compress_s, decompress_s;  /* wall time of the two halves (host + device), summed over attempts */
   /* h264_model::bill / cabac_bill (recode.cpp:615-661), indexed by avr_pip_coding_type: bytes the
    * re-coded encoder emitted per put during compress (recode.cpp:1074-1078, 1213-1220) and bytes
    * the CABAC encoder emitted per put during decompress (1443-1446, 1455-1457, 1466-1468), summed
    * over the file's coded slices (the parallel model's per-slice models included). */
   uint64_t bill[6], cabac_bill[6];
+  /* compress + decompress passes the roundtrip took: 1, or 2 when the parallel model's unverified
+   * first pass did not come back and the file was compressed again with the per-slice check */
+  uint32_t attempts, reserved;
+  avr_phase_times compress_phases, decompress_phases;   /* summed over attempts */
 } avr_file_stats;
+/* The phase breakdown of the last whole-file call on ctx (avr_compress_file(s),
+ * avr_decompress_file(s), avr_roundtrip_file: its last decompress). */
+int avr_last_phase_times(const avr_ctx* ctx, avr_phase_times* out);
 /* compress, decompress, compare (recode.cpp:1594-1624).  Returns AVR_ERR_ROUNDTRIP on mismatch. */
 int avr_roundtrip_file(avr_ctx* ctx, const uint8_t* in, size_t n, int model, uint8_t** compressed,
                        size_t* compressed_len, avr_file_stats* stats);
@@ -114,9 +138,27 @@ typedef struct {
 } avr_slice_desc;
 enum { AVR_STRUCT_FRAME = 0, AVR_STRUCT_TOP_FIELD = 1, AVR_STRUCT_BOTTOM_FIELD = 2, AVR_STRUCT_MBAFF = 3 };
 
+/* avr_slice_result.status: 0, or why the slice cannot be coded (the container stores it skip_coded) */
+enum {
+  AVR_SLICE_OK = 0,
+  AVR_SLICE_PCM = -2,             /* I_PCM macroblock (skip_bytes; the reference throws, recode.cpp:161-163) */
+  AVR_SLICE_BAD_REF_IDX = -3,     /* ref_idx unary prefix past 32 */
+  AVR_SLICE_BAD_MVD = -4,         /* mvd suffix exponent past 24 */
+  AVR_SLICE_BAD_LEVEL = -5,       /* coeff_abs_level_minus1 suffix exponent past 30 */
+  AVR_SLICE_BAD_QP_DELTA = -6,    /* mb_qp_delta past 102 */
+  AVR_SLICE_BAD_MB_ADDR = -7,     /* macroblock address past the picture */
+  AVR_SLICE_OVERREAD = -8,        /* the parse ran past the payload */
+  AVR_SLICE_NO_END = -9,          /* the walk ended without end_of_slice_flag = 1 */
+  AVR_SLICE_CODER = -10,          /* coder invariant violated (carry into an emitted byte: corrupt input) */
+  AVR_SLICE_NO_STOP = -11,        /* compress: a CABAC re-encode would not restore the payload (last-byte rule) */
+  AVR_SLICE_OVERFLOW = -12,       /* output past out_capacity */
+  AVR_SLICE_MBAFF_RING = -20,     /* MBAFF slice launched with max_mb_width < 3 * mb_width + 7 */
+  AVR_SLICE_NO_ROUNDTRIP = -21    /* file calls: the device roundtrip check did not regenerate the payload */
+};
+
 typedef struct {
   uint32_t out_len;          /* bytes written at out_offset */
-  int32_t status;            /* 0 ok, <0 parse/overflow error (slice must be stored skip_coded) */
+  int32_t status;            /* AVR_SLICE_*: 0 ok, < 0 the slice must be stored skip_coded */
   uint32_t bins;             /* CABAC bins processed */
   uint32_t mbs;              /* macroblocks parsed */
   /* h264_model billing of this slice by avr_pip_coding_type (recode.cpp:615-661), filled only
