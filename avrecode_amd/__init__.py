@@ -21,7 +21,8 @@ import numpy as np
 
 __all__ = [
     "AvrError", "Context", "MODEL_REFERENCE", "MODEL_PARALLEL", "SLICE_DESC", "SLICE_RESULT",
-    "SynthParams", "lib", "parse_stream", "assemble_container", "neighbor_tables", "library_path", "EXPORTED_SYMBOLS",
+    "SynthParams", "lib", "parse_stream", "assemble_container", "neighbor_tables",
+    "plan_decompress", "splice_container", "library_path", "EXPORTED_SYMBOLS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -47,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "avr_hook_get_bypass", "avr_hook_get_terminate", "avr_hook_skip_bytes", "avr_hook_frame_spec", "avr_hook_mb_xy",
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
     "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables", "avr_last_phase_times",
+    "avr_plan_decompress", "avr_splice_container",
 )
 
 # avr_slice_desc / avr_slice_result (include/avrecode.h), C layout
@@ -156,6 +158,8 @@ def lib() -> ctypes.CDLL:
     L.avr_compress_files.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
     L.avr_decompress_files.argtypes = [vp, i32, vp, vp, vp, vp, vp]
     L.avr_neighbor_tables.argtypes = [vp, vp]
+    L.avr_plan_decompress.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
+    L.avr_splice_container.argtypes = [vp, sz, i32, vp, vp, vp, vp, pp, psz]
     L.avr_last_phase_times.argtypes = [vp, vp]
     for name in EXPORTED_SYMBOLS:   # fails here, not at first use, when the build is stale
         getattr(L, name)
@@ -210,6 +214,41 @@ def parse_stream(data) -> ParsedStream:
     d = np.frombuffer(_take(descs, ns.value * SLICE_DESC.itemsize), dtype=SLICE_DESC).copy()
     a = np.frombuffer(_take(arena, alen.value), dtype=np.uint8).copy()
     return ParsedStream(d, a, int(wlen.value), int(mw.value), int(mh.value))
+
+
+def plan_decompress(avrc) -> ParsedStream:
+    """A PARALLEL-model container's coded slices as a decompress batch (avr_plan_decompress): the
+    descs' payloads are the re-coded streams, their outputs the regenerated CABAC bytes.  Host only."""
+    L = lib()
+    p, n, keep = _buf(avrc)
+    descs, arena = ctypes.c_void_p(), ctypes.c_void_p()
+    ns, mw, mh = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    alen, wlen = ctypes.c_size_t(), ctypes.c_size_t()
+    r = L.avr_plan_decompress(p, n, ctypes.byref(descs), ctypes.byref(ns), ctypes.byref(arena), ctypes.byref(alen),
+                              ctypes.byref(wlen), ctypes.byref(mw), ctypes.byref(mh))
+    del keep
+    if r != AVR_OK:
+        raise AvrError(r, "avr_plan_decompress failed")
+    d = np.frombuffer(_take(descs, ns.value * SLICE_DESC.itemsize), dtype=SLICE_DESC).copy()
+    a = np.frombuffer(_take(arena, alen.value), dtype=np.uint8).copy()
+    return ParsedStream(d, a, int(wlen.value), int(mw.value), int(mh.value))
+
+
+def splice_container(avrc, status: np.ndarray, regen: bytes, offsets: np.ndarray, lens: np.ndarray) -> bytes:
+    """The original file from a PARALLEL-model container and its slices' regenerated bytes
+    (avr_splice_container; last-byte patch applied here).  Host only."""
+    L = lib()
+    p, n, keep = _buf(avrc)
+    st = np.ascontiguousarray(status, dtype=np.int32)
+    of = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint32)
+    rp, _, keep2 = _buf(regen)
+    out, olen = ctypes.c_void_p(), ctypes.c_size_t()
+    r = L.avr_splice_container(p, n, len(st), st.ctypes.data, rp, of.ctypes.data, ln.ctypes.data,
+                               ctypes.byref(out), ctypes.byref(olen))
+    if r != AVR_OK:
+        raise AvrError(r, "avr_splice_container failed")
+    return _take(out, olen.value)
 
 
 def assemble_container(data, status: np.ndarray, recoded: bytes, offsets: np.ndarray, lens: np.ndarray) -> bytes:

@@ -60,13 +60,21 @@ class DeviceBatch:
         self.ctx.compress_slices(self.d_desc, self.n, self.ps.max_mb_width, self.ps.max_mb_height, self.d_in,
                                  self.d_work, self.d_res_c, model, stream)
 
-    def pack(self, stream=None):
-        """Compress outputs packed contiguously on the device (avr_pack_outputs): (d_packed uint8,
-        d_offsets uint64[n + 1]); slice k's re-coded bytes (compress status 0) start at offsets[k]."""
+    def decompress(self, model: int = MODEL_PARALLEL, stream=None):
+        """A decompress batch (ps from plan_decompress: payloads = re-coded streams): d_in -> d_work,
+        results in d_res_d (avr_decompress_slices)."""
+        self.ctx.decompress_slices(self.d_desc, self.n, self.ps.max_mb_width, self.ps.max_mb_height, self.d_in,
+                                   self.d_work, self.d_res_d, model, stream)
+
+    def pack(self, stream=None, which: str = "c"):
+        """d_work's per-slice outputs packed contiguously on the device (avr_pack_outputs) by the
+        compress ("c") or decompress ("d") results: (d_packed uint8, d_offsets uint64[n + 1]); slice
+        k's bytes (status 0) start at offsets[k]."""
         if not hasattr(self, "d_packed"):
             self.d_packed = torch.zeros(max(16, self.ps.work_len + 16), dtype=torch.uint8, device=self.device)
             self.d_offsets = torch.zeros(max(1, self.n) + 1, dtype=torch.int64, device=self.device)
-        self.ctx.pack_outputs(self.d_desc, self.d_res_c, self.n, self.d_work, self.d_packed, self.d_offsets, stream)
+        res = self.d_res_c if which == "c" else self.d_res_d
+        self.ctx.pack_outputs(self.d_desc, res, self.n, self.d_work, self.d_packed, self.d_offsets, stream)
         return self.d_packed, self.d_offsets
 
     # ----------------------------------------------------------------- results (host copies)

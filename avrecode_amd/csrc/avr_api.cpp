@@ -846,6 +846,44 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
   return AVR_OK;
 }
 
+// decompressor::run's output (recode.cpp:1338-1357): the literals and the regenerated slices in
+// block order, each slice patched by the last-byte rule (x264 padding correction, 1345-1356).
+// slice(k, &p, &len) gives plan slice k's regenerated bytes and returns its status.
+template <class Slice>
+int splice_job(avr_ctx* c, const DecJob& j, Slice&& slice, std::vector<uint8_t>* o) {
+  o->reserve(j.stream.size());
+  for (size_t i = 0; i < j.blocks.size(); i++) {
+    const avr::PbBlock& b = j.blocks[i];
+    if (b.has_literal) {
+      o->insert(o->end(), b.literal, b.literal + b.literal_len);
+      continue;
+    }
+    if (!b.has_cabac) continue;
+    const int k = j.desc_of_block[i];
+    if (k < 0) return fail(c, AVR_ERR_FORMAT, "Not all blocks were decoded.");
+    const uint8_t* p = nullptr;
+    size_t len = 0;
+    if (int stt = slice(k, &p, &len))
+      return fail(c, AVR_ERR_FORMAT, "slice " + std::to_string(k) + " failed to decode (" + std::to_string(stt) + ")");
+    const size_t o0 = o->size();
+    o->insert(o->end(), p, p + len);
+    if (b.has_parity && b.has_last_byte && !b.last_byte.empty()) {
+      const size_t n = o->size() - o0;
+      if ((int)b.length_parity != (int)(n & 1)) o->push_back((uint8_t)b.last_byte[0]);
+      else if (n) o->back() = (uint8_t)b.last_byte[0];
+    }
+  }
+  return AVR_OK;
+}
+
+int malloc_copy(const std::vector<uint8_t>& v, uint8_t** out, size_t* out_len) {
+  *out = (uint8_t*)malloc(v.size() ? v.size() : 1);
+  if (!*out) return AVR_ERR_OUT_OF_MEMORY;
+  if (!v.empty()) memcpy(*out, v.data(), v.size());
+  *out_len = v.size();
+  return AVR_OK;
+}
+
 int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* in_len, uint8_t** out,
                      size_t* out_len, int32_t* status, std::vector<Bill>* bills = nullptr) {
   HIP_TRY(c, hipSetDevice(c->device));
@@ -886,37 +924,13 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
     const std::vector<avr_slice_result>& res = j.parallel ? pres : rres;
     const std::vector<uint8_t>& outb = j.parallel ? pout : rout;
     std::vector<uint8_t> o;
-    if (st[f] == AVR_OK) {
-      o.reserve(j.stream.size());
-      for (size_t i = 0; i < j.blocks.size() && st[f] == AVR_OK; i++) {
-        const avr::PbBlock& b = j.blocks[i];
-        if (b.has_literal) {
-          o.insert(o.end(), b.literal, b.literal + b.literal_len);
-          continue;
-        }
-        if (!b.has_cabac) continue;
-        const int k = j.desc_of_block[i];
-        if (k < 0) {
-          st[f] = fail(c, AVR_ERR_FORMAT, "Not all blocks were decoded.");
-          break;
-        }
-        if (res[k].status != 0) {
-          st[f] = fail(c, AVR_ERR_FORMAT, "slice " + std::to_string(k) + " failed to decode (" +
-                                              std::to_string(res[k].status) + ")");
-          break;
-        }
-        const size_t o0 = o.size();
-        o.insert(o.end(), outb.begin() + plan.descs[k].out_offset,
-                 outb.begin() + plan.descs[k].out_offset + res[k].out_len);
-        if (bills) add_bill(&(*bills)[f], res[k]);
-        // x264 padding correction (recode.cpp:1345-1356)
-        if (b.has_parity && b.has_last_byte && !b.last_byte.empty()) {
-          const size_t len = o.size() - o0;
-          if ((int)b.length_parity != (int)(len & 1)) o.push_back((uint8_t)b.last_byte[0]);
-          else if (len) o.back() = (uint8_t)b.last_byte[0];
-        }
-      }
-    }
+    if (st[f] == AVR_OK)
+      st[f] = splice_job(c, j, [&](int k, const uint8_t** p, size_t* len) {
+        *p = outb.data() + plan.descs[k].out_offset;
+        *len = res[k].out_len;
+        if (bills && res[k].status == 0) add_bill(&(*bills)[f], res[k]);
+        return res[k].status;
+      }, &o);
     if (st[f] == AVR_OK) {
       out[f] = (uint8_t*)malloc(o.size() ? o.size() : 1);
       if (!out[f]) {
@@ -970,6 +984,64 @@ void avr_destroy(avr_ctx* c) {
 const char* avr_last_error(const avr_ctx* c) { return c ? c->err.c_str() : "no context"; }
 
 void avr_free(void* p) { free(p); }
+
+int avr_plan_decompress(const uint8_t* avrc, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
+                        size_t* arena_len, size_t* work_len, int* max_mb_width, int* max_mb_height) {
+  if (!avrc || !descs || !n_slices || !arena || !arena_len || !work_len || !max_mb_width || !max_mb_height)
+    return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(nullptr, [&]() -> int {
+    DecJob j;
+    Plan plan;
+    if (int r = decompress_setup(nullptr, avrc, n, &j, &plan)) return r;
+    if (!j.parallel) return AVR_ERR_UNSUPPORTED;   // the reference model's slices chain: no split
+    uint64_t w = 0;
+    int mh = 1;
+    for (auto& d : plan.descs) {
+      d.out_offset = w;
+      w += ((uint64_t)d.out_capacity + 15) & ~15ull;
+      mh = std::max(mh, d.mb_height);
+    }
+    plan.arena.resize(plan.arena.size() + 16, 0);
+    *descs = (avr_slice_desc*)malloc(sizeof(avr_slice_desc) * std::max<size_t>(1, plan.descs.size()));
+    *arena = (uint8_t*)malloc(plan.arena.size());
+    if (!*descs || !*arena) {
+      free(*descs);
+      free(*arena);
+      *descs = nullptr;
+      *arena = nullptr;
+      return AVR_ERR_OUT_OF_MEMORY;
+    }
+    if (!plan.descs.empty()) memcpy(*descs, plan.descs.data(), sizeof(avr_slice_desc) * plan.descs.size());
+    memcpy(*arena, plan.arena.data(), plan.arena.size());
+    *n_slices = (int)plan.descs.size();
+    *arena_len = plan.arena.size();
+    *work_len = w;
+    *max_mb_width = plan.max_w;
+    *max_mb_height = mh;
+    return AVR_OK;
+  });
+}
+
+int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int32_t* status, const uint8_t* regen,
+                         const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len) {
+  if (!avrc || n_slices < 0 || (n_slices && (!status || !regen || !offsets || !lens)) || !out || !out_len)
+    return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(nullptr, [&]() -> int {
+    DecJob j;
+    Plan plan;
+    if (int r = decompress_setup(nullptr, avrc, n, &j, &plan)) return r;
+    if (!j.parallel) return AVR_ERR_UNSUPPORTED;
+    if ((int)plan.descs.size() != n_slices) return AVR_ERR_INVALID_ARGUMENT;
+    std::vector<uint8_t> o;
+    if (int r = splice_job(nullptr, j, [&](int k, const uint8_t** p, size_t* len) {
+          *p = regen + offsets[k];
+          *len = lens[k];
+          return (int)status[k];
+        }, &o))
+      return r;
+    return malloc_copy(o, out, out_len);
+  });
+}
 
 int avr_last_phase_times(const avr_ctx* c, avr_phase_times* out) {
   if (!c || !out) return AVR_ERR_INVALID_ARGUMENT;

@@ -1,18 +1,25 @@
-"""Multi-GPU sharding of the PARALLEL model: one process per GPU.
+"""Multi-GPU sharding: one process per GPU.
 
-Every slice is an independent unit in the parallel model (fresh CABAC contexts per H.264 9.3.1,
-fresh re-coded coder per slice, recode.cpp:1263/1422, model reset per slice), so a file's slices
-are cut into contiguous ranges balanced by payload bytes, one range per rank.  The only
-collective is the final gather of the variable-length re-coded blocks to rank 0 (point-to-point
-send/recv over xGMI with backend "nccl" = RCCL; CPU tensors with "gloo"), where the host builds
-the Recoded container (avr_assemble_container).  The reference model has no such split: its
-estimators carry across slices (recode.cpp:662-665), so it runs as replicas only.
+PARALLEL model, one file over the ranks, both directions.  Every slice is an independent unit
+(fresh CABAC contexts per H.264 9.3.1, fresh re-coded coder per slice, recode.cpp:1263/1422, model
+reset per slice), so a file's slices are cut into contiguous ranges balanced by bytes, one range
+per rank.  The only collective is the final gather of the variable-length per-slice outputs to
+rank 0 (point-to-point send/recv over xGMI with backend "nccl" = RCCL; CPU tensors with "gloo"):
+  sharded_compress    re-coded blocks -> rank 0 builds the Recoded container (avr_assemble_container)
+  sharded_decompress  regenerated CABAC payloads -> rank 0 splices them with the container's
+                      literals and applies the last-byte patch (avr_splice_container)
+Both are byte-identical to the single-GPU calls.
+
+A corpus of files (BASELINE configs[4]): files are dealt to ranks whole (deal_files, LPT by
+bytes) and each rank runs its files through the batched corpus calls; the reference model's
+unit of sequential work is a file (its estimators carry across slices, recode.cpp:662-665), so
+this is also the reference model's only split -- replicas over files.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from . import MODEL_PARALLEL, ParsedStream, assemble_container, parse_stream
+from . import MODEL_PARALLEL, ParsedStream, assemble_container, parse_stream, plan_decompress, splice_container
 
 
 def partition(sizes, world: int) -> list[tuple[int, int]]:
@@ -127,11 +134,7 @@ def sharded_compress(ctx, data: bytes, device=None, ps: ParsedStream | None = No
     ps = ps if ps is not None else parse_stream(data)
     lo, hi = partition(ps.descs["payload_size"], world)[rank]
     part = subset(ps, lo, hi)
-    # RCCL ("nccl") moves device tensors only; gloo moves host tensors
-    if dist.get_backend() == "nccl":
-        dev = device if device is not None else torch.device("cuda", ctx.device)
-    else:
-        dev = torch.device("cpu")
+    dev = _gather_device(ctx, device)
     if hi > lo:
         b = DeviceBatch(ctx, part)
         b.roundtrip(MODEL_PARALLEL)
@@ -151,3 +154,98 @@ def sharded_compress(ctx, data: bytes, device=None, ps: ParsedStream | None = No
         return None
     st, blob, offs, lens = g
     return assemble_container(data, st, blob, offs, lens)
+
+
+def _gather_device(ctx, device):
+    import torch
+    import torch.distributed as dist
+    # RCCL ("nccl") moves device tensors only; gloo moves host tensors
+    if dist.get_backend() == "nccl":
+        return device if device is not None else torch.device("cuda", ctx.device)
+    return torch.device("cpu")
+
+
+def decompress_range(ctx, part: ParsedStream, device=None):
+    """This rank's slice range of a sharded decompress on its GPU: (flat uint8 tensor, status,
+    offsets, lens) with slice k's regenerated bytes at flat[offsets[k] : offsets[k] + lens[k]]
+    (packed on the device, avr_pack_outputs)."""
+    import torch
+
+    from .batch import DeviceBatch
+
+    b = DeviceBatch(ctx, part, device=device)
+    b.decompress(MODEL_PARALLEL)
+    flat, d_off = b.pack(which="d")
+    torch.cuda.synchronize()
+    res = b.results("d")
+    n = len(part.descs)
+    offs = d_off.cpu().numpy()[:n].astype(np.int64)
+    status = res["status"].astype(np.int64)
+    lens = np.where(status == 0, res["out_len"], 0).astype(np.int64)
+    return flat, status, offs, lens
+
+
+def sharded_decompress(ctx, avrc: bytes, device=None, run_range=None) -> bytes | None:
+    """PARALLEL-model decompress of one container across all ranks; the file is returned on rank 0.
+
+    Every rank plans the container (host: avr_plan_decompress), takes its contiguous range of
+    coded slices balanced by re-coded bytes (partition), regenerates them on its GPU
+    (decompress_range: avr_decompress_slices + avr_pack_outputs), and sends the packed payloads to
+    rank 0 (gather_flat over RCCL), which splices them with the literals and applies the last-byte
+    patch (avr_splice_container, recode.cpp:1338-1357).  Byte-identical to ctx.decompress(avrc).
+    run_range(part) -> (flat, status, offsets, lens) replaces the device step (CPU tests)."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    plan = plan_decompress(avrc)
+    lo, hi = partition(plan.descs["payload_size"], world)[rank]
+    part = subset(plan, lo, hi)
+    dev = _gather_device(ctx, device)
+    if hi > lo:
+        flat, status, offs, lens = (run_range or (lambda p: decompress_range(ctx, p, device)))(part)
+    else:
+        flat = torch.zeros(16, dtype=torch.uint8, device=dev)
+        offs = lens = status = np.zeros(0, np.int64)
+    g = gather_flat(flat, status, offs, lens, dst=0, device=dev)
+    if g is None:
+        return None
+    st, blob, offs, lens = g
+    return splice_container(avrc, st, blob, offs, lens)
+
+
+def deal_files(sizes, world: int) -> list[list[int]]:
+    """Files to ranks, whole: longest-processing-time-first by bytes (the largest file goes to the
+    least-loaded rank).  Returns each rank's file indices in ascending order."""
+    sizes = [int(x) for x in sizes]
+    load = [0] * max(1, world)
+    owned = [[] for _ in range(max(1, world))]
+    for f in sorted(range(len(sizes)), key=lambda i: (-sizes[i], i)):
+        r = min(range(len(load)), key=lambda q: (load[q], q))
+        load[r] += sizes[f]
+        owned[r].append(f)
+    return [sorted(o) for o in owned]
+
+
+def corpus_roundtrip(ctx, files: list[bytes], model: int, dst: int = 0):
+    """A corpus over the ranks (BASELINE configs[4]): this rank's files (deal_files) compressed
+    and decompressed as one batch each (avr_compress_files / avr_decompress_files) and checked
+    byte for byte.  Returns (files done here, bytes in, container bytes, all files bit-exact here);
+    the callers reduce these over ranks."""
+    rank, world = _rank_world()
+    mine = deal_files([len(f) for f in files], world)[rank]
+    if not mine:
+        return 0, 0, 0, True
+    sub = [files[i] for i in mine]
+    comp = ctx.compress_files(sub, model)
+    ok = not any(isinstance(c, Exception) for c in comp)
+    dec = ctx.decompress_files([c for c in comp if not isinstance(c, Exception)]) if ok else []
+    ok = ok and all(not isinstance(d, Exception) and d == f for d, f in zip(dec, sub))
+    return len(sub), sum(map(len, sub)), sum(len(c) for c in comp if not isinstance(c, Exception)), ok
+
+
+def _rank_world():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1

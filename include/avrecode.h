@@ -225,6 +225,21 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
 int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
                            const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len);
 
+/* Sharded PARALLEL-model decompress (decompressor::run, recode.cpp:1312-1357, split over ranks).
+ * avr_plan_decompress: the container's coded slices as a decompress batch, host only -- *descs
+ * (n entries, in container order; payload_offset / read_limit / payload_size index *arena = the
+ * re-coded streams, out_offset / out_capacity index a work buffer of *work_len bytes for the
+ * regenerated CABAC bytes) for avr_decompress_slices on any rank's slice range.  Returns
+ * AVR_ERR_UNSUPPORTED for a reference-model container (its slices chain: replicas only).
+ * avr_splice_container (rank 0): the original file from the container's literals and slice k's
+ * regenerated bytes regen[offsets[k] .. + lens[k]) (avr_decompress_slices output before the
+ * last-byte patch, which this applies, recode.cpp:1345-1356); status[k] != 0 fails the file with
+ * AVR_ERR_FORMAT.  Byte-identical to avr_decompress_file. */
+int avr_plan_decompress(const uint8_t* avrc, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
+                        size_t* arena_len, size_t* work_len, int* max_mb_width, int* max_mb_height);
+int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int32_t* status, const uint8_t* regen,
+                         const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len);
+
 /* Container codec check (host only): parse a Recoded protobuf (recode.proto:1-19) with the
  * library's own wire codec -- the one avr_decompress_file uses -- and return (a) its fields as JSON,
  * {"version": null | hex, "blocks": [{"size": int, "literal": hex, "skip_coded": bool, "cabac": hex,

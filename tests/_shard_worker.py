@@ -1,5 +1,6 @@
-"""World-N worker for tests/test_gpu_cli.py::test_sharded_compress_world2_gloo (one process per rank,
-all on cuda:0, gloo for the gather): sharded_compress of one file; rank 0 writes the container."""
+"""World-N worker for tests/test_gpu_cli.py::test_sharded_compress_multirank_gloo (one process per rank,
+all on cuda:0, gloo for the gather): sharded_compress of one file (rank 0 writes the container to
+dst) and sharded_decompress of the single-GPU container (rank 0 writes the file to dst + ".dec")."""
 import os
 import sys
 from pathlib import Path
@@ -22,6 +23,13 @@ def main(src: str, dst: str) -> None:
                 Path(dst).write_bytes(out)
             else:
                 assert out is None
+            # every rank decompresses its slice range of the single-GPU container (the same bytes)
+            avrc = ctx.compress(Path(src).read_bytes(), avr.MODEL_PARALLEL)
+            dec = shard.sharded_decompress(ctx, avrc)
+            if dist.get_rank() == 0:
+                Path(dst + ".dec").write_bytes(dec)
+            else:
+                assert dec is None
     finally:
         dist.destroy_process_group()
 

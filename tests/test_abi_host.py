@@ -143,3 +143,116 @@ def test_gloo_world2_sharded_assembly(name):
         mp.spawn(_gloo_worker, args=(2, port, name, td), nprocs=2, join=True)
         c = open(os.path.join(td, "out.avrc"), "rb").read()
     assert hashlib.sha256(c).hexdigest() == GOLD[(name, "P")]["avrc_sha256"]
+
+
+# ------------------------------------------------------------- sharded decompress (host side)
+def _container_payloads(data: bytes, avrc: bytes) -> list[bytes]:
+    """The original payload bytes of each cabac block of a container, in block order (a coded
+    block stands for `size` verbatim bytes of the file, recode.cpp:1275-1297)."""
+    desc, _ = avr.describe_container(avrc)
+    pos, out = 0, []
+    for b in desc["blocks"]:
+        if "literal" in b:
+            pos += len(bytes.fromhex(b["literal"]))
+        elif "cabac" in b:
+            out.append(data[pos:pos + b["size"]])
+            pos += b["size"]
+    return out
+
+
+def _oracle_p_container(name):
+    from _oracle import oracle_cli
+    return oracle_cli("compress", FIX / name, mode="P")
+
+
+@pytest.mark.parametrize("name", ["realshort.mp4", "cockatoo.mp4"])
+def test_plan_and_splice_restore_the_file(name):
+    """avr_plan_decompress lists the coded slices with their re-coded streams; avr_splice_container,
+    fed each slice's payload, rebuilds the file (literals + slices + last-byte patch)."""
+    data = (FIX / name).read_bytes()
+    avrc = _oracle_p_container(name)
+    plan = avr.plan_decompress(avrc)
+    desc, _ = avr.describe_container(avrc)
+    cabac = [bytes.fromhex(b["cabac"]) for b in desc["blocks"] if "cabac" in b]
+    assert len(plan.descs) == len(cabac) > 0
+    for d, c in zip(plan.descs, cabac):
+        o, n = int(d["payload_offset"]), int(d["payload_size"])
+        assert plan.arena[o:o + n].tobytes() == c
+        assert int(d["out_offset"]) + int(d["out_capacity"]) <= plan.work_len
+    pays = _container_payloads(data, avrc)
+    lens = np.array([len(p) for p in pays], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    st = np.zeros(len(pays), np.int32)
+    assert avr.splice_container(avrc, st, b"".join(pays), offs, lens) == data
+    # a payload one byte short of its parity gets the stored last byte appended (recode.cpp:1349-1351)
+    short = [p[:-1] for p in pays]
+    lens2 = np.array([len(p) for p in short], np.uint32)
+    offs2 = np.concatenate([[0], np.cumsum(lens2)[:-1]]).astype(np.uint64)
+    assert avr.splice_container(avrc, st, b"".join(short), offs2, lens2) == data
+    st[len(st) // 2] = -9
+    with pytest.raises(avr.AvrError):
+        avr.splice_container(avrc, st, b"".join(pays), offs, lens)
+
+
+def test_plan_decompress_refuses_reference_model():
+    from _oracle import oracle_cli
+    avrc = oracle_cli("compress", FIX / "realshort.mp4", mode="R")
+    with pytest.raises(avr.AvrError) as e:
+        avr.plan_decompress(avrc)
+    assert e.value.code == -6
+
+
+def _gloo_decompress_worker(rank, world, port, name, outdir):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = (FIX / name).read_bytes()
+        avrc = _oracle_p_container(name)
+        pays = _container_payloads(data, avrc)
+        plan = avr.plan_decompress(avrc)
+        lo, hi = shard.partition(plan.descs["payload_size"], world)[rank]
+
+        def run_range(part):   # stands in for this rank's device decompress
+            assert len(part.descs) == hi - lo
+            mine = pays[lo:hi]
+            lens = np.array([len(p) for p in mine], np.int64)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+            flat = torch.from_numpy(np.frombuffer(b"".join(mine) + b"\0" * 16, np.uint8).copy())
+            return flat, np.zeros(len(mine), np.int64), offs, lens
+
+        out = shard.sharded_decompress(None, avrc, run_range=run_range)
+        if rank == 0:
+            with open(os.path.join(outdir, "out.bin"), "wb") as f:
+                f.write(out)
+        else:
+            assert out is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_decompress_reassembles(world):
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_gloo_decompress_worker, args=(world, port, "cockatoo.mp4", td), nprocs=world, join=True)
+        out = open(os.path.join(td, "out.bin"), "rb").read()
+    assert out == (FIX / "cockatoo.mp4").read_bytes()
+
+
+def test_deal_files_lpt():
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(1, 10_000_000, size=37)
+    for world in (1, 2, 3, 8):
+        owned = shard.deal_files(sizes, world)
+        assert sorted(i for o in owned for i in o) == list(range(len(sizes)))
+        loads = [int(sum(sizes[i] for i in o)) for o in owned]
+        assert max(loads) <= sizes.sum() / world + sizes.max()
+    assert shard.deal_files([], 4) == [[], [], [], []]
+    assert shard.deal_files([5, 1, 1, 1, 1, 1], 2) == [[0], [1, 2, 3, 4, 5]]

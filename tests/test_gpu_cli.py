@@ -88,13 +88,15 @@ def test_sharded_compress_world1_rccl():
                 got = shard.sharded_compress(ctx, data)
                 assert got == ctx.compress(data, avr.MODEL_PARALLEL)
                 assert hashlib.sha256(got).hexdigest() == GOLD[(name, "P")]["avrc_sha256"]
+                # and back: the container's slices regenerated, gathered over RCCL, spliced on rank 0
+                assert shard.sharded_decompress(ctx, got) == data
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_compress_multirank_gloo(world):
-    """The sharded compress with several ranks, each a process of its own running its slice range
+    """The sharded compress and decompress with several ranks, each a process of its own running its slice range
     on the device (all on cuda:0 here; one per GPU on a node), gathered to rank 0 over gloo: the
     container equals the single-GPU compress (golden sha) for both fixtures."""
     import subprocess
@@ -117,6 +119,8 @@ def test_sharded_compress_multirank_gloo(world):
             assert rcs == [0] * world, rcs
             got = out.read_bytes()
             assert hashlib.sha256(got).hexdigest() == GOLD[(name, "P")]["avrc_sha256"], name
+            # the worker also decompressed that container across the ranks (sharded_decompress)
+            assert Path(str(out) + ".dec").read_bytes() == (FIX / name).read_bytes(), name
 
 
 def _bills(stderr: str) -> dict:
