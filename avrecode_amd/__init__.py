@@ -22,7 +22,7 @@ import numpy as np
 __all__ = [
     "AvrError", "Context", "MODEL_REFERENCE", "MODEL_PARALLEL", "SLICE_DESC", "SLICE_RESULT",
     "SynthParams", "lib", "parse_stream", "assemble_container", "neighbor_tables",
-    "plan_decompress", "splice_container", "library_path", "EXPORTED_SYMBOLS",
+    "plan_decompress", "splice_container", "source_sha", "library_path", "EXPORTED_SYMBOLS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -121,6 +121,23 @@ class SynthParams:
 
 
 _lib = None
+
+
+def source_sha() -> str:
+    """sha256 over the native sources libavrecode.so is built from (avrecode_amd/csrc/*,
+    include/avrecode.h, the Makefile): identifies the build a profile was taken on, without git
+    (the GPU box has no .git).  scripts/pmc_traffic.py records it; bench.py uses a traffic
+    profile only when it matches the tree being measured."""
+    import hashlib
+    root = os.path.dirname(_HERE)
+    files = sorted(os.path.join(_HERE, "csrc", f) for f in os.listdir(os.path.join(_HERE, "csrc")))
+    files += [os.path.join(root, "include", "avrecode.h"), os.path.join(_HERE, "Makefile")]
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.relpath(f, root).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 def lib() -> ctypes.CDLL:

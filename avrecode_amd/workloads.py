@@ -8,6 +8,9 @@
                    fixtures (tests/fixtures)
   stream_4k(ctx)   configs[3]: one 4K stream, 1 slice per frame, 1-s GOP (I + 29 P) tiled with
                    rewritten frame numbers (avr_synthesize_stream's repeat)
+  mixed_files(ctx) many independent files of mixed kinds and sizes: the corpus entries with a seed
+                   and a length of their own each (plus the fixtures), for the reference model's
+                   files-in-parallel leg
 """
 from __future__ import annotations
 
@@ -67,3 +70,24 @@ def stream_4k(ctx, seconds: int = 600, fps: int = 30, mb_width: int = 240, mb_he
     p = SynthParams(mb_width=mb_width, mb_height=mb_height, slice_type=0, slice_qp=26, chroma_format_idc=1,
                     transform_8x8_mode=1, seed=seed, gop_length=fps, repeat=seconds)
     return ctx.synthesize(p, fps)
+
+
+def mixed_files(ctx, n: int = 256, scale: float = 0.25, seed: int = 5000) -> list[tuple[str, bytes]]:
+    """n independent files cycling through the CORPUS kinds (and, every 16th, a fixture), each with
+    its own seed and a frame count drawn from 1 .. 2 x the kind's scaled length, so sizes and
+    slice structures differ from file to file (a heterogeneous load, not n copies of one file)."""
+    import random
+    rnd = random.Random(seed)
+    fixtures = [(f, (ROOT / "tests" / "fixtures" / f).read_bytes()) for f in FIXTURES]
+    out = []
+    for i in range(n):
+        if i % 16 == 15:
+            out.append(fixtures[(i // 16) % len(fixtures)])
+            continue
+        name, w, h, spf, frames, gop, st, qp, cf, structure = CORPUS[i % len(CORPUS)]
+        nf = max(1, rnd.randint(1, max(1, int(round(2 * frames * scale)))))
+        p = SynthParams(mb_width=w, mb_height=h, slice_type=st, slice_qp=qp + rnd.randint(-2, 2), chroma_format_idc=cf,
+                        transform_8x8_mode=1, num_ref_idx_l0=2, num_ref_idx_l1=1, seed=seed + i,
+                        slices_per_picture=spf, gop_length=gop, structure=structure)
+        out.append((f"{name}_{nf}f_s{seed + i}", ctx.synthesize(p, nf)))
+    return out

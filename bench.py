@@ -25,7 +25,11 @@ threads (all_cores), ~10-30 s.
 file_roundtrip (rank 0, N=1): the north-star command `recode roundtrip <file>` (recode.cpp:1594-1624)
 on whole files from host memory -- both fixtures and the BASELINE configs[1] clip (1080p, 64 frames,
 I + 31 P twice, QP 26) -- in both model modes, with the CPU oracle's R-mode single-core roundtrip
-beside each.
+beside each, and each call's phase breakdown (demux / upload / kernels / download / container).
+corpus: BASELINE configs[4] (N=1: one batch per model; N>1: files dealt to ranks, LPT by bytes).
+rmode_files (N=1): the reference model over 256 heterogeneous files at once.
+stream_shard (N=1): BASELINE configs[3] on a REDUCED stream (--stream-leg-seconds, default 30 s of
+the config's 600 s) with its own roofline and CPU baseline; `--stream-shard` runs it alone at any N.
 """
 import argparse
 import json
@@ -170,6 +174,10 @@ def _oracle_roundtrip_s(path):
     return (float(m.group(1)), float(m.group(2))) if m else None
 
 
+def _round_phases(ph):
+    return {k: round(v * 1e3, 3) for k, v in ph.items()} | {"unit": "ms"}
+
+
 def file_roundtrips(ctx, args):
     """The north-star command, `recode roundtrip <file>` (recode.cpp:1594-1624), on whole files from
     host memory: avr_roundtrip_file = demux + compress (device) + container + decompress (device) +
@@ -185,7 +193,7 @@ def file_roundtrips(ctx, args):
     for name, data in files:
         rec = {"bytes": len(data)}
         for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
-            walls, comps, decs = [], [], []
+            walls, comps, decs, stats = [], [], [], []
             # the first call warms up (buffer allocation); a call of seconds is its own sample
             for it in range(1 + args.file_reps):
                 t0 = time.perf_counter()
@@ -196,13 +204,17 @@ def file_roundtrips(ctx, args):
                 walls.append(dt)
                 comps.append(st["compress_s"])
                 decs.append(st["decompress_s"])
+                stats.append(st)
                 if dt >= 2.0:
                     break
             progress(f"file {name} {tag}: {len(data) / walls[0] / 1e6:.2f} MB/s")
             k = sorted(range(len(walls)), key=walls.__getitem__)[len(walls) // 2]
             rec[tag] = {"MB_s": len(data) / walls[k] / 1e6, "wall_s": walls[k], "compress_s": comps[k],
                         "decompress_s": decs[k], "avrc_bytes": len(avrc), "ratio": len(avrc) / len(data),
-                        "slices": int(st["slices"]), "coded": int(st["coded_slices"]), "bit_exact": True}
+                        "slices": int(st["slices"]), "coded": int(st["coded_slices"]), "bit_exact": True,
+                        "attempts": int(stats[k]["attempts"]),
+                        "phases": {"compress": _round_phases(stats[k]["compress_phases"]),
+                                   "decompress": _round_phases(stats[k]["decompress_phases"])}}
         if args.no_cpu_baseline:
             out[name] = rec
             continue
@@ -280,40 +292,54 @@ def rmode_files_section(ctx, args):
     """The reference model (R-mode) as throughput: its unit of sequential work is a file
     (DESIGN.md §2), so N independent files go through avr_compress_files / avr_decompress_files at
     once -- every slice of every file in one parallel R-mode compress pass, one workgroup per file
-    for the decompress.  The files are N copies of realshort.mp4 (independent runs of the reference
-    model; replicas stand in for a corpus of small files).  MB/s = N x file bytes / (compress +
-    decompress wall time), every file checked byte-exact."""
+    for the decompress.  The files are a heterogeneous mix (workloads.mixed_files: the configs[4]
+    kinds -- 720p/1080p/4K, IBBP/IP, 1-17 slices per frame, 4:2:0/4:2:2/4:4:4, PAFF/MBAFF -- each
+    with its own seed and length, and the fixtures), so the per-file load is uneven.  MB/s = bytes /
+    (compress + decompress wall time), every file checked byte-exact; phases = where each half's
+    wall time went (avr_last_phase_times)."""
     import avrecode_amd as avr
-    data = (ROOT / "tests" / "fixtures" / "realshort.mp4").read_bytes()
-    datas = [data] * args.rfiles
-    total = len(data) * args.rfiles
-    walls, tc, td = [], [], []
+    from avrecode_amd import workloads
+    files = workloads.mixed_files(ctx, n=args.rfiles)
+    datas = [d for _, d in files]
+    total = sum(map(len, datas))
+    sizes = sorted(map(len, datas))
+    walls, tc, td, phc, phd = [], [], [], [], []
     for it in range(1 + args.file_reps):
         t0 = time.perf_counter()
         outs = ctx.compress_files(datas, avr.MODEL_REFERENCE)
         t1 = time.perf_counter()
+        pc = ctx.last_phase_times()
         back = ctx.decompress_files(outs)
         t2 = time.perf_counter()
+        pd = ctx.last_phase_times()
         assert back == datas, "R-mode files: decompress did not restore every file"
         if it == 0:
             continue   # warm-up (buffer allocation)
         walls.append(t2 - t0)
         tc.append(t1 - t0)
         td.append(t2 - t1)
+        phc.append(pc)
+        phd.append(pd)
+        if t2 - t0 >= 5.0:
+            break
     k = sorted(range(len(walls)), key=walls.__getitem__)[len(walls) // 2]
     progress(f"R-mode files: {total / walls[k] / 1e6:.2f} MB/s")
-    return {"files": args.rfiles, "file": "realshort.mp4", "bytes": total, "model": "reference (R)",
-            "MB_s": total / walls[k] / 1e6, "wall_s": walls[k], "compress_s": tc[k], "decompress_s": td[k],
-            "bit_exact": True}
+    return {"files": len(files), "kinds": "workloads.mixed_files (configs[4] kinds, per-file seeds and lengths, "
+                                          "fixtures every 16th)",
+            "bytes": total, "file_bytes_min_median_max": [sizes[0], sizes[len(sizes) // 2], sizes[-1]],
+            "model": "reference (R)", "MB_s": total / walls[k] / 1e6, "wall_s": walls[k], "compress_s": tc[k],
+            "decompress_s": td[k], "avrc_bytes": sum(map(len, outs)), "bit_exact": True,
+            "phases": {"compress": _round_phases(phc[k]), "decompress": _round_phases(phd[k])}}
 
 
-def main_stream_shard(args):
+def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     """BASELINE configs[3]: ONE 4K stream (1 slice per frame, a 1-s GOP I + 29 P tiled to
-    --stream-seconds with rewritten frame numbers) cut by NAL unit into contiguous slice ranges
-    balanced by bytes (shard.partition), one range per GPU.  Timed: every rank's device roundtrip
-    of its range (compress + decompress + verify), the device pack of its re-coded blocks, the RCCL
-    gather to rank 0 (shard.gather_flat) and rank 0's Recoded container assembly.  value = stream
-    bytes / max-over-ranks time (strong scaling: the stream is the same at every N)."""
+    `seconds` with rewritten frame numbers) cut by NAL unit into contiguous slice ranges balanced
+    by bytes (shard.partition), one range per GPU.  Timed: every rank's device roundtrip of its
+    range (compress + decompress + verify), the device pack of its re-coded blocks, the RCCL gather
+    to rank 0 (shard.gather_flat) and rank 0's Recoded container assembly.  value = stream bytes /
+    max-over-ranks time (strong scaling: the stream is the same at every N).  Returns rank 0's
+    record (None elsewhere)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -322,32 +348,20 @@ def main_stream_shard(args):
     from avrecode_amd import shard, workloads
     from avrecode_amd.batch import DeviceBatch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if not dist.is_initialized():
-        if world > 1:
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
-            dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    ctx = avr.Context(local)
-    progress(f"rank {rank}: generating the {args.stream_seconds}-s stream")
-    data = workloads.stream_4k(ctx, seconds=args.stream_seconds, fps=30, mb_width=args.stream_mb[0],
-                               mb_height=args.stream_mb[1])
+    progress(f"rank {rank}: generating the {seconds}-s stream")
+    data = workloads.stream_4k(ctx, seconds=seconds, fps=30, mb_width=args.stream_mb[0], mb_height=args.stream_mb[1])
     progress(f"rank {rank}: {len(data)} bytes; parsing")
     ps = avr.parse_stream(data)
     lo, hi = shard.partition(ps.descs["payload_size"], world)[rank]
     part = shard.subset(ps, lo, hi)
     batch = DeviceBatch(ctx, part)
+    stream = torch.cuda.Stream(dev)
+    mk = lambda: [torch.cuda.Event(enable_timing=True) for _ in range(4)]  # noqa: E731
 
-    def step():
-        batch.roundtrip(avr.MODEL_PARALLEL)
-        flat, d_off = batch.pack()
-        torch.cuda.synchronize()
+    def step(ev):
+        batch.roundtrip_timed(ev, avr.MODEL_PARALLEL, stream)
+        flat, d_off = batch.pack(stream)
+        stream.synchronize()
         v = batch.verdicts()
         res = batch.results("c")
         offs = d_off.cpu().numpy()[: hi - lo].astype(np.int64)
@@ -358,45 +372,117 @@ def main_stream_shard(args):
             return None, bool((v == 1).all())
         return avr.assemble_container(data, *g), bool((v == 1).all())
 
-    for _ in range(args.warmup):
-        step()
-        progress(f"rank {rank}: warm-up step done")
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ok = True
-    for k in range(args.steps):
-        avrc, good = step()
-        ok = ok and good
-        progress(f"rank {rank}: step {k} done")
-    torch.cuda.synchronize()
-    dist.barrier()
-    elapsed = time.perf_counter() - t0
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step(mk())
+            progress(f"rank {rank}: warm-up step done")
+        evs = [mk() for _ in range(args.stream_steps)]
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ok = True
+        for k in range(args.stream_steps):
+            avrc, good = step(evs[k])
+            ok = ok and good
+            progress(f"rank {rank}: step {k} done")
+        torch.cuda.synchronize()
+        dist.barrier()
+        elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
     dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
     dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+    if rank != 0:
+        return None
+    # the container must decompress to the stream (checked outside the timed region)
+    exact = bool(t[1] == 0) and ctx.decompress(avrc) == data
+    t_comp = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
+    t_dec = sum(e[2].elapsed_time(e[3]) for e in evs) / len(evs) / 1e3
+    v = batch.verdicts()
+    S = int(part.descs["payload_size"].sum())
+    C = int(batch.results("c")["out_len"][v == 1].sum())
+    dominant, t_dom = ("compress", t_comp) if t_comp >= t_dec else ("decompress", t_dec)
+    kernel_name = "slices_parallel_kernel<0>" if dominant == "compress" else "slices_parallel_kernel<1>"
+    rec = {
+        "metric": METRIC, "value": len(data) * args.stream_steps / float(t[0]) / 1e6, "unit": "MB/s",
+        "n_gpus": world, "steps": args.stream_steps, "warmup": args.warmup,
+        "ms_per_step": float(t[0]) / args.stream_steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (device generator, seeded; one GOP tiled)",
+        "bit_exact": exact,
+        "config": {"workload": "one 4K stream sharded by NAL unit, RCCL gather reassembly (BASELINE configs[3])"
+                               + ("" if seconds == 600 else f"; REDUCED stream: {seconds} s of the config's 600 s"),
+                   "seconds": seconds, "fps": 30, "mb": list(args.stream_mb), "slices": len(ps.descs),
+                   "stream_bytes": len(data), "container_bytes": len(avrc), "model": "parallel",
+                   "parallelism": f"slice ranges over {world} GPU(s)", "payload_bytes_S_rank0": S,
+                   "recoded_bytes_C_rank0": C, "compress_ms": t_comp * 1e3, "decompress_ms": t_dec * 1e3},
+        "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": (S + C) / t_dom / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": (S + C) / t_dom / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "note": "rank 0's slice range: S + C per launch over the kernel's average HIP-event time"},
+        "cpu_baseline": None,
+    }
+    if with_cpu:
+        rec["cpu_baseline"] = stream_cpu_baseline(data, ps, args.cpu_seconds)
+    return rec
+
+
+def stream_cpu_baseline(data, ps, budget_s):
+    """The oracle's parallel-model (fresh model per slice) compress + decompress of the stream's
+    first slices, in stream order, on one host core, until ~budget_s of CPU work."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _oracle
+    _oracle.build_oracle()
+    done_bytes, t_tot, k = 0, 0.0, 0
+    while k < len(ps.descs) and t_tot < budget_s:
+        t0 = time.perf_counter()
+        _, recs = _oracle.slices_p(data, k, k + 1, check_recodable=False)
+        t_tot += time.perf_counter() - t0
+        assert all(r["status_c"] == 0 and r["status_d"] == 0 for r in recs)
+        done_bytes += int(ps.descs[k]["payload_size"])
+        k += 1
+    return {"value": done_bytes / t_tot / 1e6, "unit": "MB/s (slice payload bytes)", "cores": 1, "kind": "port",
+            "sample": f"first {k} slices of the stream (I + {k - 1} P, {done_bytes} payload bytes), oracle "
+                      f"parallel-model compress + decompress, one thread, {t_tot:.1f} s"}
+
+
+def main_stream_shard(args):
+    """`--stream-shard`: configs[3] alone at the full (or --stream-seconds) length, N GPUs."""
+    import torch
+    import torch.distributed as dist
+
+    import avrecode_amd as avr
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    _init_dist(world, dev)
+    ctx = avr.Context(local)
+    args.stream_steps = args.steps
+    rec = stream_shard_leg(ctx, args, args.stream_seconds, world, rank, dev, with_cpu=False)
     if rank == 0:
-        # the container must decompress to the stream (checked outside the timed region)
-        exact = bool(t[1] == 0) and ctx.decompress(avrc) == data
-        line = {
-            "metric": METRIC, "value": len(data) * args.steps / float(t[0]) / 1e6, "unit": "MB/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": float(t[0]) / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "u8", "data": "synthetic (device generator, seeded; one GOP tiled)",
-            "bit_exact": exact,
-            "config": {"workload": "one 4K stream sharded by NAL unit, RCCL gather reassembly (BASELINE configs[3])",
-                       "seconds": args.stream_seconds, "fps": 30, "mb": list(args.stream_mb), "slices": len(ps.descs),
-                       "stream_bytes": len(data), "container_bytes": len(avrc), "model": "parallel",
-                       "parallelism": f"slice ranges over {world} GPU(s)"},
-            "roofline": None, "cpu_baseline": None,
-        }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(rec), flush=True)
     dist.barrier()
     dist.destroy_process_group()
     ctx.close()
 
 
+def _init_dist(world, dev):
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    else:   # a world-1 RCCL group: the same gather path as N > 1
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+
+
 def load_traffic(args, kernel):
+    """HBM bytes per launch of `kernel` from profiles/<round>_pmc.json (scripts/pmc_traffic.py),
+    only when that profile was taken on this batch shape AND on this build of the native sources
+    (its source_sha equals avrecode_amd.source_sha() of the tree being measured); else None."""
+    import avrecode_amd as avr
     p = ROOT / "profiles" / f"{args.round}_pmc.json"
     if not p.exists():
         return None
@@ -404,9 +490,47 @@ def load_traffic(args, kernel):
         j = json.loads(p.read_text())
         if j.get("slices") != args.slices or j.get("mb") != [args.mb_width, args.mb_height]:
             return None
+        if j.get("source_sha") != avr.source_sha():
+            progress(f"traffic: {p.name} is from another build of the sources; reporting null")
+            return None
         return j["kernels"][kernel]["hbm_bytes_per_launch"]
     except Exception:
         return None
+
+
+def corpus_sharded(ctx, args, world, rank, dev):
+    """BASELINE configs[4] on N GPUs: the corpus's files dealt whole to the ranks (shard.deal_files,
+    LPT by bytes) and each rank's files run as one batch per model (avr_compress_files +
+    avr_decompress_files, byte-checked).  No collective in the timed region; MB/s = corpus bytes /
+    max-over-ranks wall time.  The reference model runs here as replicas over files (its only
+    split)."""
+    import torch
+    import torch.distributed as dist
+
+    import avrecode_amd as avr
+    from avrecode_amd import shard, workloads
+    files = workloads.corpus(ctx, scale=args.corpus_scale)
+    total = sum(len(d) for _, d in files)
+    mine = shard.deal_files([len(d) for _, d in files], world)[rank]
+    datas = [files[i][1] for i in mine]
+    rec = {"files": len(files), "bytes": total, "n_gpus": world, "scaling": "strong",
+           "files_rank0": [files[i][0] for i in shard.deal_files([len(d) for _, d in files], world)[0]]}
+    for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+        for it in range(2):   # one warm-up pass, one timed
+            dist.barrier()
+            t0 = time.perf_counter()
+            ok = True
+            if datas:
+                outs = ctx.compress_files(datas, model)
+                back = ctx.decompress_files(outs)
+                ok = back == datas
+            dt = time.perf_counter() - t0
+            t = torch.tensor([dt, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+        rec[tag] = {"MB_s": total / float(t[0]) / 1e6, "wall_s": float(t[0]), "bit_exact": bool(t[1] == 0)}
+        progress(f"corpus {tag} over {world} GPU(s): {rec[tag]['MB_s']:.2f} MB/s")
+    return rec
 
 
 def main():
@@ -420,13 +544,16 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r02")
+    ap.add_argument("--round", default="r03")
     ap.add_argument("--file-reps", type=int, default=3, help="timed reps of a whole-file call under 2 s")
     ap.add_argument("--no-files", action="store_true", help="skip the whole-file roundtrips")
     ap.add_argument("--no-clip", action="store_true", help="skip the configs[1] clip in the file roundtrips")
     ap.add_argument("--no-corpus", action="store_true", help="skip the configs[4] corpus")
     ap.add_argument("--corpus-scale", type=float, default=1.0)
-    ap.add_argument("--rfiles", type=int, default=512, help="files in the R-mode many-files leg (0: skip)")
+    ap.add_argument("--rfiles", type=int, default=256, help="files in the R-mode many-files leg (0: skip)")
+    ap.add_argument("--stream-leg-seconds", type=int, default=30,
+                    help="N=1 default run: length of the configs[3] stream leg (0: skip)")
+    ap.add_argument("--stream-steps", type=int, default=2)
     ap.add_argument("--stream-shard", action="store_true",
                     help="configs[3]: one 4K stream sharded over the GPUs with the RCCL gather (strong scaling)")
     ap.add_argument("--stream-seconds", type=int, default=600)
@@ -552,8 +679,20 @@ def main():
             line["corpus"] = corpus_section(ctx, args)
         if world == 1 and args.rfiles > 0 and not args.no_files:
             line["rmode_files"] = rmode_files_section(ctx, args)
+    if world == 1 and args.stream_leg_seconds > 0 and not args.no_files:
+        _init_dist(world, dev)
+        rec = stream_shard_leg(ctx, args, args.stream_leg_seconds, world, rank, dev,
+                               with_cpu=not args.no_cpu_baseline)
+        if rank == 0:
+            line["stream_shard"] = rec
+            progress(f"stream leg: {rec['value']:.1f} MB/s")
+    if world > 1 and not args.no_corpus:
+        rec = corpus_sharded(ctx, args, world, rank, dev)
+        if rank == 0:
+            line["corpus"] = rec
+    if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
     ctx.close()

@@ -31,7 +31,10 @@ def main():
                 continue
             k = "slices_parallel_kernel<%s>" % name.split("slices_parallel_kernel<")[1][0]
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    out = {"slices": a.slices, "mb": list(a.mb), "source": a.src,
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from avrecode_amd import source_sha
+    out = {"slices": a.slices, "mb": list(a.mb), "source": a.src, "source_sha": source_sha(),
            "note": "FETCH_SIZE x2 (gfx950 correction), WRITE_SIZE as reported; KiB -> bytes; mean per dispatch",
            "kernels": {}}
     for k, c in vals.items():
