@@ -1496,11 +1496,21 @@ extern "C" int avr_debug_profile(int mode, unsigned long long* out16) {
 // bin trace (MODE_TRACE kernel) to the caller and cross-checks the caller's parse against it.
 struct avr_hooks_session;
 
+// A significance map of the device's parse (MODE_TRACE event records): the bins [begin, end) it
+// spans and the model state it starts under -- mb_xy and begin_sub_mb's arguments.
+struct HookMap {
+  uint32_t begin = 0, end = 0;
+  int x = 0, y = 0;
+  int sub[5] = {0, 0, 0, 0, 0};   // cat, scan8 index, max_coeff, is_dc, chroma422
+};
+
 struct avr_hooks_slice {
   avr_hooks_session* sess = nullptr;
   int index = 0;                 // slice index (decode order)
-  const uint8_t* trace = nullptr;
+  const uint8_t* trace = nullptr;   // 2 bytes per bin: bin | kind << 1, state byte before it
   size_t nbins = 0, cur = 0;
+  const HookMap* maps = nullptr;
+  size_t nmaps = 0, map_cur = 0;
   bool sub_open = false;
   int sub_args[5] = {0, 0, 0, 0, 0};
   int coding_type = 0;
@@ -1514,14 +1524,19 @@ struct avr_hooks_session {
   std::vector<uint8_t> stream;     // decompress: read_packet's stream
   ParsedFile pf;
   std::vector<char> coded;
-  std::vector<uint8_t> traces;
-  std::vector<uint64_t> trace_off;
-  std::vector<uint32_t> trace_len;
+  std::vector<std::vector<uint8_t>> bins;   // per slice: the device's bins (2 bytes each)
+  std::vector<std::vector<HookMap>> maps;    // per slice: its significance maps
   std::vector<avr_hooks_slice> slices;
   size_t next_slice = 0;
   uint64_t next_marker = 1;
   avr_hooks_slice* live = nullptr;  // the slice model hooks refer to (one live CABAC context, recode.cpp:199)
   uint64_t mb_calls = 0;
+  int mb_x = -1, mb_y = -1;         // the caller's last mb_xy (h264_model::mb_coord)
+  // frame_spec (update_frame_spec, recode.cpp:824-843): the caller's last call and the slice it
+  // belonged to; a call made between slices waits for the next init_decoder
+  bool fs_have = false, fs_pending = false;
+  int fs_num = 0, fs_w = 0, fs_h = 0, fs_slice = -1;
+  int pend_num = 0, pend_w = 0, pend_h = 0;
   std::string err;
   void fail_once(const std::string& m) {
     if (err.empty()) err = m;
@@ -1551,22 +1566,59 @@ int run_traces(avr_hooks_session* hs) {
     d.read_limit = (uint32_t)s.read_limit;
     // 2 bytes per bin; H.264 bounds the bins of a slice by ~32/3 per payload byte plus a
     // per-macroblock allowance (7.4.2.2), well inside this
-    d.out_capacity = (uint32_t)std::min<uint64_t>(0xfffffff0ull, 2ull * (16ull * s.size + 2048ull * d.mb_width * d.mb_height / 8 + 4096));
+    // 2 bytes per bin (H.264 bounds a slice's bins by ~32/3 per payload byte plus a per-macroblock
+    // allowance, 7.4.2.2) and 12 bytes of map events per residual block (<= 51 per macroblock)
+    d.out_capacity = (uint32_t)std::min<uint64_t>(
+        0xfffffff0ull, 32ull * s.size + 1280ull * d.mb_width * d.mb_height + 8192);
     plan.max_w = std::max(plan.max_w, ring_cols(d));
     slice_of.push_back((int)i);
     plan.descs.push_back(d);
   }
-  hs->trace_off.assign(hs->pf.slices.size(), 0);
-  hs->trace_len.assign(hs->pf.slices.size(), 0);
+  hs->bins.assign(hs->pf.slices.size(), {});
+  hs->maps.assign(hs->pf.slices.size(), {});
   if (plan.descs.empty()) return AVR_OK;
   std::vector<avr_slice_result> res;
-  if (int r = run_plan(c, 3, false, plan, &res, &hs->traces)) return r;
+  std::vector<uint8_t> traces;
+  if (int r = run_plan(c, 3, false, plan, &res, &traces)) return r;
   for (size_t k = 0; k < plan.descs.size(); k++) {
+    const int i = slice_of[k];
     if (res[k].status != 0)
-      return fail(c, AVR_ERR_FORMAT, "hooks: device trace of slice " + std::to_string(slice_of[k]) + " failed (" +
+      return fail(c, AVR_ERR_FORMAT, "hooks: device trace of slice " + std::to_string(i) + " failed (" +
                                          std::to_string(res[k].status) + ")");
-    hs->trace_off[slice_of[k]] = plan.descs[k].out_offset;
-    hs->trace_len[slice_of[k]] = res[k].out_len / 2;
+    // split the records: bins (kinds 0-2) and map events (kind 3, avr_walker.h TRACE_EV_*)
+    const uint8_t* t = traces.data() + plan.descs[k].out_offset;
+    const size_t len = res[k].out_len;
+    std::vector<uint8_t>& b = hs->bins[i];
+    std::vector<HookMap>& m = hs->maps[i];
+    b.reserve(len);
+    bool open = false;
+    for (size_t at = 0; at + 2 <= len;) {
+      if (((t[at] >> 1) & 3) != 3) {
+        b.push_back(t[at]);
+        b.push_back(t[at + 1]);
+        at += 2;
+        continue;
+      }
+      const uint32_t bin_index = (uint32_t)(b.size() / 2);
+      if (t[at + 1] == 1 && at + 10 <= len && !open) {
+        HookMap h;
+        h.begin = bin_index;
+        h.x = t[at + 2] | t[at + 3] << 8;
+        h.y = t[at + 4] | t[at + 5] << 8;
+        h.sub[0] = t[at + 6], h.sub[1] = t[at + 7], h.sub[2] = t[at + 8];
+        h.sub[3] = t[at + 9] & 1, h.sub[4] = t[at + 9] >> 1;
+        m.push_back(h);
+        open = true;
+        at += 10;
+      } else if (t[at + 1] == 2 && open) {
+        m.back().end = bin_index;
+        open = false;
+        at += 2;
+      } else {
+        return fail(c, AVR_ERR_DEVICE, "hooks: malformed device trace of slice " + std::to_string(i));
+      }
+    }
+    if (open) return fail(c, AVR_ERR_DEVICE, "hooks: device trace of slice " + std::to_string(i) + " ends in a map");
   }
   return AVR_OK;
 }
@@ -1581,6 +1633,47 @@ bool coded_from_container(const std::vector<avr::PbBlock>& blocks, size_t n_slic
     (*coded)[i++] = b.has_cabac ? 1 : 0;
   }
   return i == n_slices;
+}
+
+// the live slice is done (the next init_decoder or avr_hooks_end): every bin and every map consumed
+void close_live(avr_hooks_session* hs) {
+  avr_hooks_slice* h = hs->live;
+  hs->live = nullptr;
+  if (!h) return;
+  if (h->cur != h->nbins)
+    hs->fail_once("hooks: slice " + std::to_string(h->index) + " ended after " + std::to_string(h->cur) + " of " +
+                  std::to_string(h->nbins) + " bins");
+  else if (h->map_cur != h->nmaps)
+    hs->fail_once("hooks: slice " + std::to_string(h->index) + " reported " + std::to_string(h->map_cur) + " of its " +
+                  std::to_string(h->nmaps) + " significance maps");
+  else if (!hs->fs_have || hs->pf.slices[hs->fs_slice].picture_id != hs->pf.slices[h->index].picture_id)
+    hs->fail_once("hooks: slice " + std::to_string(h->index) + " was decoded without a frame_spec for its picture");
+}
+
+// frame_spec of slice i: the model's frames (update_frame_spec, recode.cpp:824-843) must turn over
+// exactly where the device's pictures do -- frame_num (or the size) changes between two calls iff
+// the slices belong to different pictures (the device's decode-order picture counter, which the
+// two fields of a frame share, as they share frame_num) -- and the size must be the picture's.
+void check_frame_spec(avr_hooks_session* hs, int i, int frame_num, int w, int h) {
+  const avr::SliceInfo& s = hs->pf.slices[i];
+  const std::string where = "hooks: slice " + std::to_string(i) + ": frame_spec(" + std::to_string(frame_num) + ", " +
+                            std::to_string(w) + ", " + std::to_string(h) + ")";
+  if (w != s.h.mb_width || h != s.h.mb_height) {
+    hs->fail_once(where + " size differs from the picture's " + std::to_string(s.h.mb_width) + " x " +
+                  std::to_string(s.h.mb_height));
+    return;
+  }
+  if (hs->fs_have) {
+    const avr::SliceInfo& p = hs->pf.slices[hs->fs_slice];
+    const bool caller_new = frame_num != hs->fs_num || w != hs->fs_w || h != hs->fs_h;
+    const bool device_new = s.picture_id != p.picture_id || w != hs->fs_w || h != hs->fs_h;
+    if (caller_new != device_new)
+      hs->fail_once(where + (device_new ? " keeps the frame of slice " : " starts a new frame after slice ") +
+                    std::to_string(hs->fs_slice) + ", the device's parse " +
+                    (device_new ? "starts a new picture" : "stays in the same picture"));
+  }
+  hs->fs_have = true;
+  hs->fs_num = frame_num, hs->fs_w = w, hs->fs_h = h, hs->fs_slice = i;
 }
 
 int hooks_finish_setup(avr_hooks_session* hs, const std::vector<avr::PbBlock>& blocks) {
@@ -1652,15 +1745,16 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
 void* avr_hook_init_decoder(void* opaque, void* /*cabac_context*/, const uint8_t* buf, int size) {
   avr_hooks_session* hs = (avr_hooks_session*)opaque;
   if (!hs) return nullptr;
-  if (hs->live && hs->live->cur != hs->live->nbins)
-    hs->fail_once("hooks: slice " + std::to_string(hs->live->index) + " ended after " +
-                  std::to_string(hs->live->cur) + " of " + std::to_string(hs->live->nbins) + " bins");
-  hs->live = nullptr;
+  close_live(hs);
   if (hs->next_slice >= hs->pf.slices.size()) {
     hs->fail_once("hooks: more slices than the file holds");
     return nullptr;
   }
   const size_t i = hs->next_slice++;
+  if (hs->fs_pending) {   // the frame_spec made before this slice's decode
+    hs->fs_pending = false;
+    check_frame_spec(hs, (int)i, hs->pend_num, hs->pend_w, hs->pend_h);
+  }
   const avr::SliceInfo& s = hs->pf.slices[i];
   if (!buf || size < 0 || (size_t)size != s.size) {
     hs->fail_once("hooks: slice " + std::to_string(i) + " size differs from the device's parse");
@@ -1682,9 +1776,12 @@ void* avr_hook_init_decoder(void* opaque, void* /*cabac_context*/, const uint8_t
   avr_hooks_slice& h = hs->slices[i];
   h.sess = hs;
   h.index = (int)i;
-  h.trace = hs->traces.data() + hs->trace_off[i];
-  h.nbins = hs->trace_len[i];
+  h.trace = hs->bins[i].data();
+  h.nbins = hs->bins[i].size() / 2;
   h.cur = 0;
+  h.maps = hs->maps[i].data();
+  h.nmaps = hs->maps[i].size();
+  h.map_cur = 0;
   hs->live = &h;
   return &h;
 }
@@ -1729,10 +1826,26 @@ const uint8_t* avr_hook_skip_bytes(void* slice, int /*n*/) {
   return nullptr;
 }
 
-void avr_hook_frame_spec(void* /*opaque*/, int /*frame_num*/, int /*mb_width*/, int /*mb_height*/) {}
+void avr_hook_frame_spec(void* opaque, int frame_num, int mb_width, int mb_height) {
+  avr_hooks_session* hs = (avr_hooks_session*)opaque;
+  if (!hs) return;
+  avr_hooks_slice* h = hs->live;
+  if (h && h->cur < h->nbins) {   // inside a slice's decode: that slice's picture
+    check_frame_spec(hs, h->index, frame_num, mb_width, mb_height);
+    return;
+  }
+  if (hs->fs_pending && (hs->pend_num != frame_num || hs->pend_w != mb_width || hs->pend_h != mb_height))
+    hs->fail_once("hooks: two different frame_spec calls before one slice");
+  hs->fs_pending = true;
+  hs->pend_num = frame_num, hs->pend_w = mb_width, hs->pend_h = mb_height;
+}
 
-void avr_hook_mb_xy(void* opaque, int /*x*/, int /*y*/) {
-  if (opaque) ((avr_hooks_session*)opaque)->mb_calls++;
+void avr_hook_mb_xy(void* opaque, int x, int y) {
+  avr_hooks_session* hs = (avr_hooks_session*)opaque;
+  if (!hs) return;
+  hs->mb_calls++;
+  hs->mb_x = x;
+  hs->mb_y = y;
 }
 
 void avr_hook_begin_sub_mb(void* opaque, int cat, int scan8index, int max_coeff, int is_dc, int chroma422) {
@@ -1755,26 +1868,51 @@ void avr_hook_end_sub_mb(void* opaque, int cat, int scan8index, int max_coeff, i
   h->sub_open = false;
 }
 
-void avr_hook_begin_coding_type(void* opaque, int coding_type, int /*zigzag_index*/, int /*param0*/, int /*param1*/) {
+// begin_coding_type(SIG_MAP) (recode.cpp:951-974) starts the model's significance-map keys: it
+// must come exactly before the device's map's first bin, under the device's macroblock (mb_xy)
+// and sub-macroblock (begin_sub_mb), with zigzag_index 0 (recode.cpp:961); end_coding_type right
+// after its last bin (recode.cpp:931-950).  Other coding types carry no device event.
+void avr_hook_begin_coding_type(void* opaque, int coding_type, int zigzag_index, int /*param0*/, int /*param1*/) {
   avr_hooks_session* hs = (avr_hooks_session*)opaque;
   if (!hs || !hs->live) return;
-  if (hs->live->coding_type != AVR_PIP_UNKNOWN) hs->fail_once("hooks: nested begin_coding_type");
-  hs->live->coding_type = coding_type;
+  avr_hooks_slice* h = hs->live;
+  if (h->coding_type != AVR_PIP_UNKNOWN) hs->fail_once("hooks: nested begin_coding_type");
+  h->coding_type = coding_type;
+  if (coding_type != AVR_PIP_SIGNIFICANCE_MAP) return;
+  const std::string where = "hooks: slice " + std::to_string(h->index) + " bin " + std::to_string(h->cur) + ": ";
+  if (h->map_cur >= h->nmaps) {
+    hs->fail_once(where + "begin_coding_type(SIG_MAP) where the device's parse has no significance map");
+    return;
+  }
+  const HookMap& m = h->maps[h->map_cur];
+  if (h->cur != m.begin)
+    hs->fail_once(where + "begin_coding_type(SIG_MAP) where the device's map begins at bin " + std::to_string(m.begin));
+  else if (zigzag_index != 0)
+    hs->fail_once(where + "begin_coding_type(SIG_MAP) with zigzag_index != 0");
+  else if (hs->mb_x != m.x || hs->mb_y != m.y)
+    hs->fail_once(where + "significance map under mb_xy(" + std::to_string(hs->mb_x) + ", " + std::to_string(hs->mb_y) +
+                  "), the device's is (" + std::to_string(m.x) + ", " + std::to_string(m.y) + ")");
+  else if (!h->sub_open || memcmp(h->sub_args, m.sub, sizeof(m.sub)) != 0)
+    hs->fail_once(where + "significance map outside the device's sub-macroblock (cat " + std::to_string(m.sub[0]) +
+                  ", scan8 " + std::to_string(m.sub[1]) + ", max " + std::to_string(m.sub[2]) + ")");
 }
 
 void avr_hook_end_coding_type(void* opaque, int coding_type) {
   avr_hooks_session* hs = (avr_hooks_session*)opaque;
   if (!hs || !hs->live) return;
-  if (hs->live->coding_type != coding_type) hs->fail_once("hooks: end_coding_type does not match begin_coding_type");
-  hs->live->coding_type = AVR_PIP_UNKNOWN;
+  avr_hooks_slice* h = hs->live;
+  if (h->coding_type != coding_type) hs->fail_once("hooks: end_coding_type does not match begin_coding_type");
+  h->coding_type = AVR_PIP_UNKNOWN;
+  if (coding_type != AVR_PIP_SIGNIFICANCE_MAP || h->map_cur >= h->nmaps) return;
+  const HookMap& m = h->maps[h->map_cur++];
+  if (h->cur != m.end)
+    hs->fail_once("hooks: slice " + std::to_string(h->index) + " bin " + std::to_string(h->cur) +
+                  ": end_coding_type(SIG_MAP) where the device's map ends at bin " + std::to_string(m.end));
 }
 
 int avr_hooks_end(avr_hooks_session* hs, uint8_t** out, size_t* out_len) {
   if (!hs || !out || !out_len) return AVR_ERR_INVALID_ARGUMENT;
-  if (hs->live && hs->live->cur != hs->live->nbins)
-    hs->fail_once("hooks: slice " + std::to_string(hs->live->index) + " ended after " +
-                  std::to_string(hs->live->cur) + " of " + std::to_string(hs->live->nbins) + " bins");
-  hs->live = nullptr;
+  close_live(hs);
   if (hs->next_slice != hs->pf.slices.size())
     hs->fail_once("hooks: " + std::to_string(hs->next_slice) + " of " + std::to_string(hs->pf.slices.size()) +
                   " slices were decoded");

@@ -74,10 +74,17 @@ AVR_FI void record_placement(int s, int wave) {
 
 // MODE_TRACE: the compress-side CABAC decode + parse alone, recording every bin in decode order
 // (2 bytes: bin | kind << 1, the context's state byte before the bin) -- the bin sequence the
-// libavcodec-hooks layer (avr_hook_*) serves to its caller.
+// libavcodec-hooks layer (avr_hook_*) serves to its caller -- and, between the bins, the model
+// events that decide the model keys (kind 3 records, TRACE_EV_*): where each significance map
+// begins and ends, with the model coordinates (mb_xy) and sub-macroblock (begin_sub_mb) it runs
+// under; the hooks layer checks the caller's begin/end_coding_type(SIG_MAP), mb_xy and
+// begin_sub_mb against them (recode.cpp:166-207, 951-974).
 enum { MODE_COMPRESS = 0, MODE_DECOMPRESS = 1, MODE_GENERATE = 2, MODE_TRACE = 3 };
 enum { F_DEC = 1, F_SKIP = 2, F_INTRA = 4, F_I16 = 8, F_D16 = 16, F_T8 = 32, F_CPRED = 64 };
 enum { SE_OTHER = 0, SE_REF, SE_QPDELTA, SE_MVD_SUFFIX, SE_LEVEL_SUFFIX, SE_EOS, SE_PCM };
+// MODE_TRACE event records: 0x06 (kind 3), type, payload.  MAP_BEGIN: mb_x, model row (u16 LE
+// each), cat, scan8 index, max_coeff, is_dc | chroma422 << 1 (10 bytes); MAP_END: 2 bytes.
+enum { TRACE_EV_MAP_BEGIN = 1, TRACE_EV_MAP_END = 2 };
 
 static __constant__ uint8_t c_scan8[51] = {
   4 + 1 * 8,  5 + 1 * 8,  4 + 2 * 8,  5 + 2 * 8,  6 + 1 * 8,  7 + 1 * 8,  6 + 2 * 8,  7 + 2 * 8,
@@ -598,6 +605,23 @@ struct Walker {
   AVR_FI void trace(int b, uint32_t kind, uint32_t s) {
     out_byte(out, (uint32_t)b | kind << 1);
     out_byte(out, s);
+  }
+  AVR_FI void trace_map_begin(int cat, int n, int max, int is_dc, int c422) {
+    const uint32_t y = (uint32_t)mrow();
+    out_byte(out, 3u << 1);
+    out_byte(out, TRACE_EV_MAP_BEGIN);
+    out_byte(out, (uint32_t)mb_x & 0xff);
+    out_byte(out, (uint32_t)mb_x >> 8);
+    out_byte(out, y & 0xff);
+    out_byte(out, y >> 8);
+    out_byte(out, (uint32_t)cat);
+    out_byte(out, (uint32_t)n);
+    out_byte(out, (uint32_t)max);
+    out_byte(out, (uint32_t)is_dc | (uint32_t)c422 << 1);
+  }
+  AVR_FI void trace_map_end() {
+    out_byte(out, 3u << 1);
+    out_byte(out, TRACE_EV_MAP_END);
   }
   // a residual bin through the model on cached lane L; ctx = rc_addr(rc_cat, L)
   AVR_FI int rbin(uint32_t L, int ctx) {
@@ -1149,6 +1173,7 @@ struct Walker {
       uint64_t sigmask = 0;
       int pos, end = max - 2;
       PROF_BEGIN(t3);
+      if (MODE == MODE_TRACE) trace_map_begin(cat, n, max, is_dc, c422);
       for (pos = 0; pos < max - 1; pos++) {
         int sc, lc;
         if (max == 64) {
@@ -1164,6 +1189,7 @@ struct Walker {
         }
       }
       if (pos == max - 1) cnt++;
+      if (MODE == MODE_TRACE) trace_map_end();
       PROF_END(3, t3);
       if (MODE == MODE_COMPRESS) {
         // model: nnz first (recode.cpp:1208-1221), then the buffered map (1244-1255)

@@ -15,18 +15,60 @@
 #include "../../include/avrecode.h"
 #include "../../oracle/avr_oracle.h"
 
-static int fwd_get(void *o, uint8_t *state, int ctx_idx) { (void)ctx_idx; return avr_hook_get(o, state); }
-static int fwd_bypass(void *o) { return avr_hook_get_bypass(o); }
-static int fwd_terminate(void *o) { return avr_hook_get_terminate(o); }
+/* Perturbations (hooks_set_perturb): a caller whose hook placement differs from the device's parse
+ * in one event, which the layer must reject with AVR_ERR_FORMAT:
+ *   1  the k-th begin_coding_type(SIG_MAP) one bin late
+ *   2  frame_spec repeats picture k-1's frame_num for picture k
+ *   3  the k-th mb_xy reports x ^ 1
+ *   4  the k-th begin_sub_mb / end_sub_mb pair reports scan8 index ^ 1 */
+static int g_perturb, g_k;
+static long g_maps, g_mbs, g_subs, g_sub_bad;
+static int g_delayed;   /* a begin_coding_type(SIG_MAP) waiting for the next bin */
+static void *g_session;
+void hooks_set_perturb(int mode, int k) { g_perturb = mode; g_k = k; g_maps = g_mbs = g_subs = 0; g_delayed = 0; }
+
+static void flush_delayed(void) {
+  if (g_delayed) { g_delayed = 0; avr_hook_begin_coding_type(g_session, AVR_PIP_SIGNIFICANCE_MAP, 0, 0, 0); }
+}
+static int fwd_get(void *o, uint8_t *state, int ctx_idx) {
+  (void)ctx_idx;
+  int b = avr_hook_get(o, state);   /* the delayed begin lands after this bin */
+  flush_delayed();
+  return b;
+}
+static int fwd_bypass(void *o) { int b = avr_hook_get_bypass(o); flush_delayed(); return b; }
+static int fwd_terminate(void *o) { int b = avr_hook_get_terminate(o); flush_delayed(); return b; }
 
 /* The model hooks go to the session (AVCodecHooks.opaque); the cabac hooks to the slice object. */
-static void *g_session;
-static void m_frame_spec(void *o, int f, int w, int h) { (void)o; avr_hook_frame_spec(g_session, f, w, h); }
-static void m_mb_xy(void *o, int x, int y) { (void)o; avr_hook_mb_xy(g_session, x, y); }
-static void m_begin_sub(void *o, int a, int b, int c, int d, int e) { (void)o; avr_hook_begin_sub_mb(g_session, a, b, c, d, e); }
-static void m_end_sub(void *o, int a, int b, int c, int d, int e) { (void)o; avr_hook_end_sub_mb(g_session, a, b, c, d, e); }
-static void m_begin_ct(void *o, avr_coding_type ct, int z, int p0, int p1) { (void)o; avr_hook_begin_coding_type(g_session, (int)ct, z, p0, p1); }
-static void m_end_ct(void *o, avr_coding_type ct) { (void)o; avr_hook_end_coding_type(g_session, (int)ct); }
+static void m_frame_spec(void *o, int f, int w, int h) {
+  (void)o;
+  if (g_perturb == 2 && f == g_k) f = g_k - 1;
+  avr_hook_frame_spec(g_session, f, w, h);
+}
+static void m_mb_xy(void *o, int x, int y) {
+  (void)o;
+  if (g_perturb == 3 && g_mbs++ == g_k) x ^= 1;
+  avr_hook_mb_xy(g_session, x, y);
+}
+static void m_begin_sub(void *o, int a, int b, int c, int d, int e) {
+  (void)o;
+  g_sub_bad = g_perturb == 4 && g_subs++ == g_k;
+  avr_hook_begin_sub_mb(g_session, a, g_sub_bad ? b ^ 1 : b, c, d, e);
+}
+static void m_end_sub(void *o, int a, int b, int c, int d, int e) {
+  (void)o;
+  avr_hook_end_sub_mb(g_session, a, g_sub_bad ? b ^ 1 : b, c, d, e);
+}
+static void m_begin_ct(void *o, avr_coding_type ct, int z, int p0, int p1) {
+  (void)o;
+  if (g_perturb == 1 && ct == PIP_SIGNIFICANCE_MAP && g_maps++ == g_k) { g_delayed = 1; return; }
+  avr_hook_begin_coding_type(g_session, (int)ct, z, p0, p1);
+}
+static void m_end_ct(void *o, avr_coding_type ct) {
+  (void)o;
+  flush_delayed();
+  avr_hook_end_coding_type(g_session, (int)ct);
+}
 
 /* Decode every CABAC slice of `stream` through the hooks (the fork's av_decoder loop,
  * recode.cpp:114-135).  Returns the number of slices walked, or < 0. */

@@ -109,3 +109,28 @@ def test_hooks_detect_a_diverging_caller():
     bad[len(bad) // 2] ^= 0x5A
     r, back, _ = _call("hooks_decompress", bytes(bad), len(bad))
     assert r != 0 or back != data or bytes(bad) == avrc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,k,what", [
+    (1, 5, "begin_coding_type(SIG_MAP) one bin late"),
+    (2, 3, "frame_num repeated across two pictures"),
+    (3, 40, "mb_xy off by one macroblock"),
+    (4, 7, "begin_sub_mb with another scan8 index"),
+])
+def test_hooks_reject_misplaced_model_events(mode, k, what):
+    """The model keys depend on where the caller places its model events (recode.cpp:166-207,
+    824-843, 951-974): a caller that differs from the device's parse in ONE of them -- %s -- would
+    get a container the reference would not write for it, so the session fails with
+    AVR_ERR_FORMAT instead of returning the device's container."""
+    L, _ = _driver()
+    L.hooks_set_perturb.argtypes = [ctypes.c_int, ctypes.c_int]
+    data = (FIX / "realshort.mp4").read_bytes()
+    try:
+        L.hooks_set_perturb(mode, k)
+        r, _, _ = _call("hooks_compress", data, len(data), 1)
+    finally:
+        L.hooks_set_perturb(0, 0)
+    assert r == -3, (what, r)
+    r, avrc, _ = _call("hooks_compress", data, len(data), 1)   # unperturbed: accepted
+    assert r == 0 and hashlib.sha256(avrc).hexdigest() == GOLD[("realshort.mp4", "P")]["avrc_sha256"]
