@@ -77,7 +77,7 @@ static long drive(const uint8_t *stream, size_t n) {
   int nn = avr_demux(stream, n, &nals);
   if (nn < 0) return -1;
   avr_param_sets_t *ps = (avr_param_sets_t *)calloc(1, sizeof(avr_param_sets_t));
-  int x264_build = -1, have_prev = 0, picture_id = 0;
+  int x264_build = -1, have_prev = 0, picture_id = 0, second_field = 0;
   avr_slice_hdr_t prev;
   long walked = 0;
   memset(&prev, 0, sizeof(prev));
@@ -101,8 +101,14 @@ static long drive(const uint8_t *stream, size_t n) {
     int new_pic = !have_prev || h.first_mb == 0 || h.first_mb <= prev.first_mb || h.frame_num != prev.frame_num ||
                   h.pps_id != prev.pps_id || h.poc_lsb != prev.poc_lsb ||
                   (h.nal_unit_type == 5) != (prev.nal_unit_type == 5) || h.idr_pic_id != prev.idr_pic_id ||
-                  (h.nal_ref_idc == 0) != (prev.nal_ref_idc == 0);
-    if (new_pic) picture_id++;
+                  (h.nal_ref_idc == 0) != (prev.nal_ref_idc == 0) || h.field_pic != prev.field_pic ||
+                  h.bottom_field != prev.bottom_field;
+    /* frame_spec's frame: the two fields of a frame share frame_num, so the second field stays
+     * in the first one's frame (update_frame_spec, recode.cpp:824-843) */
+    int second = new_pic && have_prev && h.field_pic && prev.field_pic && h.frame_num == prev.frame_num &&
+                 h.bottom_field != prev.bottom_field && !second_field;
+    if (new_pic && !second) picture_id++;
+    if (new_pic) second_field = second;
     prev = h;
     have_prev = 1;
     size_t bits = avr_rbsp_bit_length(rbsp, rl);
