@@ -75,11 +75,12 @@ __device__ __noinline__ uint32_t in_fill_call(uint8_t* lds, const uint8_t* g, ui
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
   const int lane = __lane_id();
-  const uint32_t base = at + 16u * lane;
+  constexpr int per = kStage / 64;   // bytes per lane
+  const uint32_t base = at + (uint32_t)per * lane;
 #pragma unroll
-  for (int k = 0; k < 16; k++) {
+  for (int k = 0; k < per; k++) {
     uint32_t i = base + k;
-    lds[16 * lane + k] = i < limit ? g[i] : 0;
+    lds[per * lane + k] = i < limit ? g[i] : 0;
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
