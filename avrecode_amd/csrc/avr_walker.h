@@ -403,6 +403,10 @@ AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32
   const uint32_t lane = __lane_id();
   const uint32_t ent = sh->etab[home + lane];
   const uint64_t hit = __ballot((ent >> 16) == (0x8000u | lane << 7 | tag));
+#ifdef AVR_PROFILE_EST   // with AVR_PROFILE: estimator lookups that go to HBM (scripts/diag_est.py)
+  if (lane == 0) atomicAdd(&avr_prof[22], 1ull);
+  if (lane == 0 && !hit && !__ballot(ent == 0)) atomicAdd(&avr_prof[23], 1ull);
+#endif
   if (hit) {
     const uint32_t j = (uint32_t)__builtin_ctzll(hit);
     *slot = (0x8000u | j << 7 | tag) << 16 | (home + j);
