@@ -147,6 +147,7 @@ void build_tables(avr::EngineTables* t) {
     unsigned __int128 num = (unsigned __int128)1 << (63 + l);
     t->hot.div[d][0] = (uint64_t)((num + d - 1) / d);
     t->hot.div[d][1] = (uint64_t)(l - 1);
+    t->hot.rcp32[d] = (uint32_t)((1ull << 32) / d);   // P-format coder (avr_engine.h, PEncoder)
   }
   // reverse_scan_8 neighbours (recode.cpp:279-312, 444-447)
   static const uint8_t scan8[48] = {
@@ -778,6 +779,10 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
   std::string version;
   if (!avr::pb_parse(in, n, &j->blocks, &version)) return fail(c, AVR_ERR_FORMAT, "not a Recoded protobuf");
   j->parallel = version == avr::kParallelModelTag;
+  // another avrecode-amd container format (the round-2 "avrecode-amd:P", 64-bit coder) would be
+  // read as a reference-model container and fail late: refuse it here
+  if (!j->parallel && version.rfind("avrecode-amd:", 0) == 0)
+    return fail(c, AVR_ERR_FORMAT, "unsupported container version " + version + " (expected " + avr::kParallelModelTag + ")");
   // read_packet (recode.cpp:1359-1409): literals and surrogate blocks form the stream
   uint64_t seq = 1;
   for (auto& b : j->blocks) {

@@ -31,6 +31,7 @@ __device__ __forceinline__ uint32_t hi32(uint64_t x) { return opaque_u32((uint32
 struct HotTables {
   uint64_t div[128][2];     // [d] = {m, shift}: floor(n/d) = umulhi(n, m) >> shift for n <= 2^63,
                             //   m = ceil(2^(63+l)/d), l = ceil(log2 d), shift = l - 1 (one 16-B read)
+  uint32_t rcp32[128];      // [d] = floor(2^32 / d): the P-format coder's r1 = umulhi(range, rcp32[tot]) * pos
   uint64_t cabac[128];      // [state]: LPS range for q = (range >> 6) & 3 in byte q, successor state
                             //   after an MPS in byte 4, after an LPS in byte 5 (one 8-B read per bin)
   uint8_t nb_left[48];      // get_neighbor_sub_mb: block left of n (| 128 if in the left macroblock)
@@ -556,6 +557,119 @@ __device__ __forceinline__ int rd_get(RecodedDecoder& d, InStream& in, uint64_t 
   if (hi32(d.range) < (1u << 19)) {
     rd_consume(d, in);
     if (hi32(d.range) < (1u << 23)) rd_consume(d, in);
+  }
+  return bin;
+}
+
+// ------------------------------------------------------------ P-format coder (u32 / u8 digits)
+// The parallel model's container (avrecode-amd:P32) is this library's own format, not bound to the
+// reference's arithmetic_code<uint64_t, uint8_t>: a 32-bit range coder with byte digits, the same
+// estimators and the same decision rule (bin 1 takes the top r1 of the range).
+//   range in [2^24, 2^32) between decisions (0xFFFFFFFF at the start);
+//   r1 = umulhi(range, rcp32[tot]) * pos, rcp32[tot] = floor(2^32 / tot), tot = pos + neg <= 97:
+//   r1 <= range * pos / tot, so both parts keep >= range / tot - 1 > 2^17 and ONE 8-bit
+//   renormalisation step always restores range >= 2^24.
+// Per decision that is one 32-bit multiply-high and one multiply instead of the 64-bit
+// reciprocal product (~15 scalar instructions), and 32-bit compares and selects; the coding
+// loss of the truncated quotient is below 97 / 2^24 of the range (1e-5 of a bit per decision).
+// Encoder: low holds the window (bits 0-31) and the carry (bit 32); digits are bits 24-31 at each
+// renormalisation, with the cache + 0xFF-run carry scheme of RecodedEncoder.
+struct PEncoder {
+  uint64_t low;
+  uint32_t range;
+  uint32_t pending;     // deferred 0xFF digits
+  int have_cache;
+  uint32_t cache;
+  int err;
+};
+__device__ __forceinline__ void re_init(PEncoder& e) {
+  e.low = 0;
+  e.range = 0xffffffffu;
+  e.pending = 0;
+  e.have_cache = 0;
+  e.cache = 0;
+  e.err = 0;
+}
+__device__ __forceinline__ void pe_shift(PEncoder& e, OutStream& o) {
+  const uint32_t carry = (uint32_t)(e.low >> 32) & 1u;
+  const uint32_t digit = (uint32_t)(e.low >> 24) & 0xff;
+  if (digit != 0xff || carry) {
+    if (e.have_cache) {
+      if (e.cache + carry > 0xff) e.err = 1;
+      out_byte(o, e.cache + carry);
+    } else if (carry) {
+      e.err = 1;
+    }
+    if (e.pending) out_repeat(o, (0xff + carry) & 0xff, e.pending);
+    e.pending = 0;
+    e.cache = digit;
+    e.have_cache = 1;
+  } else {
+    e.pending++;
+  }
+  e.low = (e.low & 0xffffffu) << 8;
+}
+__device__ __forceinline__ void re_put(PEncoder& e, OutStream& o, int bin, uint32_t r1) {
+  const uint32_t r0 = e.range - r1;
+  e.low += bin ? r0 : 0u;
+  e.range = bin ? r1 : r0;
+  if (e.range < (1u << 24)) {
+    pe_shift(e, o);
+    e.range <<= 8;
+  }
+}
+// billing (as re_put_billed): a digit counts when its value is final, deferred digits with it
+__device__ __forceinline__ uint32_t re_put_billed(PEncoder& e, OutStream& o, int bin, uint32_t r1, uint32_t* pend) {
+  const uint32_t r0 = e.range - r1;
+  e.low += bin ? r0 : 0u;
+  e.range = bin ? r1 : r0;
+  uint32_t bytes = 0;
+  if (e.range < (1u << 24)) {
+    const uint32_t lo = (uint32_t)e.low;
+    const bool deferred = (lo >> 24) != (uint32_t)(((uint64_t)lo + e.range - 1) >> 24);   // a carry may still come
+    bytes = deferred ? 0u : *pend + 1;
+    *pend = deferred ? *pend + 1 : 0u;
+    pe_shift(e, o);
+    e.range <<= 8;
+  }
+  return bytes;
+}
+// flush: the value in [low, low + range) with the most trailing zero bits, through its last
+// non-zero digit (the decoder reads zeros past the end)
+__device__ __forceinline__ void re_finish(PEncoder& e, OutStream& o) {
+  #pragma clang loop unroll(disable)
+  for (uint64_t sb = 1ull << 32; sb; sb >>= 1) {
+    const uint64_t x = (e.low | sb) & ~(sb - 1);
+    if (sb < e.range && e.low <= x && x < e.low + e.range) {
+      e.low = x;
+      break;
+    }
+  }
+  #pragma clang loop unroll(disable)
+  while (e.low != 0) pe_shift(e, o);
+  if (e.have_cache) out_byte(o, e.cache);
+  if (e.pending) out_repeat(o, 0xff, e.pending);
+  e.pending = 0;
+  e.have_cache = 0;
+}
+// Decoder: low = (stream value - encoder low) in the 32-bit window, always < range.
+struct PDecoder {
+  uint32_t low, range;
+  uint32_t next;        // next byte index
+};
+__device__ __forceinline__ void rd_init(PDecoder& d, InStream& in) {
+  d.low = __builtin_amdgcn_readfirstlane(in_be32(in, 0));
+  d.next = 4;
+  d.range = 0xffffffffu;
+}
+__device__ __forceinline__ int rd_get(PDecoder& d, InStream& in, uint32_t r1) {
+  const uint32_t r0 = d.range - r1;
+  const bool bin = d.low >= r0;
+  d.low = bin ? d.low - r0 : d.low;
+  d.range = bin ? r1 : r0;
+  if (d.range < (1u << 24)) {
+    d.low = (d.low << 8) | __builtin_amdgcn_readfirstlane(in_byte(in, d.next++));
+    d.range <<= 8;
   }
   return bin;
 }

@@ -8,7 +8,7 @@
 
 namespace avr {
 
-const char* const kParallelModelTag = "avrecode-amd:P";
+const char* const kParallelModelTag = "avrecode-amd:P32";   // parallel model + P-format coder (avr_engine.h)
 
 namespace {
 

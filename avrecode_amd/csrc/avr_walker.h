@@ -19,6 +19,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 #include "../../include/avrecode.h"
 #include "avr_engine.h"
@@ -499,7 +500,9 @@ struct Walker {
   CabacDecoder cd;
   CabacEncoder ce;
   RecodedEncoder re;
-  RecodedDecoder rd;
+  // the reference model's container uses arithmetic_code<uint64_t, uint8_t>; the parallel model's
+  // its own 32-bit coder (avr_engine.h, PDecoder)
+  typename std::conditional<RM, RecodedDecoder, PDecoder>::type rd;
   uint64_t rng;
   // slice state
   int W, H, mb_x, mb_y, slice_type, is_b, cat_, t8mode;
@@ -655,10 +658,15 @@ struct Walker {
   // from the constant table (s_load_dwordx4 into SGPRs, scalar-cache hit): fewer instructions on
   // the walker than three v_readlane pairs and selects from a VGPR table (measured 10 % slower).
   typedef const __attribute__((address_space(4))) uint64_t cu64;
-  AVR_FI uint64_t p1(uint32_t e) const {
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  AVR_FI auto p1(uint32_t e) const {
     const uint32_t pos = (e & 0xff) + 1, tot = pos + (e >> 8) + 1;
-    cu64* dv = (cu64*)&G->hot.div[tot][0];
-    return (__umul64hi(rd.range, dv[0]) >> (uint32_t)dv[1]) * pos;
+    if constexpr (RM) {
+      cu64* dv = (cu64*)&G->hot.div[tot][0];
+      return (__umul64hi(rd.range, dv[0]) >> (uint32_t)dv[1]) * pos;
+    } else {
+      return __umulhi(rd.range, ((cu32*)G->hot.rcp32)[tot]) * pos;   // the P-format rule
+    }
   }
   // CABAC state record of state byte s: VGPR table (two v_readlane) or, with AVR_CABAC_SMEM, a
   // scalar load
@@ -2164,7 +2172,7 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
 // finish, recode.cpp:1074, 1092-1094), gathering each op's reciprocal record with its lane;
 // decompress retires ring 0 (cabac::encoder::put / put_bypass / put_terminate,
 // recode.cpp:1443-1474, cabac_code.h:33-67).
-template <int MODE>
+template <int MODE, bool RM>
 AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out, uint32_t flags) {
   const bool billing = (flags & kFlagBill) != 0;
   uint32_t bill[6] = {0, 0, 0, 0, 0, 0};
@@ -2176,7 +2184,7 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
   o.cap = d->out_capacity;
   o.n = 0;
   o.last = 0;
-  RecodedEncoder re;
+  typename std::conditional<RM, RecodedEncoder, PEncoder>::type re;   // see Walker::rd
   CabacEncoder ce;
   VTab vt;
   if (MODE == MODE_COMPRESS) {
@@ -2206,8 +2214,18 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
     follow_prio(sh, &prio);
     if (MODE == MODE_COMPRESS) {
       const uint32_t tot_v = (op_v >> 8) & 127;
-      const uint64_t m_v = T->div[tot_v][0];
-      const uint32_t s_v = (uint32_t)T->div[tot_v][1];
+      const uint64_t m_v = RM ? T->div[tot_v][0] : T->rcp32[tot_v];
+      const uint32_t s_v = RM ? (uint32_t)T->div[tot_v][1] : 0u;
+      // r1 of op j: the reference coder's exact quotient, or the P-format rule (avr_engine.h)
+      auto r1_of = [&](uint32_t j, uint32_t op) {
+        if constexpr (RM) {
+          const uint64_t m = readlane64(m_v, j);
+          const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
+          return (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
+        } else {
+          return __umulhi(re.range, __builtin_amdgcn_readlane((uint32_t)m_v, j)) * ((op >> 1) & 127);
+        }
+      };
       asm volatile("; MARK_CODER_BEGIN");
       // control ops (FINISH, END: once per slice) located up front, so the put loop has no checks
       uint64_t ctrl = __ballot(__lane_id() < n && (op_v & (OP_END | OP_FINISH)));
@@ -2216,20 +2234,14 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
         if (billing) {
           for (; j < stop; j++) {
             const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
-            const uint64_t m = readlane64(m_v, j);
-            const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
-            const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
-            const uint32_t bytes = re_put_billed(re, o, op & 1, p1, &bill_pend);
+            const uint32_t bytes = re_put_billed(re, o, op & 1, r1_of(j, op), &bill_pend);
             const int c = op_class_pip_c((op >> OPC_SHIFT_C) & 3);
             if (bytes) bill[c] += bytes;
           }
         } else {
           for (; j < stop; j++) {
             const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
-            const uint64_t m = readlane64(m_v, j);
-            const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
-            const uint64_t p1 = (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
-            re_put(re, o, op & 1, p1);
+            re_put(re, o, op & 1, r1_of(j, op));
           }
         }
         if (j >= n) break;
@@ -2396,7 +2408,7 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
     AVR_PLACE_T(s, 1);
   }
   else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
-  else coder_slice<MODE>(w.sh, w.T, d, out, flags);
+  else coder_slice<MODE, false>(w.sh, w.T, d, out, flags);
   __syncthreads();
   if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
 }
@@ -2489,7 +2501,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
     const int wave = tid >> 6;
     if (wave == 0) walker_slice(w, d, in, &res[s]);
     else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
-    else coder_slice<MODE>(w.sh, w.T, d, out, flags);
+    else coder_slice<MODE, true>(w.sh, w.T, d, out, flags);
     __syncthreads();
     if (tid == 0) finish_slice<MODE>(w.sh, d, &res[s]);
     __syncthreads();

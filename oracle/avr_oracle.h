@@ -88,6 +88,35 @@ static inline uint64_t rc_p1(uint64_t range, int pos, int neg) {
 void rc_enc_init(ac_enc_t *e, obuf_t *out);
 void rc_dec_init(ac_dec_t *d, const uint8_t *in, size_t n);
 
+/* P-format coder: NOT part of the reference.  The parallel model's container (tag
+ * "avrecode-amd:P32") is this library's own format and codes the model's decisions with a 32-bit
+ * range coder with byte digits (avrecode_amd/csrc/avr_engine.h, PEncoder / PDecoder), restated
+ * here: range in [2^24, 2^32) between decisions (0xFFFFFFFF at the start), bin 1 takes the top
+ * r1 = floor(range * floor(2^32 / tot) / 2^32) * pos of the range (tot = pos + neg), one 8-bit
+ * renormalisation step when range < 2^24. */
+typedef struct {
+  uint64_t low;           /* window bits 0-31, carry bit 32 */
+  uint32_t range, pending, cache;
+  int have_cache, err;
+  uint32_t bill_pend;     /* digits the billing rule still defers */
+  obuf_t *out;
+} pc_enc_t;
+typedef struct {
+  uint32_t low, range;
+  const uint8_t *in, *end;
+} pc_dec_t;
+static inline uint32_t pc_p1(uint32_t range, int pos, int neg) {
+  const uint32_t rcp = (uint32_t)((1ull << 32) / (uint64_t)(pos + neg));
+  return (uint32_t)(((uint64_t)range * rcp) >> 32) * (uint32_t)pos;
+}
+void pc_enc_init(pc_enc_t *e, obuf_t *out);
+/* returns the bytes billed to this put: at a renormalisation, the digit and every digit deferred
+ * before it once its value is final (as arithmetic_code::encoder::put reports, arith:146-175) */
+size_t pc_enc_put(pc_enc_t *e, int symbol, uint32_t r1);
+void pc_enc_finish(pc_enc_t *e);
+void pc_dec_init(pc_dec_t *d, const uint8_t *in, size_t n);
+int pc_dec_get(pc_dec_t *d, uint32_t r1);
+
 /* ------------------------------------------------------------------------------------------ */
 /* CABAC tables (ITU-T H.264 Tables 9-12..9-33, 9-44, 9-45) in FFmpeg layout                   */
 extern uint8_t avr_lps_range[4 * 128];    /* [q*128 + state], state=(pStateIdx<<1)|valMPS  */

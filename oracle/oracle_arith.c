@@ -178,6 +178,80 @@ int ac_dec_get(ac_dec_t *d, uint64_t range_of_1) {
 void rc_enc_init(ac_enc_t *e, obuf_t *out) { ac_enc_init(e, out, 64, 8, 0, 0); }
 void rc_dec_init(ac_dec_t *d, const uint8_t *in, size_t n) { ac_dec_init(d, in, in + n, 64, 8, 0); }
 
+/* ---------------------------------------------------------------- P-format coder (avr_oracle.h) */
+void pc_enc_init(pc_enc_t *e, obuf_t *out) {
+  memset(e, 0, sizeof(*e));
+  e->range = 0xffffffffu;
+  e->out = out;
+}
+static void pc_shift(pc_enc_t *e) {
+  const uint32_t carry = (uint32_t)(e->low >> 32) & 1u, digit = (uint32_t)(e->low >> 24) & 0xff;
+  if (digit != 0xff || carry) {
+    if (e->have_cache) {
+      if (e->cache + carry > 0xff) e->err = 1;
+      ob_put(e->out, (uint8_t)(e->cache + carry));
+    } else if (carry) {
+      e->err = 1;
+    }
+    for (; e->pending; e->pending--) ob_put(e->out, (uint8_t)(0xff + carry));
+    e->cache = digit;
+    e->have_cache = 1;
+  } else {
+    e->pending++;
+  }
+  e->low = (e->low & 0xffffffu) << 8;
+}
+size_t pc_enc_put(pc_enc_t *e, int symbol, uint32_t r1) {
+  const uint32_t r0 = e->range - r1;
+  if (symbol) e->low += r0;
+  e->range = symbol ? r1 : r0;
+  size_t billed = 0;
+  if (e->range < (1u << 24)) {
+    const uint64_t lo = e->low & 0xffffffffu;
+    if ((lo >> 24) != ((lo + e->range - 1) >> 24)) {
+      e->bill_pend++;
+    } else {
+      billed = e->bill_pend + 1;
+      e->bill_pend = 0;
+    }
+    pc_shift(e);
+    e->range <<= 8;
+  }
+  return billed;
+}
+void pc_enc_finish(pc_enc_t *e) {
+  for (uint64_t sb = 1ull << 32; sb; sb >>= 1) {
+    const uint64_t x = (e->low | sb) & ~(sb - 1);
+    if (sb < e->range && e->low <= x && x < e->low + e->range) {
+      e->low = x;
+      break;
+    }
+  }
+  while (e->low != 0) pc_shift(e);
+  if (e->have_cache) ob_put(e->out, (uint8_t)e->cache);
+  for (; e->pending; e->pending--) ob_put(e->out, 0xff);
+  e->have_cache = 0;
+}
+static uint32_t pc_byte(pc_dec_t *d) { return d->in < d->end ? *d->in++ : 0u; }   /* zeros past the end */
+void pc_dec_init(pc_dec_t *d, const uint8_t *in, size_t n) {
+  d->in = in;
+  d->end = in + n;
+  d->low = 0;
+  for (int i = 0; i < 4; i++) d->low = d->low << 8 | pc_byte(d);
+  d->range = 0xffffffffu;
+}
+int pc_dec_get(pc_dec_t *d, uint32_t r1) {
+  const uint32_t r0 = d->range - r1;
+  const int bin = d->low >= r0;
+  if (bin) d->low -= r0;
+  d->range = bin ? r1 : r0;
+  if (d->range < (1u << 24)) {
+    d->low = d->low << 8 | pc_byte(d);
+    d->range <<= 8;
+  }
+  return bin;
+}
+
 /* ---------------------------------------------------------------- CABAC re-encoder (cabac_code.h) */
 static int ilog2_u64(uint64_t x) { /* cabac_code.h:70-79 */
   int i = 0;
@@ -274,10 +348,25 @@ int cabac_dec_terminate(cabac_dec_t *d) { /* 9.3.3.2.2.3 */
 /* ---------------------------------------------------------------- op scripts (tests) */
 /* Runs the same op scripts as oracle/ref_arith_driver.cpp.  ops = quads (op, a, b, c):
  *   's' sym pos neg (recoded), 'd' sym state (cabac), 'b' sym, 't' sym, 'f' finish.
- * kind 0 = recoded coder, 1 = CABAC coder.  Returns bytes written (or -1 if cap too small). */
+ * kind 0 = recoded coder, 1 = CABAC coder, 2 = P-format coder.  Returns bytes written (or -1 if cap
+ * too small). */
 long avr_script_run(int kind, const int32_t *ops, size_t nops, uint8_t *out, size_t cap) {
   obuf_t o;
   ob_init(&o);
+  if (kind == 2) { /* the P-format coder: 's' ops, 'f' ends the stream */
+    pc_enc_t pc;
+    pc_enc_init(&pc, &o);
+    for (size_t i = 0; i < nops; i++) {
+      const int32_t *q = ops + 4 * i;
+      if (q[0] == 's') pc_enc_put(&pc, q[1], pc_p1(pc.range, q[2], q[3]));
+    }
+    pc_enc_finish(&pc);
+    long n = pc.err ? -2 : (long)o.len;
+    if (n >= 0 && o.len > cap) n = -1;
+    else if (n >= 0) memcpy(out, o.data, o.len);
+    ob_free(&o);
+    return n;
+  }
   ac_enc_t rc;
   cabac_enc_t cb;
   if (kind == 0) rc_enc_init(&rc, &o);
@@ -311,6 +400,20 @@ long avr_script_decode_recoded(const uint8_t *in, size_t n, const int32_t *ops, 
     const int32_t *q = ops + 4 * i;
     if (q[0] != 's') continue;
     if (ac_dec_get(&d, rc_p1(d.range, q[2], q[3])) != q[1]) return ok;
+    ok++;
+  }
+  return ok;
+}
+
+/* decode a P-format stream with the given (pos, neg) sequence; returns #symbols matching */
+long avr_script_decode_p(const uint8_t *in, size_t n, const int32_t *ops, size_t nops) {
+  pc_dec_t d;
+  pc_dec_init(&d, in, n);
+  long ok = 0;
+  for (size_t i = 0; i < nops; i++) {
+    const int32_t *q = ops + 4 * i;
+    if (q[0] != 's') continue;
+    if (pc_dec_get(&d, pc_p1(d.range, q[2], q[3])) != q[1]) return ok;
     ok++;
   }
   return ok;

@@ -225,7 +225,7 @@ uint64_t model_p1(avr_model_t *m, uint64_t range, model_key_t key) {
   FILE *kl = keylog_file();
   if (kl) fwrite(&key, sizeof(key), 1, kl);
   estimator_t *e = estimator(m, key);
-  return rc_p1(range, e->pos, e->neg);
+  return m->p32 ? pc_p1((uint32_t)range, e->pos, e->neg) : rc_p1(range, e->pos, e->neg);
 }
 
 /* update_frame_spec (824-843) */

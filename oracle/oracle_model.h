@@ -43,6 +43,7 @@ struct avr_model {
   uint8_t *used;
   size_t cap, count;
   int decompress_side; /* set by the decompressor driver: see finished_queueing */
+  int p32;             /* the parallel model's container: P-format coder (pc_p1), not rc_p1 */
   size_t bill[8], cabac_bill[8];
 };
 

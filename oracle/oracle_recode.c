@@ -28,7 +28,7 @@
 avr_stats_t avr_last_stats;
 size_t avr_last_bill[8], avr_last_cabac_bill[8];
 static const int SURROGATE_MARKER_BYTES = 8; /* recode.cpp:27 */
-#define AVR_P_MODE_TAG "avrecode-amd:P"
+#define AVR_P_MODE_TAG "avrecode-amd:P32"   /* the parallel model + P-format coder (avr_oracle.h) */
 
 /* ===================================================================== protobuf wire codec */
 static void pb_varint(obuf_t *o, uint64_t v) {
@@ -189,22 +189,29 @@ typedef struct {
   avr_model_t *model;
   cabac_dec_t dec;
   obuf_t enc_out;
-  ac_enc_t enc;
+  ac_enc_t enc;       /* reference model: arithmetic_code<uint64_t, uint8_t> */
+  pc_enc_t penc;      /* parallel model (model->p32): the P-format coder */
   int queueing;
   int *bsym, *bctx, nbuf, capbuf;
   int finished;
   size_t bins;
 } cdrv_t;
 
+static size_t c_put(cdrv_t *c, int symbol, model_key_t key) { /* encoder::put of the model's coder */
+  avr_model_t *m = c->model;
+  if (m->p32) return pc_enc_put(&c->penc, symbol, (uint32_t)model_p1(m, c->penc.range, key));
+  return ac_enc_put(&c->enc, symbol, model_p1(m, c->enc.range, key));
+}
 static void c_execute(cdrv_t *c, int symbol, int ctx) { /* h264_symbol::execute (1068-1096) */
   avr_model_t *m = c->model;
   if (m->coding_type != PIP_SIGNIFICANCE_EOB) {
-    size_t billable = ac_enc_put(&c->enc, symbol, model_p1(m, c->enc.range, model_get_key(m, ctx)));
+    size_t billable = c_put(c, symbol, model_get_key(m, ctx));
     m->bill[m->coding_type] += billable;
   }
   model_update_state(m, symbol, ctx);
   if (ctx == K_TERMINATE && symbol) {
-    ac_enc_finish(&c->enc);
+    if (m->p32) pc_enc_finish(&c->penc);
+    else ac_enc_finish(&c->enc);
     c->finished = 1;
   }
 }
@@ -243,7 +250,7 @@ static int c_get_terminate(void *o) {
 }
 static void c_put_nz(void *ctx, avr_model_t *m, model_key_t key, int *symbol) { /* 1213-1221 */
   cdrv_t *c = (cdrv_t *)ctx;
-  size_t billable = ac_enc_put(&c->enc, *symbol, model_p1(m, c->enc.range, key));
+  size_t billable = c_put(c, *symbol, key);
   model_update_key(m, *symbol, key);
   m->bill[m->coding_type] += billable;
 }
@@ -271,12 +278,18 @@ static void c_end_coding_type(void *o, avr_coding_type ct) {
 /* ==================================================== decompressor::cabac_decoder (1411-1520) */
 typedef struct {
   avr_model_t *model;
-  ac_dec_t dec;
+  ac_dec_t dec;       /* reference model */
+  pc_dec_t pdec;      /* parallel model (model->p32) */
   cabac_enc_t cenc;
   obuf_t cabac_out;
   int finished;
 } ddrv_t;
 
+static int d_dec(ddrv_t *d, model_key_t key) { /* decoder::get of the model's coder */
+  avr_model_t *m = d->model;
+  if (m->p32) return pc_dec_get(&d->pdec, (uint32_t)model_p1(m, d->pdec.range, key));
+  return ac_dec_get(&d->dec, model_p1(m, d->dec.range, key));
+}
 static int d_get(void *o, uint8_t *state, int ctx) {
   ddrv_t *d = (ddrv_t *)o;
   avr_model_t *m = d->model;
@@ -285,7 +298,7 @@ static int d_get(void *o, uint8_t *state, int ctx) {
     model_key_t k = model_get_key(m, ctx);
     s = (int)((k >> 24) & 0xffffff); /* std::get<1>(key) */
   } else {
-    s = ac_dec_get(&d->dec, model_p1(m, d->dec.range, model_get_key(m, ctx)));
+    s = d_dec(d, model_get_key(m, ctx));
   }
   m->cabac_bill[m->coding_type] += cabac_enc_put(&d->cenc, s, state);
   model_update_state(m, s, ctx);
@@ -293,14 +306,14 @@ static int d_get(void *o, uint8_t *state, int ctx) {
 }
 static int d_get_bypass(void *o) {
   ddrv_t *d = (ddrv_t *)o;
-  int s = ac_dec_get(&d->dec, model_p1(d->model, d->dec.range, model_get_key(d->model, K_BYPASS)));
+  int s = d_dec(d, model_get_key(d->model, K_BYPASS));
   model_update_state(d->model, s, K_BYPASS);
   d->model->cabac_bill[d->model->coding_type] += cabac_enc_put_bypass(&d->cenc, s);
   return s;
 }
 static int d_get_terminate(void *o) {
   ddrv_t *d = (ddrv_t *)o;
-  int s = ac_dec_get(&d->dec, model_p1(d->model, d->dec.range, model_get_key(d->model, K_TERMINATE)));
+  int s = d_dec(d, model_get_key(d->model, K_TERMINATE));
   model_update_state(d->model, s, K_TERMINATE);
   d->model->cabac_bill[d->model->coding_type] += cabac_enc_put_terminate(&d->cenc, s);
   if (s) {
@@ -311,7 +324,7 @@ static int d_get_terminate(void *o) {
 }
 static void d_get_nz(void *ctx, avr_model_t *m, model_key_t key, int *symbol) { /* 1481-1486 */
   ddrv_t *d = (ddrv_t *)ctx;
-  *symbol = ac_dec_get(&d->dec, model_p1(m, d->dec.range, key));
+  *symbol = d_dec(d, key);
   model_update_key(m, *symbol, key);
 }
 static void d_begin_coding_type(void *o, avr_coding_type ct, int zz, int p0, int p1) {
@@ -465,18 +478,27 @@ static int slice_recodable(const slice_t *s) {
   return ok;
 }
 
+/* a fresh parallel model: its container uses the P-format coder */
+static avr_model_t *model_new_p(void) {
+  avr_model_t *m = avr_model_new();
+  m->p32 = 1;
+  return m;
+}
+
 static int compress_slice_with_model(avr_model_t *m, const slice_t *s, obuf_t *recoded, size_t *bins) {
   cdrv_t c;
   memset(&c, 0, sizeof(c));
   c.model = m;
   cabac_dec_init(&c.dec, s->payload, s->rbsp_len - s->h.cabac_start);
   ob_init(&c.enc_out);
-  rc_enc_init(&c.enc, &c.enc_out);
+  if (m->p32) pc_enc_init(&c.penc, &c.enc_out);
+  else rc_enc_init(&c.enc, &c.enc_out);
   c.queueing = PIP_UNKNOWN;
   avr_hooks_t hk = {&c, c_get, c_get_bypass, c_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
                     h_end_sub_mb, c_begin_coding_type, c_end_coding_type};
   int ret = avr_walk_slice(&s->h, &hk, s->picture_id);
-  ac_enc_free(&c.enc);
+  if (!m->p32) ac_enc_free(&c.enc);
+  else if (c.penc.err) ret = -23;   /* carry into a finished digit: cannot happen */
   free(c.bsym);
   free(c.bctx);
   if (ret == 0 && !c.finished) ret = -21;
@@ -491,7 +513,8 @@ static int decompress_slice_with_model(avr_model_t *m, const avr_slice_hdr_t *h,
   memset(&d, 0, sizeof(d));
   d.model = m;
   m->decompress_side = 1;
-  rc_dec_init(&d.dec, rc, rn);
+  if (m->p32) pc_dec_init(&d.pdec, rc, rn);
+  else rc_dec_init(&d.dec, rc, rn);
   ob_init(&d.cabac_out);
   cabac_enc_init(&d.cenc, &d.cabac_out);
   avr_hooks_t hk = {&d, d_get, d_get_bypass, d_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
@@ -509,19 +532,19 @@ int avr_compress_slice_p(const avr_slice_hdr_t *h, const uint8_t *payload, size_
   s.h = *h;
   s.payload = payload;
   s.rbsp_len = n + h->cabac_start;
-  avr_model_t *m = avr_model_new();
+  avr_model_t *m = model_new_p();
   int r = compress_slice_with_model(m, &s, recoded, bins);
   avr_model_free(m);
   return r;
 }
 static int decompress_slice_with_model_fresh(const slice_t *s, const uint8_t *rc, size_t n, obuf_t *cabac) {
-  avr_model_t *m = avr_model_new();
+  avr_model_t *m = model_new_p();
   int r = decompress_slice_with_model(m, &s->h, s->picture_id, rc, n, cabac);
   avr_model_free(m);
   return r;
 }
 int avr_decompress_slice_p(const avr_slice_hdr_t *h, const uint8_t *rc, size_t n, obuf_t *cabac) {
-  avr_model_t *m = avr_model_new();
+  avr_model_t *m = model_new_p();
   int r = decompress_slice_with_model(m, h, 0, rc, n, cabac);
   avr_model_free(m);
   return r;
@@ -556,7 +579,7 @@ long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int ch
       size_t bins = 0;
       int rcs = -30;
       if (s.h.supported) {
-        avr_model_t *m = avr_model_new();
+        avr_model_t *m = model_new_p();
         rcs = compress_slice_with_model(m, &s, &rc, &bins);
         avr_model_free(m);
       } else {
@@ -622,7 +645,7 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
       lit.literal_len = gap;
       avr_pb_put_block(&o, &lit);
       prev_end += gap + s.size;
-      avr_model_t *m = mode == AVR_MODE_R ? model : avr_model_new();
+      avr_model_t *m = mode == AVR_MODE_R ? model : model_new_p();
       obuf_t rc;
       size_t bins = 0;
       int r = compress_slice_with_model(m, &s, &rc, &bins);
@@ -734,7 +757,7 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
     if (b->has_cabac) {
       avr_model_t *m = model;
       avr_model_t *fresh = NULL;
-      if (!mode_r) m = fresh = avr_model_new();
+      if (!mode_r) m = fresh = model_new_p();
       obuf_t cab;
       int r = decompress_slice_with_model(m, &s.h, s.picture_id, b->cabac, b->cabac_len, &cab);
       if (fresh) {

@@ -30,6 +30,8 @@ def lib():
     L.avr_script_decode_recoded.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
     L.avr_script_decode_cabac.restype = ctypes.c_long
     L.avr_script_decode_cabac.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    L.avr_script_decode_p.restype = ctypes.c_long
+    L.avr_script_decode_p.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
     return L
 
 
@@ -41,18 +43,19 @@ def _ops_array(ops):
 
 
 def script_encode(kind, ops):
-    """kind: 'recoded' or 'cabac'; ops: list of (op, a, b, c).  Returns bytes."""
+    """kind: 'recoded', 'cabac' or 'p' (the P-format coder); ops: list of (op, a, b, c).  Returns bytes."""
     arr = _ops_array(ops)
     cap = 64 + 4 * len(ops)
     buf = ctypes.create_string_buffer(cap)
-    n = lib().avr_script_run(0 if kind == "recoded" else 1, arr, len(ops), buf, cap)
+    n = lib().avr_script_run({"recoded": 0, "cabac": 1, "p": 2}[kind], arr, len(ops), buf, cap)
     assert n >= 0
     return buf.raw[:n]
 
 
 def script_decode_ok(kind, data, ops):
     arr = _ops_array(ops)
-    fn = lib().avr_script_decode_recoded if kind == "recoded" else lib().avr_script_decode_cabac
+    fn = {"recoded": lib().avr_script_decode_recoded, "cabac": lib().avr_script_decode_cabac,
+          "p": lib().avr_script_decode_p}[kind]
     return fn(data, len(data), arr, len(ops))
 
 

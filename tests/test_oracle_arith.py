@@ -74,3 +74,76 @@ def test_live_reference_random_scripts():
         text = "recoded\n" + "\n".join(f"s {a} {b} {c}" if o == "s" else "f" for o, a, b, c in ops) + "\n"
         r = subprocess.run([str(ref)], input=text, capture_output=True, text=True, check=True)
         assert r.stdout.split()[0] == script_encode("recoded", ops).hex()
+
+
+# --------------------------------------------------------------------------- P-format coder
+# The parallel model's container ("avrecode-amd:P32") is this library's own format: its coder
+# has no reference implementation to be pinned against.  It is pinned here against an
+# independent restatement in exact integer arithmetic (the whole coded value as one Python int),
+# and the GPU's P-mode output is pinned against the oracle by the -m gpu parity tests.
+def _p1(rng_, pos, neg):
+    return ((rng_ * ((1 << 32) // (pos + neg))) >> 32) * pos
+
+
+def _p_encode_bigint(ops):
+    low, rng_, k = 0, 0xFFFFFFFF, 0
+    for op in ops:
+        if op[0] != "s":
+            continue
+        r1 = _p1(rng_, op[2], op[3])
+        r0 = rng_ - r1
+        assert r1 > 0 and r0 > 0
+        if op[1]:
+            low += r0
+            rng_ = r1
+        else:
+            rng_ = r0
+        if rng_ < 1 << 24:
+            low, rng_, k = low << 8, rng_ << 8, k + 1
+    sb = 1 << 31
+    while sb:
+        x = (low | sb) & ~(sb - 1)
+        if sb < rng_ and low <= x < low + rng_:
+            low = x
+            break
+        sb >>= 1
+    return low.to_bytes(k + 4, "big").rstrip(b"\0")
+
+
+def _p_scripts():
+    out = []
+    for seed, n, skew in [(21, 0, 0), (22, 1, 0), (23, 300, 0), (24, 5000, 0), (25, 5000, 1), (26, 40000, 2)]:
+        rng = random.Random(seed)
+        ops = []
+        for _ in range(n):
+            if skew == 2:
+                pos, neg = rng.choice([(1, 95), (95, 1), (48, 48), (1, 1)])
+            else:
+                pos, neg = rng.randint(1, 0x60), rng.randint(1, 0x60)
+            p = pos / (pos + neg)
+            ops.append(("s", int(rng.random() < (p if skew != 1 else 1 - p)), pos, neg))
+        out.append((seed, ops + [("f", 0, 0, 0)]))
+    return out
+
+
+@pytest.mark.parametrize("seed,ops", _p_scripts(), ids=lambda v: str(v) if isinstance(v, int) else "")
+def test_p_coder_matches_exact_restatement(seed, ops):
+    out = script_encode("p", ops)
+    assert out == _p_encode_bigint(ops)
+    assert script_decode_ok("p", out, ops) == sum(1 for o in ops if o[0] == "s")
+
+
+def test_p_coder_costs_no_more_than_the_reference_coder():
+    """The 32-bit coder's truncated quotient costs < 1e-5 bit per decision: within a few bytes
+    of the reference's arithmetic_code<uint64_t, uint8_t> on the same decisions."""
+    for seed, ops in _p_scripts()[3:]:
+        p, r = script_encode("p", ops), script_encode("recoded", ops)
+        assert len(p) <= len(r) + 4, (seed, len(p), len(r))
+
+
+def test_p_coder_carry_chain():
+    # a run of near-certain ones after a long run of 0xFF digits forces carries through them
+    ops = [("s", 0, 1, 96)] * 3000 + [("s", 1, 1, 96)] * 20 + [("s", 1, 96, 1)] * 5000 + [("f", 0, 0, 0)]
+    out = script_encode("p", ops)
+    assert out == _p_encode_bigint(ops)
+    assert script_decode_ok("p", out, ops) == len(ops) - 1
