@@ -1903,6 +1903,9 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
     SPROF_ENDW(7, ps7);
     if (eos) break;
     if (Walker<MODE, RM, FLD>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = AVR_SLICE_OVERREAD; break; }
+    // a P32 decoder reads at most 4 bytes past its stream (rd_init's window): a damaged stream is
+    // stopped within a macroblock of running off its end
+    if (MODE == MODE_DECOMPRESS && !RM && w.in.limit && w.rd.next > w.in.limit + 8) { w.err = AVR_SLICE_OVERREAD; break; }
     addr++;
     if ((FLD && w.mbaff) && !(w.pst & Walker<MODE, RM, FLD>::PST_BOT)) {
       w.pst |= Walker<MODE, RM, FLD>::PST_BOT;
@@ -2311,8 +2314,11 @@ AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_re
   int status = sh->p_status;
   if (sh->c_err) status = AVR_SLICE_CODER;
   if (MODE == MODE_COMPRESS && !status && !sh->p_stop_ok) status = AVR_SLICE_NO_STOP;
-  if (sh->c_len > d->out_capacity) status = AVR_SLICE_OVERFLOW;
   uint32_t len = sh->c_len;
+  if (len > d->out_capacity) {   // nothing past the capacity was written: report what was
+    status = AVR_SLICE_OVERFLOW;
+    len = d->out_capacity;
+  }
   if (MODE == MODE_DECOMPRESS && !status && len && sh->c_last == 0x80) len--;  // recode.cpp:1503-1505
   res->out_len = len;
   res->status = status;
