@@ -1186,20 +1186,30 @@ struct Walker {
       int pos, end = max - 2;
       PROF_BEGIN(t3);
       if (MODE == MODE_TRACE) trace_map_begin(cat, n, max, is_dc, c422);
-      for (pos = 0; pos < max - 1; pos++) {
-        int sc, lc;
-        if (max == 64) {
-          sc = (int)__builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);
-          lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
+      // the loop once per block kind (K: 0 4x4-class, 1 chroma DC, 2 8x8), so that no per-bin
+      // code selects between them (one call site, kinds known only at run time)
+      auto map_loop = [&](auto K) {
+        constexpr int k = decltype(K)::value;
+        for (pos = 0; pos < max - 1; pos++) {
+          int sc, lc;
+          if constexpr (k == 2) {
+            sc = (int)__builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);
+            lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
+          } else if constexpr (k == 1) {
+            sc = lc = min(pos / numc8x8, 2);
+          } else {
+            sc = lc = pos;
+          }
+          if (rdecide(sc)) {
+            sigmask |= 1ull << pos;
+            cnt++;
+            if (rdecide(16 + lc)) { end = pos; break; }
+          }
         }
-        else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
-        else sc = lc = pos;
-        if (rdecide(sc)) {
-          sigmask |= 1ull << pos;
-          cnt++;
-          if (rdecide(16 + lc)) { end = pos; break; }
-        }
-      }
+      };
+      if (max == 64) map_loop(std::integral_constant<int, 2>());
+      else if (cat == 3) map_loop(std::integral_constant<int, 1>());
+      else map_loop(std::integral_constant<int, 0>());
       if (pos == max - 1) cnt++;
       if (MODE == MODE_TRACE) trace_map_end();
       PROF_END(3, t3);
@@ -1224,32 +1234,42 @@ struct Walker {
       PROF_END(4, t4);
       PROF_BEGIN(t3);
       int pos;
-      for (pos = 0; pos < max - 1; pos++) {
-        int sc, lc, zk = 0;
-        if (max == 64) {
-          const uint32_t v = __builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);   // CABAC inc | key inc << 8 (FLD)
-          sc = FLD ? (int)(v & 0xff) : (int)v;
-          zk = FLD ? (int)(v >> 8) : (int)v;
-          lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
-        }
-        else if (cat == 3) { sc = lc = min(pos / numc8x8, 2); }
-        else sc = lc = pos;
-        const int zo = max == 64 ? zk : (is_dc && c422) ? (pos < 2 ? 0 : pos < 4 ? 1 : 2) : pos;
-        const int idx = seb + (zo * (max == 64 ? 64 : 16) + nnz_m) * (max == 64 ? 64 : 16) + cnt;   // sig_est_index
-        uint32_t slot;
-        uint32_t e = est_load(sh, est_g, idx, &slot);
-        int b = rd_get(rd, in, p1(e));
-        est_store(sh, est_g, idx, slot, est_update(e, b, 0x50));
-        bins++;
-        push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3 | 1u << OPC_SHIFT_D);
-        if (b) {
-          cnt++;
-          int last = nnz_m == cnt;   // derived EOB (recode.cpp:1437-1438)
+      // one loop per block kind (K: 0 4x4-class, 1 chroma DC, 2 8x8; see the DEC side)
+      auto map_loop = [&](auto K) {
+        constexpr int k = decltype(K)::value;
+        constexpr int stride = k == 2 ? 64 : 16;
+        for (pos = 0; pos < max - 1; pos++) {
+          int sc, lc, zo;
+          if constexpr (k == 2) {
+            const uint32_t v = __builtin_amdgcn_readlane(sig8_v, (uint32_t)pos);   // CABAC inc | key inc << 8 (FLD)
+            sc = FLD ? (int)(v & 0xff) : (int)v;
+            zo = FLD ? (int)(v >> 8) : (int)v;
+            lc = (int)__builtin_amdgcn_readlane(last8_v, (uint32_t)pos);
+          } else if constexpr (k == 1) {
+            sc = lc = min(pos / numc8x8, 2);
+            zo = (is_dc && c422) ? (pos < 2 ? 0 : pos < 4 ? 1 : 2) : pos;
+          } else {
+            sc = lc = zo = pos;
+          }
+          const int idx = seb + (zo * stride + nnz_m) * stride + cnt;   // sig_est_index
+          uint32_t slot;
+          uint32_t e = est_load(sh, est_g, idx, &slot);
+          int b = rd_get(rd, in, p1(e));
+          est_store(sh, est_g, idx, slot, est_update(e, b, 0x50));
           bins++;
-          push((uint32_t)last | OPK_DECISION << 1 | (uint32_t)(lb + lc) << 3 | 2u << OPC_SHIFT_D);
-          if (last) break;
+          push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3 | 1u << OPC_SHIFT_D);
+          if (b) {
+            cnt++;
+            int last = nnz_m == cnt;   // derived EOB (recode.cpp:1437-1438)
+            bins++;
+            push((uint32_t)last | OPK_DECISION << 1 | (uint32_t)(lb + lc) << 3 | 2u << OPC_SHIFT_D);
+            if (last) break;
+          }
         }
-      }
+      };
+      if (max == 64) map_loop(std::integral_constant<int, 2>());
+      else if (cat == 3) map_loop(std::integral_constant<int, 1>());
+      else map_loop(std::integral_constant<int, 0>());
       if (pos == max - 1) cnt++;
       PROF_END(3, t3);
     } else {
