@@ -128,42 +128,41 @@ __device__ __forceinline__ bool out_overflow(const OutStream& o) { return o.n > 
 
 // ------------------------------------------------------------- CABAC state records in VGPRs
 // Per pStateIdx p (state byte s = 2p + valMPS): the four LPS ranges (byte q for
-// q = (range >> 6) & 3) and transIdxLPS[p].  Successor states follow arithmetically:
-// MPS -> s + 2 while p < 62; LPS -> 2 transIdxLPS[p] + (valMPS ^ (p == 0)).
+// q = (range >> 6) & 3) and the successor states of both state bytes of p: byte
+// (s & 1) + 2 is_lps of `nxt` (MPS -> s + 2 while p < 62; LPS -> 2 transIdxLPS[p] + (valMPS ^
+// (p == 0))), so the successor is one shift and mask of a record read with the LPS ranges.
 struct CabacRec {
-  uint32_t lps4, tlps;
+  uint32_t lps4, nxt;
 };
 __device__ __forceinline__ CabacRec rec_of(uint64_t packed) {  // from HotTables::cabac[s]
   CabacRec r;
   r.lps4 = (uint32_t)packed;
-  r.tlps = (uint32_t)(packed >> 41) & 63;
+  const uint32_t mps = (uint32_t)(packed >> 32) & 0xff, lps = (uint32_t)(packed >> 40) & 0xff;
+  r.nxt = (mps | lps << 16) * 0x101u;   // this state's successors in both byte slots
   return r;
 }
 // The table in two VGPRs (lane p); a lookup with a wave-uniform state is two independent
 // v_readlane, no LDS round trip and no branch.
 struct VTab {
-  uint32_t lps4, tlps;
+  uint32_t lps4, nxt;
 };
 __device__ __forceinline__ void vtab_load(VTab& v, const HotTables* T) {
-  const CabacRec r = rec_of(T->cabac[2 * __lane_id()]);
-  v.lps4 = r.lps4;
-  v.tlps = r.tlps;
+  const uint64_t p0 = T->cabac[2 * __lane_id()], p1 = T->cabac[2 * __lane_id() + 1];
+  v.lps4 = (uint32_t)p0;
+  v.nxt = ((uint32_t)(p0 >> 32) & 0xff) | ((uint32_t)(p1 >> 32) & 0xff) << 8 |
+          ((uint32_t)(p0 >> 40) & 0xff) << 16 | ((uint32_t)(p1 >> 40) & 0xff) << 24;
 }
 __device__ __forceinline__ CabacRec vtab_rec(const VTab& v, uint32_t s) {
   CabacRec r;
   r.lps4 = __builtin_amdgcn_readlane(v.lps4, s >> 1);
-  r.tlps = __builtin_amdgcn_readlane(v.tlps, s >> 1);
+  r.nxt = __builtin_amdgcn_readlane(v.nxt, s >> 1);
   return r;
 }
 // Shared by the decoder and the encoder: the LPS range for the current range and the successor
-// state for either outcome; is_lps is 0 or 1 and selects through masks, not booleans (a boolean
-// turned back into an integer costs a vector select and a scalar<->vector round trip).
+// state for either outcome (is_lps is 0 or 1).
 __device__ __forceinline__ uint32_t cabac_lps(uint32_t range, CabacRec r) { return (r.lps4 >> ((range >> 3) & 0x18)) & 0xff; }
 __device__ __forceinline__ uint32_t cabac_next(uint32_t s, CabacRec r, uint32_t is_lps) {
-  const uint32_t p = s >> 1;
-  const uint32_t ns_mps = s + (p < 62 ? 2u : 0u);
-  const uint32_t ns_lps = (r.tlps << 1) | ((s & 1) ^ (p == 0 ? 1u : 0u));
-  return ns_mps ^ ((ns_lps ^ ns_mps) & (0u - is_lps));
+  return (r.nxt >> (((s & 1) | is_lps << 1) << 3)) & 0xff;
 }
 
 // ---------------------------------------------------------------------- CABAC decoding engine

@@ -421,7 +421,7 @@ AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32
   }
   // HBM: slot 1 marks the entry's first store (to be logged), 0 a stored one
   const uint32_t raw = __builtin_amdgcn_readfirstlane(est_g[idx]);
-  *slot = (raw & kEstWritten) ? 0u : 1u;
+  *slot = __builtin_amdgcn_readfirstlane((raw >> 15 & 1u) ^ 1u);   // a scalar, like the LDS slots
   return raw & (kEstWritten - 1);
 }
 AVR_FI void est_store(Shared* sh, uint16_t* est_g, uint32_t idx, uint32_t slot, uint32_t e) {
@@ -561,8 +561,7 @@ struct Walker {
   // lane L of v := x (L and x wave-uniform).  Decompress: one v_writelane, no lane-mask compare
   // to keep live (R-mode decompress -1 %); compress keeps the select (v_writelane there: +2 %).
   AVR_FI static uint32_t wlane(uint32_t v, uint32_t L, uint32_t x) {
-    if (MODE == MODE_DECOMPRESS) return (uint32_t)avr_llvm_writelane((int)x, (int)L, (int)v);
-    return __lane_id() == L ? x : v;
+    return (uint32_t)avr_llvm_writelane((int)x, (int)L, (int)v);
   }
   AVR_FI int rc_addr(int cat, uint32_t j) const {
     // Only the contexts the category can use: a lane past them would alias another syntax
