@@ -205,7 +205,7 @@ __device__ __forceinline__ int cd_decide(CabacDecoder& d, InStream& in, uint32_t
   d.low -= scaled & m;
   d.range = rmps ^ ((lps ^ rmps) & m);
   *ns = cabac_next(s, r, is_lps);
-  const int n = __clz(d.range) - 23;
+  const int n = __builtin_clz(d.range) - 23;   // range >= 2 here: no zero case (one s_flbit, no clamp)
   d.range <<= n;
   d.k -= n;
   cd_refill(d, in);
@@ -296,7 +296,7 @@ __device__ __forceinline__ void ce_encode(CabacEncoder& e, OutStream& o, int bin
   e.low += rmps & m;
   e.range = rmps ^ ((lps ^ rmps) & m);
   *ns = cabac_next(s, r, is_lps);
-  const int n = __clz(e.range) - 23;   // <= 6: at most one byte per decision
+  const int n = __builtin_clz(e.range) - 23;   // <= 6: at most one byte per decision
   e.range <<= n;
   e.low <<= n;
   e.queue += n;
@@ -655,11 +655,13 @@ __device__ __forceinline__ void re_finish(PEncoder& e, OutStream& o) {
 struct PDecoder {
   uint32_t low, range;
   uint32_t next;        // next byte index
+  uint32_t pf;          // byte next, read from LDS one renormalisation ahead (its latency off the chain)
 };
 __device__ __forceinline__ void rd_init(PDecoder& d, InStream& in) {
   d.low = __builtin_amdgcn_readfirstlane(in_be32(in, 0));
   d.next = 4;
   d.range = 0xffffffffu;
+  d.pf = in_byte(in, 4);
 }
 __device__ __forceinline__ int rd_get(PDecoder& d, InStream& in, uint32_t r1) {
   const uint32_t r0 = d.range - r1;
@@ -667,7 +669,8 @@ __device__ __forceinline__ int rd_get(PDecoder& d, InStream& in, uint32_t r1) {
   d.low = bin ? d.low - r0 : d.low;
   d.range = bin ? r1 : r0;
   if (d.range < (1u << 24)) {
-    d.low = (d.low << 8) | __builtin_amdgcn_readfirstlane(in_byte(in, d.next++));
+    d.low = (d.low << 8) | __builtin_amdgcn_readfirstlane(d.pf);
+    d.pf = in_byte(in, ++d.next);
     d.range <<= 8;
   }
   return bin;
