@@ -659,7 +659,7 @@ struct Walker {
   typedef const __attribute__((address_space(4))) uint64_t cu64;
   typedef const __attribute__((address_space(4))) uint32_t cu32;
   AVR_FI auto p1(uint32_t e) const {
-    const uint32_t pos = (e & 0xff) + 1, tot = pos + (e >> 8) + 1;
+    const uint32_t pos = (e & 0xff) + 1, tot = (e & 0xff) + (e >> 8) + 2;   // the sum est_update tests
     if constexpr (RM) {
       cu64* dv = (cu64*)&G->hot.div[tot][0];
       return (__umul64hi(rd.range, dv[0]) >> (uint32_t)dv[1]) * pos;
