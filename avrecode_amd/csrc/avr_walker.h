@@ -290,6 +290,9 @@ AVR_FI void follow_prio(Shared* sh, uint32_t* cur) {
   }
 }
 
+// v_writelane_b32 (clang has no builtin for it; the LLVM intrinsic by its name)
+extern "C" __device__ int avr_llvm_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 // Producer end of ring r: entries go to LDS at once, the head counter every 32 entries (and on
 // demand), the tail is re-read only when the ring looks full.
 template <bool STAGED>
@@ -329,7 +332,11 @@ struct RingOutT {
   }
   AVR_FI void push(uint32_t op) {
     if (STAGED) {
+#ifdef AVR_WL_PUSH
+      stage_v = (uint32_t)avr_llvm_writelane((int)op, (int)stage_n, (int)stage_v);
+#else
       stage_v = __lane_id() == stage_n ? op : stage_v;
+#endif
       if (++stage_n == 64) flush();
       return;
     }
@@ -409,9 +416,11 @@ AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32
   if (lane == 0 && !hit && !__ballot(ent == 0)) atomicAdd(&avr_prof[23], 1ull);
 #endif
   if (hit) {
+    // the entry's upper half is the slot's tag word already
     const uint32_t j = (uint32_t)__builtin_ctzll(hit);
-    *slot = (0x8000u | j << 7 | tag) << 16 | (home + j);
-    return __builtin_amdgcn_readlane(ent, j) & 0xffff;
+    const uint32_t ej = __builtin_amdgcn_readlane(ent, j);
+    *slot = (ej & 0xffff0000u) | (home + j);
+    return ej & 0xffff;
   }
   const uint64_t free_v = __ballot(ent == 0);
   if (free_v) {
@@ -476,8 +485,6 @@ AVR_FI void est_table_reset(uint16_t* est_g, Shared* sh) {
 // FLD: field-coded slices (PAFF, MBAFF) -- a second instantiation (kernels of their own, launched
 // only when a batch may hold such slices: kFlagFields), so that the progressive walker carries no
 // field tests in its per-bin and per-macroblock code
-// v_writelane_b32 (clang has no builtin for it; the LLVM intrinsic by its name)
-extern "C" __device__ int avr_llvm_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
 template <int MODE, bool RM, bool FLD = false>
 struct Walker {
@@ -1176,7 +1183,7 @@ struct Walker {
   // significance map of one residual block; returns the coefficient count
   AVR_FI int sig_map(int cat, int n, int max, int is_dc, int c422) {
     const int numc8x8 = cat_ == 2 ? 2 : 1;
-    const int sb = T->sig_base[cat], lb = T->last_base[cat], seb = T->sig_est_base[cat];
+    const int sb = T->sig_base[cat], lb = T->last_base[cat], seb = (int)opaque_u32((uint32_t)T->sig_est_base[cat]);
     const int bits = max > 16 ? 6 : max > 4 ? 4 : 2;
     const int mask = (1 << bits) - 1;
     int cnt = 0;
@@ -1233,6 +1240,9 @@ struct Walker {
       PROF_END(4, t4);
       PROF_BEGIN(t3);
       int pos;
+      // the coder ops of the map's bins: scalar bases, one add of (ctxIdxInc << 3) + bin each
+      const uint32_t sop = opaque_u32((uint32_t)sb << 3 | OPK_DECISION << 1 | 1u << OPC_SHIFT_D);
+      const uint32_t lop = opaque_u32((uint32_t)lb << 3 | OPK_DECISION << 1 | 2u << OPC_SHIFT_D);
       // one loop per block kind (K: 0 4x4-class, 1 chroma DC, 2 8x8; see the DEC side)
       auto map_loop = [&](auto K) {
         constexpr int k = decltype(K)::value;
@@ -1256,12 +1266,12 @@ struct Walker {
           int b = rd_get(rd, in, p1(e));
           est_store(sh, est_g, idx, slot, est_update(e, b, 0x50));
           bins++;
-          push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)(sb + sc) << 3 | 1u << OPC_SHIFT_D);
+          push(sop + ((uint32_t)sc << 3) + (uint32_t)b);
           if (b) {
             cnt++;
             int last = nnz_m == cnt;   // derived EOB (recode.cpp:1437-1438)
             bins++;
-            push((uint32_t)last | OPK_DECISION << 1 | (uint32_t)(lb + lc) << 3 | 2u << OPC_SHIFT_D);
+            push(lop + ((uint32_t)lc << 3) + (uint32_t)last);
             if (last) break;
           }
         }
@@ -1314,7 +1324,7 @@ struct Walker {
       rc_select(cat);
       cnt = sig_map(cat, n, max, is_dc, c422);
       // coeff_abs_level_minus1 + sign, reverse scan order
-      const int ab = T->abs_base[cat];
+      const int ab = (int)opaque_u32((uint32_t)T->abs_base[cat]);   // scalar: the coder ops' base
       int gt1 = 0, eq1 = 0;
       PROF_BEGIN(t6);
       for (int i = cnt - 1; i >= 0 && !err; i--) {
