@@ -34,6 +34,7 @@ the config's 600 s) with its own roofline and CPU baseline; `--stream-shard` run
 import argparse
 import json
 import os
+import shutil
 import sys
 import time
 from pathlib import Path
@@ -74,6 +75,27 @@ def cpu_threads():
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return max(1, min(n, cap) if cap > 0 else n)
+
+
+def _split_slices(stream):
+    """An Annex-B stream's non-slice NAL units (parameter sets, ...) and its slice NAL units
+    (nal_unit_type 1 or 5), each with its start code."""
+    starts = []
+    i = stream.find(b"\x00\x00\x01")
+    while i >= 0:
+        starts.append(i + 3)
+        i = stream.find(b"\x00\x00\x01", i + 3)
+    head, nals = b"", []
+    for k, a in enumerate(starts):
+        b = starts[k + 1] - 3 if k + 1 < len(starts) else len(stream)
+        while b > a and stream[b - 1] == 0 and k + 1 < len(starts):
+            b -= 1   # a 4-byte start code's leading zero
+        unit = b"\x00\x00\x00\x01" + stream[a:b]
+        if stream[a] & 0x1F in (1, 5):
+            nals.append(unit)
+        elif not nals:
+            head += unit
+    return head, nals
 
 
 def _cpu_slice_task(job):
@@ -126,22 +148,36 @@ def cpu_baseline(ctx, args, n_bytes_hint):
     if nt > 1:
         import multiprocessing as mp
         import tempfile
-        per = max(1, -(-2 * nt // 3))
-        big = b"".join(ctx.synthesize(synth_params(qp, args.seed + j, args), per) for j, qp in enumerate(QPS))
-        n = 3 * per
-        with tempfile.NamedTemporaryFile(suffix=".264", delete=False) as fh:
-            fh.write(big)
+        # sized from the one-thread rate so the pool works ~half the budget (a stable sample, not
+        # one slice per worker): bytes = rate x threads x budget / 2, at most 128 slices per QP group
+        slice_bytes = total_bytes / max(1, slices)
+        want = (total_bytes / total_t) * nt * t_budget / 2
+        per = max(-(-2 * nt // 3), min(128, int(want / (3 * slice_bytes)) + 1))
+        # one Annex-B file per slice, so a task reads and parses only its own slice
+        tmpd = tempfile.mkdtemp(prefix="avr_cpu_")
+        paths, nbytes = [], 0
+        progress(f"cpu baseline: {3 * per} slices on {nt} host threads")
+        for j, qp in enumerate(QPS):
+            # one generator launch per QP group (slices in parallel), then cut into standalone
+            # streams: the group's parameter sets + one slice NAL unit each
+            stream = ctx.synthesize(synth_params(qp, args.seed + j, args), per)
+            head, nals = _split_slices(stream)
+            for i, nal in enumerate(nals):
+                paths.append(os.path.join(tmpd, f"s{j}_{i}.264"))
+                Path(paths[-1]).write_bytes(head + nal)
+                nbytes += len(nal)
+        n = len(paths)
         try:
             with mp.get_context("spawn").Pool(nt) as pool:
-                pool.map(_cpu_slice_task, [(fh.name, 0)] * nt)  # warm the workers (imports)
+                pool.map(_cpu_slice_task, [(paths[0], 0)] * nt)  # warm the workers (imports)
                 t0 = time.perf_counter()
-                outs = pool.map(_cpu_slice_task, [(fh.name, i) for i in range(n)], chunksize=1)
+                outs = pool.map(_cpu_slice_task, [(q, 0) for q in paths], chunksize=1)
                 dt = time.perf_counter() - t0
         finally:
-            os.unlink(fh.name)
+            shutil.rmtree(tmpd, ignore_errors=True)
         assert all(ok for ok, _ in outs)
-        line["all_cores"] = {"value": len(big) / dt / 1e6, "unit": "MB/s", "cores": nt,
-                             "sample": f"{n} slices ({len(big)} input bytes), parallel model (fresh model per "
+        line["all_cores"] = {"value": nbytes / dt / 1e6, "unit": "MB/s", "cores": nt,
+                             "sample": f"{n} slices ({nbytes} input bytes), parallel model (fresh model per "
                                        f"slice), one slice per task, {nt} worker processes, {dt:.1f} s"}
     return line
 

@@ -22,12 +22,26 @@ from avrecode_amd.batch import DeviceBatch
 data = open(sys.argv[1] + '/tests/fixtures/cockatoo.mp4', 'rb').read()
 out = {}
 with avr.Context(0) as ctx:
-    avrc = ctx.compress(data, avr.MODEL_REFERENCE)
+    cts = []
+    for _ in range(int(sys.argv[2])):
+        t0 = time.perf_counter(); avrc = ctx.compress(data, avr.MODEL_REFERENCE); cts.append(time.perf_counter() - t0)
+    out['rmode_cockatoo_compress_s'] = min(cts)
     ts = []
     for _ in range(int(sys.argv[2])):
         t0 = time.perf_counter(); r = ctx.decompress(avrc); ts.append(time.perf_counter() - t0)
         assert r == data
     out['rmode_cockatoo_decompress_s'] = min(ts)
+    if sys.argv[4] == '1':   # P-mode whole files (latency regime: few slices per CU)
+        import argparse, bench
+        clip = bench.make_clip(ctx, argparse.Namespace(mb_width=120, mb_height=68, seed=0))
+        for name, d in (('cockatoo', data), ('clip', clip)):
+            cs, ds = [], []
+            for _ in range(3):
+                t0 = time.perf_counter(); a = ctx.compress(d, avr.MODEL_PARALLEL); cs.append(time.perf_counter() - t0)
+                t0 = time.perf_counter(); r = ctx.decompress(a); ds.append(time.perf_counter() - t0)
+                assert r == d
+            out['P_' + name + '_compress_s'] = min(cs)
+            out['P_' + name + '_decompress_s'] = min(ds)
     if sys.argv[3] == '1':
         import argparse, bench
         args = argparse.Namespace(mb_width=120, mb_height=68, seed=0)
@@ -50,12 +64,13 @@ print(json.dumps(out))
 def main():
     libs = sys.argv[1:]
     batch = os.environ.get("AB_BATCH", "1")
+    pfiles = os.environ.get("AB_PFILES", "0")
     reps = os.environ.get("AB_REPS", "2")
     res = {l: [] for l in libs}
     for rnd in range(2):
         for lib in (libs if rnd == 0 else libs[::-1]):
             env = dict(os.environ, AVR_LIBRARY=str(Path(lib).resolve()))
-            p = subprocess.run([sys.executable, "-c", CHILD, str(ROOT), reps, batch], env=env, capture_output=True,
+            p = subprocess.run([sys.executable, "-c", CHILD, str(ROOT), reps, batch, pfiles], env=env, capture_output=True,
                                text=True, timeout=600)
             if p.returncode != 0:
                 print(p.stdout, p.stderr[-3000:])
