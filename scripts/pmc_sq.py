@@ -30,7 +30,10 @@ def main():
             if name is None:
                 continue
             vals[(name, r["Counter_Name"])][(p, r["Dispatch_Id"])] += float(r["Counter_Value"])
-    out = {"source": a.src, "bins_per_launch": a.bins, "kernels": {}}
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from avrecode_amd import source_sha   # the build the counters were taken on
+    out = {"source": a.src, "source_sha": source_sha(), "bins_per_launch": a.bins, "kernels": {}}
     for (name, ctr), d in sorted(vals.items()):
         per_launch = sum(d.values()) / len(d)
         k = out["kernels"].setdefault(name, {})
