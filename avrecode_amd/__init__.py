@@ -44,7 +44,8 @@ EXPORTED_SYMBOLS = (
     "avr_roundtrip_file", "avr_compress_slices", "avr_decompress_slices", "avr_pack_outputs",
     "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream", "avr_assemble_container", "avr_synthesize_stream",
     "avr_container_describe", "avr_compress_files", "avr_decompress_files",
-    "avr_hooks_compress_begin", "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
+    "avr_hooks_compress_begin", "avr_hooks_compress_stream_begin", "avr_hooks_feed",
+    "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
     "avr_hook_get_bypass", "avr_hook_get_terminate", "avr_hook_skip_bytes", "avr_hook_frame_spec", "avr_hook_mb_xy",
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
     "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables", "avr_last_phase_times",

@@ -1542,6 +1542,10 @@ struct avr_hooks_session {
   bool fs_have = false, fs_pending = false;
   int fs_num = 0, fs_w = 0, fs_h = 0, fs_slice = -1;
   int pend_num = 0, pend_w = 0, pend_h = 0;
+  // streaming compress (avr_hooks_compress_stream_begin): `original` grows by avr_hooks_feed; pf is
+  // the parse of the bytes fed so far, redone at an init_decoder after a feed (dirty)
+  bool streaming = false, dirty = false;
+  int model = 0;
   std::string err;
   void fail_once(const std::string& m) {
     if (err.empty()) err = m;
@@ -1557,13 +1561,12 @@ uint8_t next_state(uint8_t s, int bin) {
   return (uint8_t)(p == 0 ? (s ^ 1) : 2 * avr::kTransIdxLPS[p] + mps);
 }
 
-// Device trace of every coded slice of hs->pf (decode order), MODE_TRACE kernel.
-int run_traces(avr_hooks_session* hs) {
+// Device trace (MODE_TRACE kernel) of the slices `which` of hs->pf into hs->bins / hs->maps.
+int trace_slices(avr_hooks_session* hs, const std::vector<int>& which) {
   avr_ctx* c = hs->c;
   Plan plan;
   std::vector<int> slice_of;
-  for (size_t i = 0; i < hs->pf.slices.size(); i++) {
-    if (!hs->coded[i]) continue;
+  for (const int i : which) {
     const avr::SliceInfo& s = hs->pf.slices[i];
     avr_slice_desc d = desc_from_header(s);
     append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
@@ -1576,11 +1579,9 @@ int run_traces(avr_hooks_session* hs) {
     d.out_capacity = (uint32_t)std::min<uint64_t>(
         0xfffffff0ull, 32ull * s.size + 1280ull * d.mb_width * d.mb_height + 8192);
     plan.max_w = std::max(plan.max_w, ring_cols(d));
-    slice_of.push_back((int)i);
+    slice_of.push_back(i);
     plan.descs.push_back(d);
   }
-  hs->bins.assign(hs->pf.slices.size(), {});
-  hs->maps.assign(hs->pf.slices.size(), {});
   if (plan.descs.empty()) return AVR_OK;
   std::vector<avr_slice_result> res;
   std::vector<uint8_t> traces;
@@ -1595,6 +1596,8 @@ int run_traces(avr_hooks_session* hs) {
     const size_t len = res[k].out_len;
     std::vector<uint8_t>& b = hs->bins[i];
     std::vector<HookMap>& m = hs->maps[i];
+    b.clear();
+    m.clear();
     b.reserve(len);
     bool open = false;
     for (size_t at = 0; at + 2 <= len;) {
@@ -1625,6 +1628,31 @@ int run_traces(avr_hooks_session* hs) {
     }
     if (open) return fail(c, AVR_ERR_DEVICE, "hooks: device trace of slice " + std::to_string(i) + " ends in a map");
   }
+  return AVR_OK;
+}
+
+// Device trace of every coded slice of hs->pf (decode order).
+int run_traces(avr_hooks_session* hs) {
+  std::vector<int> which;
+  for (size_t i = 0; i < hs->pf.slices.size(); i++)
+    if (hs->coded[i]) which.push_back((int)i);
+  hs->bins.assign(hs->pf.slices.size(), {});
+  hs->maps.assign(hs->pf.slices.size(), {});
+  return trace_slices(hs, which);
+}
+
+// Streaming session: parse the bytes fed so far.  Slice indices are stable (a longer prefix only
+// adds slices or completes the last one); per-slice state grows with the parse.
+int stream_reparse(avr_hooks_session* hs) {
+  ParsedFile pf;
+  if (int r = parse_file(hs->c, hs->original.data(), hs->original.size(), &pf)) return r;
+  hs->pf = std::move(pf);
+  const size_t n = hs->pf.slices.size();
+  hs->coded.resize(n, 0);
+  hs->bins.resize(n);
+  hs->maps.resize(n);
+  hs->slices.resize(n);   // no slice object is live here (init_decoder closed it first)
+  hs->dirty = false;
   return AVR_OK;
 }
 
@@ -1747,12 +1775,45 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
   return AVR_OK;
 }
 
+int avr_hooks_compress_stream_begin(avr_ctx* c, int model, avr_hooks_session** out) {
+  if (!c || !out) return AVR_ERR_INVALID_ARGUMENT;
+  if (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL) return AVR_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  avr_hooks_session* hs = new (std::nothrow) avr_hooks_session;
+  if (!hs) return AVR_ERR_OUT_OF_MEMORY;
+  hs->c = c;
+  hs->streaming = true;
+  hs->model = model;
+  *out = hs;
+  return AVR_OK;
+}
+
+int avr_hooks_feed(avr_hooks_session* hs, const uint8_t* bytes, size_t n) {
+  if (!hs || (!bytes && n) || !hs->streaming) return AVR_ERR_INVALID_ARGUMENT;
+  try {
+    hs->original.insert(hs->original.end(), bytes, bytes + n);
+  } catch (const std::bad_alloc&) {
+    return AVR_ERR_OUT_OF_MEMORY;
+  }
+  if (n) hs->dirty = true;
+  return AVR_OK;
+}
+
 void* avr_hook_init_decoder(void* opaque, void* /*cabac_context*/, const uint8_t* buf, int size) {
   avr_hooks_session* hs = (avr_hooks_session*)opaque;
   if (!hs) return nullptr;
   close_live(hs);
+  if (hs->streaming && (hs->dirty || hs->next_slice >= hs->pf.slices.size())) {
+    // the slice the decoder starts is in the bytes its demuxer has read (read_packet feeds them
+    // before the packet is decoded): parse them, then trace this slice alone on the device
+    if (int r = stream_reparse(hs)) {
+      hs->fail_once("hooks: the bytes fed so far do not parse (" + std::to_string(r) + "): " + hs->c->err);
+      hs->next_slice++;
+      return nullptr;
+    }
+  }
   if (hs->next_slice >= hs->pf.slices.size()) {
-    hs->fail_once("hooks: more slices than the file holds");
+    hs->fail_once(hs->streaming ? "hooks: init_decoder for a slice not yet fed" : "hooks: more slices than the file holds");
     return nullptr;
   }
   const size_t i = hs->next_slice++;
@@ -1764,6 +1825,15 @@ void* avr_hook_init_decoder(void* opaque, void* /*cabac_context*/, const uint8_t
   if (!buf || size < 0 || (size_t)size != s.size) {
     hs->fail_once("hooks: slice " + std::to_string(i) + " size differs from the device's parse");
     return nullptr;
+  }
+  if (hs->streaming) {
+    // find_next_coded_block (recode.cpp:1139-1145, 1275-1297) on the slice's own bytes: a slice the
+    // device can re-code gets hooks; the container (avr_hooks_end) may still store it skip_coded
+    hs->coded[i] = memcmp(buf, s.payload(), s.size) == 0 && recodable_candidate(s) ? 1 : 0;
+    if (hs->coded[i] && trace_slices(hs, {(int)i}) != AVR_OK) {
+      hs->fail_once("hooks: device trace of slice " + std::to_string(i) + " failed: " + hs->c->err);
+      return nullptr;
+    }
   }
   if (!hs->coded[i]) return nullptr;  // not re-coded: decode natively (recode.cpp:1139-1145)
   if (hs->decompress) {
@@ -1918,6 +1988,21 @@ void avr_hook_end_coding_type(void* opaque, int coding_type) {
 int avr_hooks_end(avr_hooks_session* hs, uint8_t** out, size_t* out_len) {
   if (!hs || !out || !out_len) return AVR_ERR_INVALID_ARGUMENT;
   close_live(hs);
+  if (hs->streaming) {
+    // the whole file is in: its slice count, and the container (the model runs over every slice,
+    // recode.cpp:1102-1125)
+    if (hs->dirty || hs->pf.slices.empty()) {
+      if (int r = stream_reparse(hs)) return r;
+    }
+    if (hs->err.empty()) {
+      uint8_t* avrc = nullptr;
+      size_t avrc_len = 0;
+      if (int r = avr_compress_file(hs->c, hs->original.data(), hs->original.size(), hs->model, &avrc, &avrc_len))
+        return r;
+      hs->result.assign(avrc, avrc + avrc_len);
+      free(avrc);
+    }
+  }
   if (hs->next_slice != hs->pf.slices.size())
     hs->fail_once("hooks: " + std::to_string(hs->next_slice) + " of " + std::to_string(hs->pf.slices.size()) +
                   " slices were decoded");

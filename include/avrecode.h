@@ -280,6 +280,16 @@ int avr_hooks_compress_begin(avr_ctx* ctx, const uint8_t* file, size_t n, int mo
  * avr_hooks_destroy. */
 int avr_hooks_decompress_begin(avr_ctx* ctx, const uint8_t* avrc, size_t n, avr_hooks_session** out,
                                const uint8_t** stream, size_t* stream_len);
+/* Streaming compress: the caller's demuxer hands the file's bytes to the session as it reads them
+ * (avr_hooks_feed: the fork's read_packet, recode.cpp:1127-1131) instead of the whole file up front.
+ * Each init_decoder finds its slice in the bytes fed so far and traces that slice alone on the device
+ * (the hooks answer with the CABAC parse, whichever model the container uses); a slice not yet fed
+ * completely fails the session.  avr_hooks_end compresses the complete file with `model` -- the
+ * container needs every slice's model state, as the reference writes it after the last slice
+ * (recode.cpp:1102-1125) -- and returns it as avr_hooks_compress_begin's session would.  The
+ * callbacks and their checks are the same. */
+int avr_hooks_compress_stream_begin(avr_ctx* ctx, int model, avr_hooks_session** out);
+int avr_hooks_feed(avr_hooks_session* s, const uint8_t* bytes, size_t n);
 /* AVCodecHooks.cabac: opaque = the session.  init_decoder returns the per-slice opaque, or NULL
  * when the slice is not re-coded (the caller then decodes it natively, recode.cpp:1139-1145). */
 void* avr_hook_init_decoder(void* opaque, void* cabac_context, const uint8_t* buf, int size);

@@ -25,6 +25,19 @@ static int g_perturb, g_k;
 static long g_maps, g_mbs, g_subs, g_sub_bad;
 static int g_delayed;   /* a begin_coding_type(SIG_MAP) waiting for the next bin */
 static void *g_session;
+/* streaming compress (hooks_compress_stream): the bytes of `g_file` handed to the session so far;
+ * before each slice's init_decoder the driver feeds through the end of that slice's NAL unit, in two
+ * pieces, as a demuxer's read_packet would (recode.cpp:1127-1131) */
+static const uint8_t *g_file;
+static size_t g_fed;
+static int g_feed_err;
+static void feed_to(size_t end) {
+  if (!g_file || end <= g_fed) return;
+  size_t mid = g_fed + (end - g_fed) / 2;
+  if (avr_hooks_feed((avr_hooks_session *)g_session, g_file + g_fed, mid - g_fed) != AVR_OK) g_feed_err = 1;
+  if (avr_hooks_feed((avr_hooks_session *)g_session, g_file + mid, end - mid) != AVR_OK) g_feed_err = 1;
+  g_fed = end;
+}
 void hooks_set_perturb(int mode, int k) { g_perturb = mode; g_k = k; g_maps = g_mbs = g_subs = 0; g_delayed = 0; }
 
 static void flush_delayed(void) {
@@ -115,6 +128,7 @@ static long drive(const uint8_t *stream, size_t n) {
     size_t end = (bits + 7) / 8;
     size_t size = end > h.cabac_start ? end - h.cabac_start : 0;
     m_frame_spec(NULL, picture_id, h.mb_width, h.mb_height);
+    feed_to(nals[i].offset + nals[i].size);
     void *slice = avr_hook_init_decoder(g_session, NULL, rbsp + h.cabac_start, (int)size);
     if (slice) {
       avr_hooks_t hk = {slice, fwd_get, fwd_bypass, fwd_terminate, m_frame_spec, m_mb_xy,
@@ -143,6 +157,32 @@ int hooks_compress(const uint8_t *file, size_t n, int model, uint8_t **out, size
   r = avr_hooks_end(s, out, out_len);
   avr_hooks_destroy(s);
   avr_destroy(c);
+  return *walked < 0 ? -100 + (int)*walked : r;
+}
+
+/* the same through a streaming session: the file's bytes reach the session only as the slices
+ * that need them are decoded (the rest after the last slice). */
+int hooks_compress_stream(const uint8_t *file, size_t n, int model, uint8_t **out, size_t *out_len, long *walked) {
+  avr_ctx *c;
+  int r = avr_create(0, &c);
+  if (r) return r;
+  avr_hooks_session *s;
+  r = avr_hooks_compress_stream_begin(c, model, &s);
+  if (r) { avr_destroy(c); return r; }
+  g_session = s;
+  g_file = file;
+  g_fed = 0;
+  g_feed_err = 0;
+  /* MP4 read through a non-seekable read_packet (recode.cpp:84-90): the mov demuxer reads up to
+   * the moov box before the first packet -- for moov-last files, the whole file */
+  if (n >= 8 && memcmp(file + 4, "ftyp", 4) == 0) feed_to(n);
+  *walked = drive(file, n);
+  feed_to(n);
+  g_file = NULL;
+  r = avr_hooks_end(s, out, out_len);
+  avr_hooks_destroy(s);
+  avr_destroy(c);
+  if (g_feed_err) return -200;
   return *walked < 0 ? -100 + (int)*walked : r;
 }
 

@@ -41,7 +41,7 @@ def driver_path():
 def test_hooks_driver_builds_and_links():
     """CPU: the driver compiles against include/avrecode.h and links every avr_hook_* symbol."""
     L = ctypes.CDLL(str(driver_path()))
-    assert L.hooks_compress and L.hooks_decompress
+    assert L.hooks_compress and L.hooks_decompress and L.hooks_compress_stream
 
 
 def _driver():
@@ -49,6 +49,7 @@ def _driver():
     pp = ctypes.POINTER(ctypes.c_uint8)
     L.hooks_compress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(pp),
                                  ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_long)]
+    L.hooks_compress_stream.argtypes = L.hooks_compress.argtypes
     L.hooks_decompress.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(pp),
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_long)]
     return L, pp
@@ -96,6 +97,28 @@ def test_hooks_field_streams(name, mode, model):
     r, back, walked_d = _call("hooks_decompress", avrc, len(avrc))
     assert r == 0, r
     assert walked_d == walked and back == data
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["paff_ipp.264", "mbaff_ib.264", "realshort.mp4"])
+@pytest.mark.parametrize("mode,model", [("R", 0), ("P", 1)])
+def test_hooks_streaming_compress(name, mode, model):
+    """A streaming session: the driver hands the file to avr_hooks_feed only as far as the slice it
+    is about to decode (Annex-B: through that slice's NAL unit, in two pieces; MP4 with its moov
+    box last: the whole file first, as a non-seekable mov demuxer reads it), each init_decoder
+    traces its slice alone, and avr_hooks_end returns the same pinned container as the whole-file
+    session -- which the whole-file session then decompresses through the hooks."""
+    if name.endswith(".264"):
+        gold = {e["file"]: e for e in json.loads((ROOT / "tests/golden/fields.json").read_text())["files"]}[name][mode]
+    else:
+        gold = GOLD[(name, mode)]
+    data = (FIX / name).read_bytes()
+    r, avrc, walked = _call("hooks_compress_stream", data, len(data), model)
+    assert r == 0, r
+    assert hashlib.sha256(avrc).hexdigest() == gold["avrc_sha256"]
+    r, back, walked_d = _call("hooks_decompress", avrc, len(avrc))
+    assert r == 0, r
+    assert walked_d == walked > 0 and back == data
 
 
 @pytest.mark.gpu
