@@ -198,7 +198,11 @@ def _buf(data) -> tuple[ctypes.c_void_p, int, object]:
 def _take(p: ctypes.c_void_p, n: int) -> bytes:
     L = lib()
     try:
-        return ctypes.string_at(p.value, n) if n else b""
+        if not n:
+            return b""
+        # ctypes.string_at's length is a C int: a buffer of 2 GiB or more (a 10-minute 4K stream,
+        # its container) is copied through an array view instead
+        return ctypes.string_at(p.value, n) if n < (1 << 31) else bytes((ctypes.c_char * n).from_address(p.value))
     finally:
         L.avr_free(p)
 

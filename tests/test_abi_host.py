@@ -256,3 +256,21 @@ def test_deal_files_lpt():
         assert max(loads) <= sizes.sum() / world + sizes.max()
     assert shard.deal_files([], 4) == [[], [], [], []]
     assert shard.deal_files([5, 1, 1, 1, 1, 1], 2) == [[0], [1, 2, 3, 4, 5]]
+
+
+def test_take_copies_buffers_past_2gib():
+    """Library outputs of 2 GiB and more (a full-size configs[3] stream and its container) come back
+    whole: ctypes.string_at's int length would wrap them (a 4.47 GB stream came back as 172 MB)."""
+    import ctypes
+
+    import avrecode_amd as avr
+    libc = ctypes.CDLL(None)
+    libc.malloc.restype = ctypes.c_void_p
+    libc.malloc.argtypes = [ctypes.c_size_t]
+    n = (1 << 31) + 4099
+    p = libc.malloc(n)
+    assert p
+    ctypes.memset(p, 0x5A, n)
+    ctypes.memset(p + n - 7, 0x33, 7)
+    b = avr._take(ctypes.c_void_p(p), n)   # frees p
+    assert len(b) == n and b[:4] == b"ZZZZ" and b[-8:] == b"Z" + b"\x33" * 7
