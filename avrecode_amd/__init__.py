@@ -20,17 +20,21 @@ from dataclasses import dataclass
 import numpy as np
 
 __all__ = [
-    "AvrError", "Context", "MODEL_REFERENCE", "MODEL_PARALLEL", "SLICE_DESC", "SLICE_RESULT",
-    "SynthParams", "lib", "parse_stream", "assemble_container", "neighbor_tables",
-    "plan_decompress", "splice_container", "source_sha", "library_path", "EXPORTED_SYMBOLS",
+    "AvrError", "Context", "MODEL_REFERENCE", "MODEL_PARALLEL", "MODEL_PARALLEL32", "MODEL_NAMES", "SLICE_DESC",
+    "SLICE_RESULT", "SynthParams", "lib", "parse_stream", "assemble_container", "neighbor_tables",
+    "plan_decompress", "splice_container", "container_model", "source_sha", "library_path", "EXPORTED_SYMBOLS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # AVR_LIBRARY selects an instrumented build (e.g. prof/libavrecode.so, `make -C avrecode_amd prof`)
 library_path = os.environ.get("AVR_LIBRARY") or os.path.join(_HERE, "libavrecode.so")
 
+# avr_model (include/avrecode.h): the reference model; the parallel model (fresh model per slice)
+# on the reference's arithmetic_code<uint64_t, uint8_t>; the parallel model on the optional P32 coder
 MODEL_REFERENCE = 0
 MODEL_PARALLEL = 1
+MODEL_PARALLEL32 = 2
+MODEL_NAMES = {MODEL_REFERENCE: "R", MODEL_PARALLEL: "P", MODEL_PARALLEL32: "P32"}
 
 AVR_OK = 0
 _STATUS = {
@@ -42,7 +46,8 @@ _STATUS = {
 EXPORTED_SYMBOLS = (
     "avr_create", "avr_destroy", "avr_last_error", "avr_free", "avr_compress_file", "avr_decompress_file",
     "avr_roundtrip_file", "avr_compress_slices", "avr_decompress_slices", "avr_pack_outputs",
-    "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream", "avr_assemble_container", "avr_synthesize_stream",
+    "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream",
+    "avr_assemble_container", "avr_assemble_container_parsed", "avr_container_model", "avr_synthesize_stream",
     "avr_container_describe", "avr_compress_files", "avr_decompress_files",
     "avr_hooks_compress_begin", "avr_hooks_compress_stream_begin", "avr_hooks_feed",
     "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
@@ -170,14 +175,16 @@ def lib() -> ctypes.CDLL:
     L.avr_verify_slices.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
     L.avr_pack_outputs.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
     L.avr_parse_stream.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
-    L.avr_assemble_container.argtypes = [vp, sz, i32, vp, vp, vp, vp, pp, psz]
+    L.avr_assemble_container.argtypes = [vp, sz, i32, i32, vp, vp, sz, vp, vp, pp, psz]
+    L.avr_assemble_container_parsed.argtypes = [vp, sz, i32, vp, i32, vp, sz, vp, vp, sz, vp, vp, pp, psz]
+    L.avr_container_model.argtypes = [vp, sz, pi]
     L.avr_synthesize_stream.argtypes = [vp, ctypes.POINTER(_SynthParams), i32, pp, psz]
     L.avr_container_describe.argtypes = [vp, sz, pp, pp, psz]
     L.avr_compress_files.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
     L.avr_decompress_files.argtypes = [vp, i32, vp, vp, vp, vp, vp]
     L.avr_neighbor_tables.argtypes = [vp, vp]
     L.avr_plan_decompress.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
-    L.avr_splice_container.argtypes = [vp, sz, i32, vp, vp, vp, vp, pp, psz]
+    L.avr_splice_container.argtypes = [vp, sz, i32, vp, vp, sz, vp, vp, pp, psz]
     L.avr_last_phase_times.argtypes = [vp, vp]
     for name in EXPORTED_SYMBOLS:   # fails here, not at first use, when the build is stale
         getattr(L, name)
@@ -186,13 +193,18 @@ def lib() -> ctypes.CDLL:
 
 
 def _buf(data) -> tuple[ctypes.c_void_p, int, object]:
-    """(pointer, length, keepalive) for bytes / bytearray / numpy uint8."""
+    """(pointer, length, keepalive) for bytes / bytearray / memoryview / numpy uint8, without a copy
+    (the library only reads its inputs; a 4.47 GB stream must not be duplicated per call)."""
     if isinstance(data, np.ndarray):
-        a = np.ascontiguousarray(data, dtype=np.uint8)
-        return ctypes.c_void_p(a.ctypes.data), a.nbytes, a
-    b = bytes(data)
-    cb = ctypes.create_string_buffer(b, len(b)) if b else ctypes.create_string_buffer(1)
-    return ctypes.cast(cb, ctypes.c_void_p), len(b), cb
+        a = np.ascontiguousarray(data).reshape(-1).view(np.uint8)
+    elif isinstance(data, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(data, dtype=np.uint8)
+    else:
+        a = np.frombuffer(bytes(data), dtype=np.uint8)
+    if a.nbytes == 0:   # a valid, non-null pointer for empty inputs
+        cb = ctypes.create_string_buffer(1)
+        return ctypes.cast(cb, ctypes.c_void_p), 0, cb
+    return ctypes.c_void_p(a.ctypes.data), a.nbytes, a
 
 
 def _take(p: ctypes.c_void_p, n: int) -> bytes:
@@ -203,6 +215,18 @@ def _take(p: ctypes.c_void_p, n: int) -> bytes:
         # ctypes.string_at's length is a C int: a buffer of 2 GiB or more (a 10-minute 4K stream,
         # its container) is copied through an array view instead
         return ctypes.string_at(p.value, n) if n < (1 << 31) else bytes((ctypes.c_char * n).from_address(p.value))
+    finally:
+        L.avr_free(p)
+
+
+def _take_array(p: ctypes.c_void_p, n: int) -> np.ndarray:
+    """A library buffer as a numpy uint8 array: one copy, then the buffer is freed."""
+    L = lib()
+    try:
+        a = np.empty(n, dtype=np.uint8)
+        if n:
+            ctypes.memmove(a.ctypes.data, p.value, n)
+        return a
     finally:
         L.avr_free(p)
 
@@ -233,8 +257,8 @@ def parse_stream(data) -> ParsedStream:
     del keep
     if r != AVR_OK:
         raise AvrError(r, "avr_parse_stream failed")
-    d = np.frombuffer(_take(descs, ns.value * SLICE_DESC.itemsize), dtype=SLICE_DESC).copy()
-    a = np.frombuffer(_take(arena, alen.value), dtype=np.uint8).copy()
+    d = _take_array(descs, ns.value * SLICE_DESC.itemsize).view(SLICE_DESC)
+    a = _take_array(arena, alen.value)
     return ParsedStream(d, a, int(wlen.value), int(mw.value), int(mh.value))
 
 
@@ -251,39 +275,60 @@ def plan_decompress(avrc) -> ParsedStream:
     del keep
     if r != AVR_OK:
         raise AvrError(r, "avr_plan_decompress failed")
-    d = np.frombuffer(_take(descs, ns.value * SLICE_DESC.itemsize), dtype=SLICE_DESC).copy()
-    a = np.frombuffer(_take(arena, alen.value), dtype=np.uint8).copy()
+    d = _take_array(descs, ns.value * SLICE_DESC.itemsize).view(SLICE_DESC)
+    a = _take_array(arena, alen.value)
     return ParsedStream(d, a, int(wlen.value), int(mw.value), int(mh.value))
 
 
-def splice_container(avrc, status: np.ndarray, regen: bytes, offsets: np.ndarray, lens: np.ndarray) -> bytes:
+def container_model(avrc) -> int:
+    """The model mode a Recoded container was written with (avr_container_model): MODEL_*.  Host only."""
+    p, n, keep = _buf(avrc)
+    m = ctypes.c_int()
+    r = lib().avr_container_model(p, n, ctypes.byref(m))
+    if r != AVR_OK:
+        raise AvrError(r, "avr_container_model failed")
+    return int(m.value)
+
+
+def splice_container(avrc, status: np.ndarray, regen, offsets: np.ndarray, lens: np.ndarray) -> bytes:
     """The original file from a PARALLEL-model container and its slices' regenerated bytes
-    (avr_splice_container; last-byte patch applied here).  Host only."""
+    (avr_splice_container; last-byte patch applied here).  regen: bytes or a uint8 array.  Host only."""
     L = lib()
     p, n, keep = _buf(avrc)
     st = np.ascontiguousarray(status, dtype=np.int32)
     of = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lens, dtype=np.uint32)
-    rp, _, keep2 = _buf(regen)
+    rp, rn, keep2 = _buf(regen)
     out, olen = ctypes.c_void_p(), ctypes.c_size_t()
-    r = L.avr_splice_container(p, n, len(st), st.ctypes.data, rp, of.ctypes.data, ln.ctypes.data,
+    r = L.avr_splice_container(p, n, len(st), st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data,
                                ctypes.byref(out), ctypes.byref(olen))
     if r != AVR_OK:
         raise AvrError(r, "avr_splice_container failed")
     return _take(out, olen.value)
 
 
-def assemble_container(data, status: np.ndarray, recoded: bytes, offsets: np.ndarray, lens: np.ndarray) -> bytes:
-    """PARALLEL-model Recoded container from per-slice outputs (avr_assemble_container).  Host only."""
+def assemble_container(data, status: np.ndarray, recoded, offsets: np.ndarray, lens: np.ndarray,
+                       model: int = MODEL_PARALLEL, ps: "ParsedStream | None" = None) -> bytes:
+    """PARALLEL-model Recoded container from per-slice outputs (avr_assemble_container; with ps =
+    parse_stream(data) already in hand, avr_assemble_container_parsed: no second parse).  recoded:
+    bytes or a uint8 array.  model: the coder the outputs were made with.  Host only."""
     L = lib()
     p, n, keep = _buf(data)
     st = np.ascontiguousarray(status, dtype=np.int32)
     of = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lens, dtype=np.uint32)
-    rp, _, keep2 = _buf(recoded)
+    rp, rn, keep2 = _buf(recoded)
     out, olen = ctypes.c_void_p(), ctypes.c_size_t()
-    r = L.avr_assemble_container(p, n, len(st), st.ctypes.data, rp, of.ctypes.data, ln.ctypes.data,
-                                 ctypes.byref(out), ctypes.byref(olen))
+    if ps is not None:
+        dd = np.ascontiguousarray(ps.descs)
+        if len(dd) != len(st) or len(of) != len(st) or len(ln) != len(st):
+            raise ValueError("assemble_container: status / offsets / lens need one entry per parsed slice")
+        r = L.avr_assemble_container_parsed(p, n, model, dd.ctypes.data, len(dd), ps.arena.ctypes.data, ps.arena.nbytes,
+                                            st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data, ctypes.byref(out),
+                                            ctypes.byref(olen))
+    else:
+        r = L.avr_assemble_container(p, n, model, len(st), st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data,
+                                     ctypes.byref(out), ctypes.byref(olen))
     if r != AVR_OK:
         raise AvrError(r, "avr_assemble_container failed")
     return _take(out, olen.value)

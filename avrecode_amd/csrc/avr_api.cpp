@@ -10,6 +10,7 @@
 // AVR_ERR_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <chrono>
 #include <cmath>
@@ -86,6 +87,12 @@ struct avr_ctx {
 namespace {
 
 constexpr int kMaxSlicesPerLaunch = 4096;
+
+// Model modes (include/avrecode.h): the reference model, and the parallel model on the reference's
+// arithmetic_code<uint64_t, uint8_t> (PARALLEL) or on the optional 32-bit P32 coder (PARALLEL32).
+bool valid_model(int m) { return m == AVR_MODEL_REFERENCE || m == AVR_MODEL_PARALLEL || m == AVR_MODEL_PARALLEL32; }
+bool parallel_model(int m) { return m == AVR_MODEL_PARALLEL || m == AVR_MODEL_PARALLEL32; }
+uint32_t coder_flag(int m) { return m == AVR_MODEL_PARALLEL32 ? avr::kFlagP32 : 0u; }
 constexpr size_t kLdsBudget = 160 * 1024;   // LDS per workgroup (one slice) on gfx950
 constexpr uint64_t kMaxSynthBytes = (uint64_t)1 << 35;   // avr_synthesize_stream's output cap (32 GiB)
 
@@ -476,7 +483,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
       HIP_TRY(c, avr::launch_slices(1, false, c->tables.as<avr::EngineTables>(), dd + s0, m, plan.max_w,
                                     c->out.as<uint8_t>(), c->regen.as<uint8_t>(), rd + s0, c->est.as<uint16_t>(),
                                     nullptr, nullptr, c->order_or_null(), c->stream, avr::SeqFiles(),
-                                    plan.fields() ? avr::kFlagFields : 0u));
+                                    (plan.fields() ? avr::kFlagFields : 0u) | (flags & avr::kFlagP32)));
     }
     HIP_TRY(c, avr::launch_verify(c->descs.as<avr_slice_desc>(), c->res.as<avr_slice_result>(), rd, n,
                                   c->in.as<uint8_t>(), c->regen.as<uint8_t>(), c->verdict.as<int32_t>(), c->stream));
@@ -526,34 +533,101 @@ bool recodable_candidate(const avr::SliceInfo& s) {
   return s.h.supported && s.size >= (size_t)avr::kSurrogateMarkerBytes && avr::shared_bytes(cols) <= kLdsBudget;
 }
 
+// A slice as the container writer sees it: its payload (init_decoder's buf, size) and whether the
+// device may re-code it (recodable_candidate).
+struct SliceView {
+  const uint8_t* payload;
+  size_t size;
+  bool candidate;
+};
+std::vector<SliceView> views_of(const ParsedFile& pf) {
+  std::vector<SliceView> v(pf.slices.size());
+  for (size_t i = 0; i < v.size(); i++) v[i] = {pf.slices[i].payload(), pf.slices[i].size, recodable_candidate(pf.slices[i])};
+  return v;
+}
+
+// The positions p of every 00 00 0y trigram (y <= 3) of a file, by y, ascending.  In an escaped
+// H.264 stream these occur only at start codes, emulation-prevention bytes (00 00 03) and container
+// bytes (MP4 lengths and boxes), so the index is small.
+struct TrigramIndex {
+  bool built = false;
+  std::vector<uint64_t> pos[4];
+  void build(const uint8_t* f, size_t n) {
+    built = true;
+    const uint8_t* e = f + n;
+    for (const uint8_t* p = f; p + 2 < e;) {
+      p = (const uint8_t*)memchr(p, 0, (size_t)(e - 2 - p));
+      if (!p) break;
+      if (p[1] == 0 && p[2] <= 3) pos[p[2]].push_back((uint64_t)(p - f));
+      p++;
+    }
+  }
+};
+
+// memmem(in + from, n - from, P, m) (the reference's search, recode.cpp:1285) without its cost on a
+// miss.  A payload P holding a 00 00 0y trigram (y <= 3) at offset j -- an unescaped payload whose
+// NAL had emulation-prevention bytes -- can only occur at q with a trigram of the file at q + j, so
+// the index's trigrams with the same y, in ascending order, are the only candidates and the first
+// that matches is memmem's answer.  Such payloads are exactly the ones that usually occur nowhere,
+// where memmem would scan to the end of the file for each of them (O(misses x file): minutes for a
+// 10-minute 4K stream).  A payload without one is found in its own NAL (its bytes are verbatim
+// there), so memmem stops at most one NAL past `from`.
+const uint8_t* find_payload(const uint8_t* in, size_t n, size_t from, const uint8_t* P, size_t m, TrigramIndex* ix) {
+  size_t j = 0;
+  bool anchor = false;
+  for (const uint8_t* q = P; m >= 3 && q + 2 < P + m;) {
+    q = (const uint8_t*)memchr(q, 0, (size_t)(P + m - 2 - q));
+    if (!q) break;
+    if (q[1] == 0 && q[2] <= 3) {
+      j = (size_t)(q - P);
+      anchor = true;
+      break;
+    }
+    q++;
+  }
+  if (!anchor) return (const uint8_t*)memmem(in + from, n - from, P, m);
+  if (!ix->built) ix->build(in, n);
+  const std::vector<uint64_t>& v = ix->pos[P[j + 2]];
+  for (auto it = std::lower_bound(v.begin(), v.end(), (uint64_t)(from + j)); it != v.end(); ++it) {
+    const size_t q = (size_t)*it - j;
+    if (q + m > n) break;
+    if (memcmp(in + q, P, m) == 0) return in + q;
+  }
+  return nullptr;
+}
+
 // find_next_coded_block_and_emit_literal (recode.cpp:1275-1297): slice i becomes a cabac block when
 // it is recodable (ok[i]), at least a surrogate marker long, and its payload occurs verbatim after
 // the previous coded block.  Returns the payload's position in the file per slice (null = skip).
-std::vector<const uint8_t*> segment(const uint8_t* in, size_t n, const ParsedFile& pf, const std::vector<char>& ok) {
-  std::vector<const uint8_t*> found(pf.slices.size(), nullptr);
+std::vector<const uint8_t*> segment(const uint8_t* in, size_t n, const std::vector<SliceView>& sv,
+                                    const std::vector<char>& ok) {
+  std::vector<const uint8_t*> found(sv.size(), nullptr);
+  TrigramIndex ix;
   size_t prev_end = 0;
-  for (size_t i = 0; i < pf.slices.size(); i++) {
-    const avr::SliceInfo& s = pf.slices[i];
-    if (!ok[i] || s.size < (size_t)avr::kSurrogateMarkerBytes) continue;
-    const uint8_t* f = (const uint8_t*)memmem(in + prev_end, n - prev_end, s.payload(), s.size);
+  for (size_t i = 0; i < sv.size(); i++) {
+    if (!ok[i] || sv[i].size < (size_t)avr::kSurrogateMarkerBytes) continue;
+    const uint8_t* f = find_payload(in, n, prev_end, sv[i].payload, sv[i].size, &ix);
     if (f) {
       found[i] = f;
-      prev_end = (size_t)(f - in) + s.size;
+      prev_end = (size_t)(f - in) + sv[i].size;
     }
   }
   return found;
 }
+std::vector<const uint8_t*> segment(const uint8_t* in, size_t n, const ParsedFile& pf, const std::vector<char>& ok) {
+  return segment(in, n, views_of(pf), ok);
+}
 
 // compressor::run's block stream (recode.cpp:1115-1125, 1275-1297) as a Recoded protobuf.
-int emit_container(const uint8_t* in, size_t n, const ParsedFile& pf, const std::vector<const uint8_t*>& found,
-                   const std::vector<std::pair<const uint8_t*, size_t>>& recoded, bool parallel, uint8_t** out,
+int emit_container(const uint8_t* in, size_t n, const std::vector<SliceView>& sv, const std::vector<const uint8_t*>& found,
+                   const std::vector<std::pair<const uint8_t*, size_t>>& recoded, int model, uint8_t** out,
                    size_t* out_len) {
   std::vector<uint8_t> o;
   o.reserve(n + n / 8 + 1024);
-  if (parallel) avr::pb_put_metadata_version(&o, avr::kParallelModelTag);
+  if (const char* tag = avr::version_of_model(model)) avr::pb_put_metadata_version(&o, tag);
   size_t prev_end = 0;
-  for (size_t i = 0; i < pf.slices.size(); i++) {
-    const avr::SliceInfo& s = pf.slices[i];
+  for (size_t i = 0; i < sv.size(); i++) {
+    const SliceView& s = sv[i];
     avr::PbBlock b;
     if (found[i]) {
       avr::PbBlock lit;
@@ -566,7 +640,7 @@ int emit_container(const uint8_t* in, size_t n, const ParsedFile& pf, const std:
       b.size = (int64_t)s.size;
       b.has_parity = true;
       b.length_parity = s.size & 1;
-      if (s.size > 1) b.has_last_byte = true, b.last_byte.assign(1, (char)s.payload()[s.size - 1]);
+      if (s.size > 1) b.has_last_byte = true, b.last_byte.assign(1, (char)s.payload[s.size - 1]);
       b.has_cabac = true;
       b.cabac = recoded[i].first;
       b.cabac_len = recoded[i].second;
@@ -666,7 +740,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   std::vector<uint8_t> outb;
   pc.mark_demux();
   if (int r = run_plan(c, 0, false, plan, &res, &outb, verify,
-                       bills && model == AVR_MODEL_PARALLEL ? avr::kFlagBill : 0))
+                       (bills ? avr::kFlagBill : 0u) | coder_flag(model)))
     return r;
   // 2) segmentation (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297)
   std::vector<std::vector<char>> ok(nf);
@@ -755,7 +829,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
     if (st[f] == AVR_OK) {
       std::vector<std::pair<const uint8_t*, size_t>> blobs(pf[f].slices.size(), {nullptr, 0});
       for (size_t i = 0; i < pf[f].slices.size(); i++) blobs[i] = {recoded[f][i].data(), recoded[f][i].size()};
-      st[f] = emit_container(in[f], in_len[f], pf[f], found[f], blobs, model == AVR_MODEL_PARALLEL, &out[f],
+      st[f] = emit_container(in[f], in_len[f], views_of(pf[f]), found[f], blobs, model, &out[f],
                              &out_len[f]);
     }
     if (status) status[f] = st[f];
@@ -772,17 +846,20 @@ struct DecJob {
   std::vector<avr::PbBlock> blocks;
   std::vector<uint8_t> stream;       // read_packet's stream: literals + surrogate blocks
   bool parallel = false;
+  int model = AVR_MODEL_REFERENCE;   // from Recoded.Metadata.version
   std::vector<int> desc_of_block;    // plan index per coded block (-1: none)
 };
 
 int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* plan) {
   std::string version;
   if (!avr::pb_parse(in, n, &j->blocks, &version)) return fail(c, AVR_ERR_FORMAT, "not a Recoded protobuf");
-  j->parallel = version == avr::kParallelModelTag;
-  // another avrecode-amd container format (the round-2 "avrecode-amd:P", 64-bit coder) would be
-  // read as a reference-model container and fail late: refuse it here
-  if (!j->parallel && version.rfind("avrecode-amd:", 0) == 0)
-    return fail(c, AVR_ERR_FORMAT, "unsupported container version " + version + " (expected " + avr::kParallelModelTag + ")");
+  j->model = avr::model_of_version(version);
+  // another avrecode-amd container format (the round-2 "avrecode-amd:P", ...) would be read as a
+  // reference-model container and fail late: refuse it here
+  if (j->model < 0)
+    return fail(c, AVR_ERR_FORMAT, "unsupported container version " + version + " (expected " + avr::kParallelModelTag +
+                                       " or " + avr::kParallel32ModelTag + ")");
+  j->parallel = parallel_model(j->model);
   // read_packet (recode.cpp:1359-1409): literals and surrogate blocks form the stream
   uint64_t seq = 1;
   for (auto& b : j->blocks) {
@@ -897,14 +974,18 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
   const uint32_t flags = bills ? avr::kFlagBill : 0;
   std::vector<int32_t> st(nf, AVR_OK);
   std::vector<DecJob> jobs(nf);
-  Plan pp, rp;   // parallel-model slices; reference-model files (one workgroup each)
+  // plans[AVR_MODEL_*]: reference-model files (one workgroup each); parallel-model slices on the
+  // u64 coder; on the P32 coder
+  Plan plans[3];
+  Plan& rp = plans[AVR_MODEL_REFERENCE];
   for (int f = 0; f < nf; f++) {
     out[f] = nullptr;
     out_len[f] = 0;
     std::string version;
     std::vector<avr::PbBlock> probe;
-    const bool parallel = avr::pb_parse(in[f], in_len[f], &probe, &version) && version == avr::kParallelModelTag;
-    Plan* plan = parallel ? &pp : &rp;
+    const int m = avr::pb_parse(in[f], in_len[f], &probe, &version) ? std::max(0, avr::model_of_version(version)) : 0;
+    const bool parallel = parallel_model(m);
+    Plan* plan = &plans[m];
     const size_t n0 = plan->descs.size();
     if (!parallel) rp.file_first.push_back((int)n0);
     st[f] = decompress_setup(c, in[f], in_len[f], &jobs[f], plan);
@@ -913,21 +994,22 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
       if (!parallel) rp.file_first.pop_back();
     }
   }
-  std::vector<avr_slice_result> pres, rres;
-  std::vector<uint8_t> pout, rout;
+  std::vector<avr_slice_result> res_of[3];
+  std::vector<uint8_t> out_of[3];
   pc.mark_demux();
-  if (!pp.descs.empty())
-    if (int r = run_plan(c, 1, false, pp, &pres, &pout, false, flags)) return r;
+  for (int m = AVR_MODEL_PARALLEL; m <= AVR_MODEL_PARALLEL32; m++)
+    if (!plans[m].descs.empty())
+      if (int r = run_plan(c, 1, false, plans[m], &res_of[m], &out_of[m], false, flags | coder_flag(m))) return r;
   if (!rp.file_first.empty()) {
     rp.file_first.push_back((int)rp.descs.size());
-    if (int r = run_plan(c, 1, true, rp, &rres, &rout, false, flags)) return r;
+    if (int r = run_plan(c, 1, true, rp, &res_of[0], &out_of[0], false, flags)) return r;
   }
   int first_err = AVR_OK;
   for (int f = 0; f < nf; f++) {
     DecJob& j = jobs[f];
-    const Plan& plan = j.parallel ? pp : rp;
-    const std::vector<avr_slice_result>& res = j.parallel ? pres : rres;
-    const std::vector<uint8_t>& outb = j.parallel ? pout : rout;
+    const Plan& plan = plans[j.model];
+    const std::vector<avr_slice_result>& res = res_of[j.model];
+    const std::vector<uint8_t>& outb = out_of[j.model];
     std::vector<uint8_t> o;
     if (st[f] == AVR_OK)
       st[f] = splice_job(c, j, [&](int k, const uint8_t** p, size_t* len) {
@@ -1028,7 +1110,8 @@ int avr_plan_decompress(const uint8_t* avrc, size_t n, avr_slice_desc** descs, i
 }
 
 int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int32_t* status, const uint8_t* regen,
-                         const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len) {
+                         size_t regen_len, const uint64_t* offsets, const uint32_t* lens, uint8_t** out,
+                         size_t* out_len) {
   if (!avrc || n_slices < 0 || (n_slices && (!status || !regen || !offsets || !lens)) || !out || !out_len)
     return AVR_ERR_INVALID_ARGUMENT;
   return guarded(nullptr, [&]() -> int {
@@ -1037,6 +1120,11 @@ int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int3
     if (int r = decompress_setup(nullptr, avrc, n, &j, &plan)) return r;
     if (!j.parallel) return AVR_ERR_UNSUPPORTED;
     if ((int)plan.descs.size() != n_slices) return AVR_ERR_INVALID_ARGUMENT;
+    // every slice's regenerated bytes inside regen and within its own output capacity
+    for (int k = 0; k < n_slices; k++)
+      if (status[k] == 0 && (offsets[k] > regen_len || lens[k] > regen_len - offsets[k] ||
+                             lens[k] > plan.descs[k].out_capacity))
+        return AVR_ERR_INVALID_ARGUMENT;
     std::vector<uint8_t> o;
     if (int r = splice_job(nullptr, j, [&](int k, const uint8_t** p, size_t* len) {
           *p = regen + offsets[k];
@@ -1070,8 +1158,7 @@ int avr_neighbor_tables(avr_ctx* c, uint8_t out[96]) {
 }
 
 int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** out, size_t* out_len) {
-  if (!c || !in || !out || !out_len || (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL))
-    return AVR_ERR_INVALID_ARGUMENT;
+  if (!c || !in || !out || !out_len || !valid_model(model)) return AVR_ERR_INVALID_ARGUMENT;
   int32_t st = 0;
   const int r = guarded(c, [&] { return compress_files(c, 1, &in, &n, model, out, out_len, &st); });
   return r ? r : st;
@@ -1079,31 +1166,74 @@ int avr_compress_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_
 
 int avr_compress_files(avr_ctx* c, int n_files, const uint8_t* const* in, const size_t* in_len, int model,
                        uint8_t** out, size_t* out_len, int32_t* status) {
-  if (!c || n_files < 0 || (n_files && (!in || !in_len || !out || !out_len)) ||
-      (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL))
+  if (!c || n_files < 0 || (n_files && (!in || !in_len || !out || !out_len)) || !valid_model(model))
     return AVR_ERR_INVALID_ARGUMENT;
   for (int f = 0; f < n_files; f++)
     if (!in[f]) return AVR_ERR_INVALID_ARGUMENT;
   return guarded(c, [&] { return compress_files(c, n_files, in, in_len, model, out, out_len, status); });
 }
 
-int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
-                           const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len) {
-  if (!file || !out || !out_len || n_slices < 0 || (n_slices && (!status || !offsets || !lens)))
-    return AVR_ERR_INVALID_ARGUMENT;
-  ParsedFile pf;
-  if (int r = parse_file(nullptr, file, n, &pf)) return r;
-  if ((size_t)n_slices != pf.slices.size()) return AVR_ERR_INVALID_ARGUMENT;
-  std::vector<char> ok(pf.slices.size(), 0);
-  std::vector<std::pair<const uint8_t*, size_t>> blobs(pf.slices.size(), {nullptr, 0});
-  for (size_t i = 0; i < pf.slices.size(); i++) {
-    ok[i] = recodable_candidate(pf.slices[i]) && status[i] == 0;
+namespace {
+// Rank 0's container from gathered per-slice outputs (both avr_assemble_container entry points).
+int assemble(const uint8_t* file, size_t n, int model, const std::vector<SliceView>& sv, const int32_t* status,
+             const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets, const uint32_t* lens, uint8_t** out,
+             size_t* out_len) {
+  std::vector<char> ok(sv.size(), 0);
+  std::vector<std::pair<const uint8_t*, size_t>> blobs(sv.size(), {nullptr, 0});
+  for (size_t i = 0; i < sv.size(); i++) {
+    ok[i] = sv[i].candidate && status[i] == 0;
     if (ok[i]) {
-      if (!recoded) return AVR_ERR_INVALID_ARGUMENT;
+      if (!recoded || offsets[i] > recoded_len || lens[i] > recoded_len - offsets[i]) return AVR_ERR_INVALID_ARGUMENT;
       blobs[i] = {recoded + offsets[i], lens[i]};
     }
   }
-  return emit_container(file, n, pf, segment(file, n, pf, ok), blobs, true, out, out_len);
+  return emit_container(file, n, sv, segment(file, n, sv, ok), blobs, model, out, out_len);
+}
+}  // namespace
+
+int avr_assemble_container(const uint8_t* file, size_t n, int model, int n_slices, const int32_t* status,
+                           const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets, const uint32_t* lens,
+                           uint8_t** out, size_t* out_len) {
+  if (!file || !out || !out_len || n_slices < 0 || (n_slices && (!status || !offsets || !lens)) ||
+      !parallel_model(model))
+    return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(nullptr, [&]() -> int {
+    ParsedFile pf;
+    if (int r = parse_file(nullptr, file, n, &pf)) return r;
+    if ((size_t)n_slices != pf.slices.size()) return AVR_ERR_INVALID_ARGUMENT;
+    return assemble(file, n, model, views_of(pf), status, recoded, recoded_len, offsets, lens, out, out_len);
+  });
+}
+
+int avr_assemble_container_parsed(const uint8_t* file, size_t n, int model, const avr_slice_desc* descs, int n_slices,
+                                  const uint8_t* arena, size_t arena_len, const int32_t* status,
+                                  const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets,
+                                  const uint32_t* lens, uint8_t** out, size_t* out_len) {
+  if (!file || !out || !out_len || n_slices < 0 || (n_slices && (!descs || !arena || !status || !offsets || !lens)) ||
+      !parallel_model(model))
+    return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(nullptr, [&]() -> int {
+    std::vector<SliceView> sv((size_t)n_slices);
+    for (int i = 0; i < n_slices; i++) {
+      const avr_slice_desc& d = descs[i];
+      if (d.payload_offset > arena_len || d.payload_size > arena_len - d.payload_offset) return AVR_ERR_INVALID_ARGUMENT;
+      sv[i] = {arena + d.payload_offset, d.payload_size, d.coded != 0};
+    }
+    return assemble(file, n, model, sv, status, recoded, recoded_len, offsets, lens, out, out_len);
+  });
+}
+
+int avr_container_model(const uint8_t* avrc, size_t n, int* model) {
+  if (!avrc || !model) return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(nullptr, [&]() -> int {
+    std::vector<avr::PbBlock> blocks;
+    std::string version;
+    if (!avr::pb_parse(avrc, n, &blocks, &version)) return AVR_ERR_FORMAT;
+    const int m = avr::model_of_version(version);
+    if (m < 0) return AVR_ERR_FORMAT;
+    *model = m;
+    return AVR_OK;
+  });
 }
 
 int avr_decompress_file(avr_ctx* c, const uint8_t* in, size_t n, uint8_t** out, size_t* out_len) {
@@ -1130,7 +1260,7 @@ int avr_roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8
 static int roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, uint8_t** compressed,
                           size_t* compressed_len, avr_file_stats* stats) {
   if (!c || !in) return AVR_ERR_INVALID_ARGUMENT;
-  if (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL) return AVR_ERR_INVALID_ARGUMENT;
+  if (!valid_model(model)) return AVR_ERR_INVALID_ARGUMENT;
   uint8_t *comp = nullptr, *dec = nullptr;
   size_t cn = 0, dn = 0;
   std::vector<Bill> cbill, dbill;
@@ -1145,7 +1275,7 @@ static int roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, ui
   bool same = false;
   // the parallel model's per-slice device check is left to the whole-file compare below; a file
   // that does not come back is compressed again with it (every slice that fails it stored as is)
-  for (int attempt = model == AVR_MODEL_PARALLEL ? 0 : 1; attempt < 2; attempt++) {
+  for (int attempt = parallel_model(model) ? 0 : 1; attempt < 2; attempt++) {
     free(comp);
     comp = nullptr;
     cn = 0;
@@ -1212,8 +1342,7 @@ static int roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, ui
 
 static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int max_w, int max_h,
                  const uint8_t* d_in, uint8_t* d_out, avr_slice_result* d_res, int model, void* stream) {
-  if (!c || n < 0 || (n && (!d_desc || !d_in || !d_out || !d_res)) || max_w <= 0 || max_h <= 0 ||
-      (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL))
+  if (!c || n < 0 || (n && (!d_desc || !d_in || !d_out || !d_res)) || max_w <= 0 || max_h <= 0 || !valid_model(model))
     return AVR_ERR_INVALID_ARGUMENT;
   if (avr::shared_bytes(max_w) > 160 * 1024) return fail(c, AVR_ERR_UNSUPPORTED, "picture too wide for the LDS ring");
   HIP_TRY(c, hipSetDevice(c->device));
@@ -1234,7 +1363,7 @@ static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int 
     const int m = std::min(chunk, n - s0);
     HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), d_desc + s0, m, max_w, d_in, d_out,
                                   d_res + s0, c->est.as<uint16_t>(), nullptr, nullptr, c->order_or_null(), s,
-                                  avr::SeqFiles(), avr::kFlagFields));
+                                  avr::SeqFiles(), avr::kFlagFields | coder_flag(model)));
   }
   return AVR_OK;
 }
@@ -1777,7 +1906,7 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
 
 int avr_hooks_compress_stream_begin(avr_ctx* c, int model, avr_hooks_session** out) {
   if (!c || !out) return AVR_ERR_INVALID_ARGUMENT;
-  if (model != AVR_MODEL_REFERENCE && model != AVR_MODEL_PARALLEL) return AVR_ERR_INVALID_ARGUMENT;
+  if (!valid_model(model)) return AVR_ERR_INVALID_ARGUMENT;
   *out = nullptr;
   avr_hooks_session* hs = new (std::nothrow) avr_hooks_session;
   if (!hs) return AVR_ERR_OUT_OF_MEMORY;

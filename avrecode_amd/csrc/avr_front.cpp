@@ -8,7 +8,17 @@
 
 namespace avr {
 
-const char* const kParallelModelTag = "avrecode-amd:P32";   // parallel model + P-format coder (avr_engine.h)
+const char* const kParallelModelTag = "avrecode-amd:P64";     // parallel model, arithmetic_code<uint64_t, uint8_t>
+const char* const kParallel32ModelTag = "avrecode-amd:P32";   // parallel model, P32 coder (avr_engine.h)
+
+int model_of_version(const std::string& v) {
+  if (v == kParallelModelTag) return 1;
+  if (v == kParallel32ModelTag) return 2;
+  return v.rfind("avrecode-amd:", 0) == 0 ? -1 : 0;
+}
+const char* version_of_model(int model) {
+  return model == 1 ? kParallelModelTag : model == 2 ? kParallel32ModelTag : nullptr;
+}
 
 namespace {
 

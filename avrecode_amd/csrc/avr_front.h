@@ -82,7 +82,16 @@ void pb_put_metadata_version(std::vector<uint8_t>* o, const std::string& version
 bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version,
               bool* has_metadata = nullptr);
 
-extern const char* const kParallelModelTag;   // Recoded.Metadata.version for the parallel model
+// Recoded.Metadata.version of the parallel model's containers (the reference model writes none, as
+// the reference does): its decisions through the reference's arithmetic_code<uint64_t, uint8_t>, or
+// through the optional 32-bit P32 coder
+extern const char* const kParallelModelTag;     // "avrecode-amd:P64"
+extern const char* const kParallel32ModelTag;   // "avrecode-amd:P32"
+// The model a container's Metadata.version names: 0 reference (no tag, or any foreign one), 1
+// parallel / u64 coder, 2 parallel / P32 coder (AVR_MODEL_*); -1 another avrecode-amd format (the
+// round-2 "avrecode-amd:P", ...), which must be refused rather than read as a reference container.
+int model_of_version(const std::string& version);
+const char* version_of_model(int model);   // nullptr for the reference model
 constexpr int kSurrogateMarkerBytes = 8;      // recode.cpp:27
 void surrogate_marker(uint64_t seq, uint8_t out[8]);
 

@@ -1,22 +1,12 @@
-// parallel slice kernel, MODE_DECOMPRESS (one translation unit per kernel: see avr_walker.h).
+// parallel slice kernel, MODE_DECOMPRESS, the reference's arithmetic_code<uint64_t, uint8_t> coder (one
+// translation unit per kernel: see avr_walker.h).
 #include "avr_walker.h"
 
 namespace avr {
 
 hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
                     uint8_t* out, avr_slice_result* res, uint16_t* est, const int* order, uint32_t flags, hipStream_t stream) {
-  // the per-CU priority board of this kernel starts empty on every launch (cu_cell's slot counter
-  // must not carry a previous launch's residue)
-  if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
-  hipLaunchKernelGGL((slices_parallel_kernel<MODE_DECOMPRESS, false>), dim3(n), dim3(slice_threads<MODE_DECOMPRESS>()), lds, stream, T, descs, n, in, out, res, est, order, flags);
-  // field pictures / MBAFF frames: a second launch over the batch (its workgroups for progressive
-  // slices return at once)
-  if (flags & kFlagFields) {
-    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-    if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
-    hipLaunchKernelGGL((slices_parallel_kernel<MODE_DECOMPRESS, true>), dim3(n), dim3(slice_threads<MODE_DECOMPRESS>()), lds, stream, T, descs, n, in, out, res, est, order, flags);
-  }
-  return hipGetLastError();
+  return launch_parallel<MODE_DECOMPRESS, false>(T, descs, n, lds, in, out, res, est, order, flags, stream);
 }
 
 // AVR_PROFILE builds: read (and clear) this kernel's section cycle counters; zeros otherwise.

@@ -28,6 +28,9 @@ constexpr int kFlagRingShift = 16;
 // launch flag: the batch may hold field pictures / MBAFF frames -- the parallel launches add a
 // launch of the field-capable kernel for them, the sequential ones use it for every file
 constexpr uint32_t kFlagFields = 2;
+// launch flag: parallel model with the P32 container coder (avr_k_*32.hip) instead of the reference's
+// arithmetic_code<uint64_t, uint8_t>
+constexpr uint32_t kFlagP32 = 4;
 size_t shared_bytes(int max_mb_width);
 // does workgroup b of a 4G-workgroup launch land on CU group b mod G (schedule_kernel's assumption)?
 hipError_t probe_round_robin(size_t lds, bool* ok);
@@ -52,6 +55,12 @@ hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc*
 hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                       const int* order, uint32_t flags, hipStream_t stream);
+hipError_t launch_parallel_compress32(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
+                                      const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
+                                      const int* order, uint32_t flags, hipStream_t stream);
+hipError_t launch_parallel_decompress32(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
+                                        const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
+                                        const int* order, uint32_t flags, hipStream_t stream);
 hipError_t launch_parallel_generate(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                     const int* order, uint32_t flags, hipStream_t stream);

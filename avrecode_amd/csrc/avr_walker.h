@@ -486,7 +486,7 @@ AVR_FI void est_table_reset(uint16_t* est_g, Shared* sh) {
 // only when a batch may hold such slices: kFlagFields), so that the progressive walker carries no
 // field tests in its per-bin and per-macroblock code
 
-template <int MODE, bool RM, bool FLD = false>
+template <int MODE, bool RM, bool FLD = false, bool P32 = false>
 struct Walker {
   static constexpr bool DEC = MODE == MODE_COMPRESS || MODE == MODE_TRACE;  // CABAC decoding side
   const HotTables* T;     // LDS copy
@@ -507,9 +507,10 @@ struct Walker {
   CabacDecoder cd;
   CabacEncoder ce;
   RecodedEncoder re;
-  // the reference model's container uses arithmetic_code<uint64_t, uint8_t>; the parallel model's
-  // its own 32-bit coder (avr_engine.h, PDecoder)
-  typename std::conditional<RM, RecodedDecoder, PDecoder>::type rd;
+  // the model's decisions go through the reference's arithmetic_code<uint64_t, uint8_t> (both
+  // models' default containers); P32 = the parallel model's optional 32-bit coder (avr_engine.h,
+  // PDecoder; container tag avrecode-amd:P32)
+  typename std::conditional<P32, PDecoder, RecodedDecoder>::type rd;
   uint64_t rng;
   // slice state
   int W, H, mb_x, mb_y, slice_type, is_b, cat_, t8mode;
@@ -667,7 +668,7 @@ struct Walker {
   typedef const __attribute__((address_space(4))) uint32_t cu32;
   AVR_FI auto p1(uint32_t e) const {
     const uint32_t pos = (e & 0xff) + 1, tot = (e & 0xff) + (e >> 8) + 2;   // the sum est_update tests
-    if constexpr (RM) {
+    if constexpr (!P32) {
       cu64* dv = (cu64*)&G->hot.div[tot][0];
       return (__umul64hi(rd.range, dv[0]) >> (uint32_t)dv[1]) * pos;
     } else {
@@ -1777,8 +1778,8 @@ struct Walker {
 };
 
 // ---------------------------------------------------------------------------------------
-template <int MODE, bool RM, bool FLD>
-AVR_FI void init_slice_state(Walker<MODE, RM, FLD>& w, const EngineTables* T) {
+template <int MODE, bool RM, bool FLD, bool P32>
+AVR_FI void init_slice_state(Walker<MODE, RM, FLD, P32>& w, const EngineTables* T) {
   const int lane = threadIdx.x, nt = blockDim.x;  // every wave of the workgroup takes part
   const avr_slice_desc* d = w.d;
   // cabac contexts: 9.3.1.1
@@ -1812,8 +1813,8 @@ AVR_FI void init_slice_state(Walker<MODE, RM, FLD>& w, const EngineTables* T) {
   __syncthreads();
 }
 
-template <int MODE, bool RM, bool FLD>
-AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
+template <int MODE, bool RM, bool FLD, bool P32>
+AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
   const avr_slice_desc* d = w.d;
   w.W = d->mb_width;
   // a field picture is a picture of half the frame's rows (d->mb_height is the frame's)
@@ -1866,7 +1867,7 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
       // the upper neighbour's flags + cbp: the first dword of its edge record
       w.tf = *(const uint32_t*)&w.ring[w.mb_x];
       w.top_ok = (w.tf & F_DEC) != 0;
-    } else if (!(w.pst & Walker<MODE, RM, FLD>::PST_BOT)) {
+    } else if (!(w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT)) {
       w.mbaff_pair_start();
     }
     w.cf = 0;
@@ -1903,7 +1904,7 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
         if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
         w.lf = w.cf;
       } else {   // the pair edge of this macroblock; the pair's records move left after its bottom
-        const int bot = (w.pst & Walker<MODE, RM, FLD>::PST_BOT) != 0;
+        const int bot = (w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT) != 0;
         uint32_t* e32 = (uint32_t*)&w.pair_edge(bot)[w.mb_x];
         if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;
         uint32_t* pr = (uint32_t*)w.pair_rec();
@@ -1928,16 +1929,16 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
       if (!RM) w.update_prio();
     }
     // MBAFF: end_of_slice_flag follows the bottom macroblock of a pair only (7.3.4)
-    const int eos = (!(FLD && w.mbaff) || (w.pst & Walker<MODE, RM, FLD>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
+    const int eos = (!(FLD && w.mbaff) || (w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
     SPROF_ENDW(7, ps7);
     if (eos) break;
-    if (Walker<MODE, RM, FLD>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = AVR_SLICE_OVERREAD; break; }
-    // a P32 decoder reads at most 4 bytes past its stream (rd_init's window): a damaged stream is
-    // stopped within a macroblock of running off its end
-    if (MODE == MODE_DECOMPRESS && !RM && w.in.limit && w.rd.next > w.in.limit + 8) { w.err = AVR_SLICE_OVERREAD; break; }
+    if (Walker<MODE, RM, FLD, P32>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = AVR_SLICE_OVERREAD; break; }
+    // a parallel-model decoder reads at most 8 bytes past its stream (the recoded decoder's 63-bit
+    // window; P32: 4): a damaged stream is stopped within a macroblock of running off its end
+    if (MODE == MODE_DECOMPRESS && !RM && w.in.limit && w.rd.next > w.in.limit + 16) { w.err = AVR_SLICE_OVERREAD; break; }
     addr++;
-    if ((FLD && w.mbaff) && !(w.pst & Walker<MODE, RM, FLD>::PST_BOT)) {
-      w.pst |= Walker<MODE, RM, FLD>::PST_BOT;
+    if ((FLD && w.mbaff) && !(w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT)) {
+      w.pst |= Walker<MODE, RM, FLD, P32>::PST_BOT;
       w.my++;
       continue;
     }
@@ -1956,8 +1957,8 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD>& w) {
 // Run f on the walker instantiation of the slice's structure: w itself for a progressive frame,
 // a field-capable copy (FLD = true, set up from w) for field pictures and MBAFF frames.
 // --------------------------------------------------------------------------- kernel bodies
-template <int MODE, bool RM, bool FLD>
-AVR_FI void begin_slice(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out) {
+template <int MODE, bool RM, bool FLD, bool P32>
+AVR_FI void begin_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out) {
   w.d = d;
   w.in.g = in + d->payload_offset;
   w.in.limit = MODE == MODE_GENERATE ? 0 : d->read_limit;
@@ -1998,8 +1999,8 @@ AVR_FI void begin_slice(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, const
 #endif
 }
 
-template <int MODE, bool RM, bool FLD>
-AVR_FI void profile_slice(Walker<MODE, RM, FLD>& w) {
+template <int MODE, bool RM, bool FLD, bool P32>
+AVR_FI void profile_slice(Walker<MODE, RM, FLD, P32>& w) {
 #ifdef AVR_PROFILE
   w.bins = 0;
   const uint64_t t0 = PROF_T();
@@ -2021,8 +2022,8 @@ AVR_FI void profile_slice(Walker<MODE, RM, FLD>& w) {
 
 // The walker wave of a pipelined slice: parse + model, one op per bin into the ring, OP_END at
 // the end whatever happened.  Leaves its status in LDS for finish_slice.
-template <int MODE, bool RM, bool FLD>
-AVR_FI void walker_slice(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
+template <int MODE, bool RM, bool FLD, bool P32>
+AVR_FI void walker_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
   begin_slice(w, d, in, nullptr);
   profile_slice(w);
   if (!RM) cu_post(w.prio_cell, 0);   // leave the CU board
@@ -2204,7 +2205,7 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
 // finish, recode.cpp:1074, 1092-1094), gathering each op's reciprocal record with its lane;
 // decompress retires ring 0 (cabac::encoder::put / put_bypass / put_terminate,
 // recode.cpp:1443-1474, cabac_code.h:33-67).
-template <int MODE, bool RM>
+template <int MODE, bool P32>
 AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out, uint32_t flags) {
   const bool billing = (flags & kFlagBill) != 0;
   uint32_t bill[6] = {0, 0, 0, 0, 0, 0};
@@ -2216,7 +2217,7 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
   o.cap = d->out_capacity;
   o.n = 0;
   o.last = 0;
-  typename std::conditional<RM, RecodedEncoder, PEncoder>::type re;   // see Walker::rd
+  typename std::conditional<P32, PEncoder, RecodedEncoder>::type re;   // see Walker::rd
   CabacEncoder ce;
   VTab vt;
   if (MODE == MODE_COMPRESS) {
@@ -2246,11 +2247,11 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
     follow_prio(sh, &prio);
     if (MODE == MODE_COMPRESS) {
       const uint32_t tot_v = (op_v >> 8) & 127;
-      const uint64_t m_v = RM ? T->div[tot_v][0] : T->rcp32[tot_v];
-      const uint32_t s_v = RM ? (uint32_t)T->div[tot_v][1] : 0u;
+      const uint64_t m_v = !P32 ? T->div[tot_v][0] : T->rcp32[tot_v];
+      const uint32_t s_v = !P32 ? (uint32_t)T->div[tot_v][1] : 0u;
       // r1 of op j: the reference coder's exact quotient, or the P-format rule (avr_engine.h)
       auto r1_of = [&](uint32_t j, uint32_t op) {
-        if constexpr (RM) {
+        if constexpr (!P32) {
           const uint64_t m = readlane64(m_v, j);
           const uint32_t shift = __builtin_amdgcn_readlane(s_v, j);
           return (__umul64hi(re.range, m) >> shift) * ((op >> 1) & 127);
@@ -2355,8 +2356,8 @@ AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_re
 }
 
 // Single-wave slice (the generator: CABAC encode inline, no coder wave).
-template <int MODE, bool RM, bool FLD>
-AVR_FI void run_slice_inline(Walker<MODE, RM, FLD>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
+template <int MODE, bool RM, bool FLD, bool P32>
+AVR_FI void run_slice_inline(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
                              avr_slice_result* res) {
   begin_slice(w, d, in, out);
   profile_slice(w);
@@ -2391,7 +2392,7 @@ constexpr int slice_threads() {
 
 // FLD = false: the progressive frames of the batch; FLD = true: its field pictures and MBAFF frames
 // (a second launch over the same batch: each kernel leaves the other's slices alone)
-template <int MODE, bool FLD>
+template <int MODE, bool FLD, bool P32 = false>
 __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                 const uint8_t* in, uint8_t* out, avr_slice_result* res,
                                                                 uint16_t* est_scratch, const int* order,
@@ -2401,7 +2402,7 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   const int s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
   const avr_slice_desc* d = &descs[s];
   if ((d->structure != AVR_STRUCT_FRAME) != FLD) return;
-  Walker<MODE, false, FLD> w;
+  Walker<MODE, false, FLD, P32> w;
   w.sh = (Shared*)smem;
   w.ring = (EdgeRec*)(smem + sizeof(Shared));
   load_hot_tables(w.sh, G);
@@ -2443,9 +2444,30 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
     AVR_PLACE_T(s, 1);
   }
   else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
-  else coder_slice<MODE, false>(w.sh, w.T, d, out, flags);
+  else coder_slice<MODE, P32>(w.sh, w.T, d, out, flags);
   __syncthreads();
   if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
+}
+
+// Host side of the parallel launches (instantiated in each kernel TU, avr_k_*.hip, with that TU's
+// own CU board): the progressive kernel over the batch, then -- when the batch may hold field
+// pictures / MBAFF frames -- the field-capable kernel over the same batch (its workgroups for
+// progressive slices return at once).  The board starts empty on every launch (cu_cell's slot
+// counter must not carry a previous launch's residue).
+template <int MODE, bool P32>
+inline hipError_t launch_parallel(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
+                                  const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
+                                  const int* order, uint32_t flags, hipStream_t stream) {
+  if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
+  hipLaunchKernelGGL((slices_parallel_kernel<MODE, false, P32>), dim3(n), dim3(slice_threads<MODE>()), lds, stream,
+                     T, descs, n, in, out, res, est, order, flags);
+  if (flags & kFlagFields) {
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
+    hipLaunchKernelGGL((slices_parallel_kernel<MODE, true, P32>), dim3(n), dim3(slice_threads<MODE>()), lds, stream,
+                       T, descs, n, in, out, res, est, order, flags);
+  }
+  return hipGetLastError();
 }
 
 // Reference model: one workgroup (walker + coder wave) walks every slice of a file in file order
@@ -2536,7 +2558,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
     const int wave = tid >> 6;
     if (wave == 0) walker_slice(w, d, in, &res[s]);
     else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
-    else coder_slice<MODE, true>(w.sh, w.T, d, out, flags);
+    else coder_slice<MODE, false>(w.sh, w.T, d, out, flags);
     __syncthreads();
     if (tid == 0) finish_slice<MODE>(w.sh, d, &res[s]);
     __syncthreads();

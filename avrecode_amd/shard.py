@@ -19,7 +19,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import MODEL_PARALLEL, ParsedStream, assemble_container, parse_stream, plan_decompress, splice_container
+from . import (MODEL_PARALLEL, ParsedStream, assemble_container, container_model, parse_stream, plan_decompress,
+               splice_container)
 
 
 def partition(sizes, world: int) -> list[tuple[int, int]]:
@@ -45,8 +46,9 @@ def gather_flat(flat, status, offsets, lens, dst: int = 0, device=None):
     """Gather every rank's per-slice (status, bytes) to `dst`, in rank order.
 
     flat: this rank's outputs packed in one uint8 tensor (device tensor with RCCL), slice k's bytes
-    at flat[offsets[k] : offsets[k] + lens[k]].  Returns (status int32[n_total], blob bytes,
-    offsets uint64, lens uint32) on dst, None elsewhere.  Counts first (a fixed-size all_gather),
+    at flat[offsets[k] : offsets[k] + lens[k]].  Returns (status int32[n_total], blob uint8 array,
+    offsets uint64, lens uint32) on dst, None elsewhere (the blob is one host array written in
+    place: a multi-GB gather is copied once, device to host).  Counts first (a fixed-size all_gather),
     then one send/recv of the per-slice metadata and one of the flat bytes per rank: RCCL has no
     gatherv, and the payload moves device to device over xGMI."""
     import torch
@@ -72,7 +74,8 @@ def gather_flat(flat, status, offsets, lens, dst: int = 0, device=None):
         if sizes[rank]:
             dist.send(body, dst)
         return None
-    st, offs, ln, blobs, base = [], [], [], [], 0
+    st, offs, ln, base = [], [], [], 0
+    blob = np.empty(sum(sizes), dtype=np.uint8)
     for r in range(world):
         if r == rank:
             m, f = meta, body
@@ -88,10 +91,11 @@ def gather_flat(flat, status, offsets, lens, dst: int = 0, device=None):
         st.append(m[:c])
         offs.append(m[c:2 * c] + base)
         ln.append(m[2 * c:])
-        blobs.append(f.cpu().numpy().tobytes())
+        if sizes[r]:
+            torch.from_numpy(blob[base:base + sizes[r]]).copy_(f)
         base += sizes[r]
     cat = lambda xs, t: np.concatenate(xs).astype(t) if xs else np.zeros(0, t)  # noqa: E731
-    return cat(st, np.int32), b"".join(blobs), cat(offs, np.uint64), cat(ln, np.uint32)
+    return cat(st, np.int32), blob, cat(offs, np.uint64), cat(ln, np.uint32)
 
 
 def gather_blocks(local: list[bytes], status: list[int], dst: int = 0, device=None):
@@ -118,13 +122,15 @@ def subset(ps: ParsedStream, lo: int, hi: int) -> ParsedStream:
     return ParsedStream(d, ps.arena[a0:a1].copy(), w1 - w0, ps.max_mb_width, ps.max_mb_height)
 
 
-def sharded_compress(ctx, data: bytes, device=None, ps: ParsedStream | None = None) -> bytes | None:
+def sharded_compress(ctx, data: bytes, device=None, ps: ParsedStream | None = None,
+                     model: int = MODEL_PARALLEL) -> bytes | None:
     """PARALLEL-model compress of one file across all ranks; the container is returned on rank 0.
 
     Every rank parses the file (host), takes its contiguous slice range (partition), runs it on its
     GPU (compress + device roundtrip check: a slice is coded only if it regenerates its payload),
     packs the re-coded bytes on the device and sends them to rank 0 (gather_flat over RCCL), which
-    assembles the Recoded container.  Byte-identical to ctx.compress(data, MODEL_PARALLEL)."""
+    assembles the Recoded container from its own parse (avr_assemble_container_parsed).
+    Byte-identical to ctx.compress(data, model); model = MODEL_PARALLEL or MODEL_PARALLEL32."""
     import torch
     import torch.distributed as dist
 
@@ -137,7 +143,7 @@ def sharded_compress(ctx, data: bytes, device=None, ps: ParsedStream | None = No
     dev = _gather_device(ctx, device)
     if hi > lo:
         b = DeviceBatch(ctx, part)
-        b.roundtrip(MODEL_PARALLEL)
+        b.roundtrip(model)
         flat, d_off = b.pack()
         torch.cuda.synchronize()
         v = b.verdicts()
@@ -153,7 +159,7 @@ def sharded_compress(ctx, data: bytes, device=None, ps: ParsedStream | None = No
     if g is None:
         return None
     st, blob, offs, lens = g
-    return assemble_container(data, st, blob, offs, lens)
+    return assemble_container(data, st, blob, offs, lens, model=model, ps=ps)
 
 
 def _gather_device(ctx, device):
@@ -165,16 +171,16 @@ def _gather_device(ctx, device):
     return torch.device("cpu")
 
 
-def decompress_range(ctx, part: ParsedStream, device=None):
+def decompress_range(ctx, part: ParsedStream, device=None, model: int = MODEL_PARALLEL):
     """This rank's slice range of a sharded decompress on its GPU: (flat uint8 tensor, status,
     offsets, lens) with slice k's regenerated bytes at flat[offsets[k] : offsets[k] + lens[k]]
-    (packed on the device, avr_pack_outputs)."""
+    (packed on the device, avr_pack_outputs).  model: the container's (container_model)."""
     import torch
 
     from .batch import DeviceBatch
 
     b = DeviceBatch(ctx, part, device=device)
-    b.decompress(MODEL_PARALLEL)
+    b.decompress(model)
     flat, d_off = b.pack(which="d")
     torch.cuda.synchronize()
     res = b.results("d")
@@ -199,11 +205,12 @@ def sharded_decompress(ctx, avrc: bytes, device=None, run_range=None) -> bytes |
 
     rank, world = dist.get_rank(), dist.get_world_size()
     plan = plan_decompress(avrc)
+    model = container_model(avrc)
     lo, hi = partition(plan.descs["payload_size"], world)[rank]
     part = subset(plan, lo, hi)
     dev = _gather_device(ctx, device)
     if hi > lo:
-        flat, status, offs, lens = (run_range or (lambda p: decompress_range(ctx, p, device)))(part)
+        flat, status, offs, lens = (run_range or (lambda p: decompress_range(ctx, p, device, model)))(part)
     else:
         flat = torch.zeros(16, dtype=torch.uint8, device=dev)
         offs = lens = status = np.zeros(0, np.int64)

@@ -1,11 +1,15 @@
-"""Headline benchmark: input H.264 MB/s (compress + roundtrip), bit-exact, PARALLEL model.
+"""Headline benchmark: input H.264 MB/s (compress + roundtrip), bit-exact, PARALLEL model on the
+reference's arithmetic coder (arithmetic_code<uint64_t, uint8_t>, recode.cpp:315-316, 816-820).
 
 Workload (BASELINE.json configs[2]): a synthetic batch of 1024 independent
 1080p (120x68 MB) 4:2:0 High-profile CABAC I-slices, QP 22/26/30 by i%3, 8x8 transform on, made by
 the device generator (avr_synthesize_stream) before timing.  One step = one roundtrip of the whole
 batch, resident in HBM: compress every slice (CABAC decode -> model -> re-encode), derive the
 decompress descriptors, decompress every slice (model decode -> CABAC re-encode) and verify the
-regenerated payloads + last-byte patch against the input (recode.cpp:1594-1624 per slice).
+regenerated payloads + last-byte patch against the input (recode.cpp:1594-1624 per slice).  The
+parallel model is the reference model reset per slice and codes its decisions with
+the reference's own 64-bit coder; the optional 32-bit P32 coder is measured on the same batch
+afterwards and reported as the labelled extra key `p32` (with its container-size delta).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
@@ -46,6 +50,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, /opt/skills/guides/MI355X_MICROAR
 QPS = (22, 26, 30)
 METRIC = "input H.264 MB/s (compress+roundtrip) at 1/2/4/8 GPUs; bit-exact pass"
 WORKLOAD = "synthetic batch of independent 1080p CABAC I-slices (BASELINE configs[2])"
+# the progressive-slice kernels of the u64 coder (template <MODE, FLD, P32>), as rocprofv3 names them
+KERNEL_NAMES = {"compress": "slices_parallel_kernel<0, false, false>",
+                "decompress": "slices_parallel_kernel<1, false, false>"}
 
 
 def progress(msg):
@@ -384,49 +391,75 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     from avrecode_amd import shard, workloads
     from avrecode_amd.batch import DeviceBatch
 
+    model = avr.MODEL_PARALLEL
     progress(f"rank {rank}: generating the {seconds}-s stream")
     data = workloads.stream_4k(ctx, seconds=seconds, fps=30, mb_width=args.stream_mb[0], mb_height=args.stream_mb[1])
     progress(f"rank {rank}: {len(data)} bytes; parsing")
+    setup = {}
+    t = time.perf_counter()
     ps = avr.parse_stream(data)
+    setup["parse_s"] = time.perf_counter() - t
+    progress(f"rank {rank}: parsed {len(ps.descs)} slices in {setup['parse_s']:.1f} s")
+    t = time.perf_counter()
     lo, hi = shard.partition(ps.descs["payload_size"], world)[rank]
     part = shard.subset(ps, lo, hi)
+    setup["subset_s"] = time.perf_counter() - t
+    t = time.perf_counter()
     batch = DeviceBatch(ctx, part)
+    torch.cuda.synchronize()
+    setup["h2d_s"] = time.perf_counter() - t
+    progress(f"rank {rank}: slices [{lo}, {hi}) resident on the GPU ({setup['h2d_s']:.1f} s)")
     stream = torch.cuda.Stream(dev)
     mk = lambda: [torch.cuda.Event(enable_timing=True) for _ in range(4)]  # noqa: E731
+    gdev = _coll(dev)
+    PH = ("kernels_s", "results_d2h_s", "gather_s", "assemble_s")
 
-    def step(ev):
-        batch.roundtrip_timed(ev, avr.MODEL_PARALLEL, stream)
+    def step(ev, ph):
+        # wall-clock phases of one step: device roundtrip + pack; per-slice results to the host;
+        # the gather to rank 0 (RCCL send/recv, device to device, then one D2H into one array);
+        # rank 0's container assembly from its own parse (no second parse of the stream)
+        t0 = time.perf_counter()
+        batch.roundtrip_timed(ev, model, stream)
         flat, d_off = batch.pack(stream)
         stream.synchronize()
+        t1 = time.perf_counter()
         v = batch.verdicts()
         res = batch.results("c")
         offs = d_off.cpu().numpy()[: hi - lo].astype(np.int64)
         lens = np.where(res["status"] == 0, res["out_len"], 0).astype(np.int64)
         st = np.where(v == 1, 0, -1).astype(np.int64)
-        g = shard.gather_flat(flat, st, offs, lens, dst=0, device=dev)
-        if g is None:
-            return None, bool((v == 1).all())
-        return avr.assemble_container(data, *g), bool((v == 1).all())
+        t2 = time.perf_counter()
+        g = shard.gather_flat(flat, st, offs, lens, dst=0, device=gdev)
+        t3 = time.perf_counter()
+        avrc = None if g is None else avr.assemble_container(data, *g, model=model, ps=ps)
+        t4 = time.perf_counter()
+        for k, dt in zip(PH, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
+            ph[k] = ph.get(k, 0.0) + dt
+        return avrc, bool((v == 1).all())
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
-            step(mk())
-            progress(f"rank {rank}: warm-up step done")
+            wph = {}
+            step(mk(), wph)
+            progress(f"rank {rank}: warm-up step done ({', '.join(f'{k} {v:.1f}' for k, v in wph.items())})")
         evs = [mk() for _ in range(args.stream_steps)]
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ok = True
+        phases = {}
         for k in range(args.stream_steps):
-            avrc, good = step(evs[k])
+            avrc, good = step(evs[k], phases)
             ok = ok and good
             progress(f"rank {rank}: step {k} done")
         torch.cuda.synchronize()
         dist.barrier()
         elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
-    dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
-    dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+    mx = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
+    bad = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=gdev)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+    t = torch.cat([mx, bad])
     if rank != 0:
         return None
     # the container must decompress to the stream (checked outside the timed region)
@@ -437,19 +470,22 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     S = int(part.descs["payload_size"].sum())
     C = int(batch.results("c")["out_len"][v == 1].sum())
     dominant, t_dom = ("compress", t_comp) if t_comp >= t_dec else ("decompress", t_dec)
-    kernel_name = "slices_parallel_kernel<0>" if dominant == "compress" else "slices_parallel_kernel<1>"
+    kernel_name = KERNEL_NAMES[dominant]
     rec = {
         "metric": METRIC, "value": len(data) * args.stream_steps / float(t[0]) / 1e6, "unit": "MB/s",
         "n_gpus": world, "steps": args.stream_steps, "warmup": args.warmup,
         "ms_per_step": float(t[0]) / args.stream_steps * 1e3, "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "u8", "data": "synthetic (device generator, seeded; one GOP tiled)",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic (device generator, seeded; one GOP tiled)",
         "bit_exact": exact,
         "config": {"workload": "one 4K stream sharded by NAL unit, RCCL gather reassembly (BASELINE configs[3])"
                                + ("" if seconds == 600 else f"; REDUCED stream: {seconds} s of the config's 600 s"),
                    "seconds": seconds, "fps": 30, "mb": list(args.stream_mb), "slices": len(ps.descs),
                    "stream_bytes": len(data), "container_bytes": len(avrc), "model": "parallel",
                    "parallelism": f"slice ranges over {world} GPU(s)", "payload_bytes_S_rank0": S,
-                   "recoded_bytes_C_rank0": C, "compress_ms": t_comp * 1e3, "decompress_ms": t_dec * 1e3},
+                   "recoded_bytes_C_rank0": C, "compress_ms": t_comp * 1e3, "decompress_ms": t_dec * 1e3,
+                   "coder": "arithmetic_code<uint64_t,uint8_t>",
+                   "setup_s_rank0": {k: round(v, 3) for k, v in setup.items()},
+                   "step_phases_s_rank0": {k: round(v / args.stream_steps, 3) for k, v in phases.items()}},
         "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": (S + C) / t_dom / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (S + C) / t_dom / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "note": "rank 0's slice range: S + C per launch over the kernel's average HIP-event time"},
@@ -488,7 +524,7 @@ def main_stream_shard(args):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = _local_device()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     _init_dist(world, dev)
@@ -502,16 +538,37 @@ def main_stream_shard(args):
     ctx.close()
 
 
+def _backend():
+    """The process-group backend: RCCL ("nccl") by default; AVR_DIST_BACKEND=gloo runs the N > 1
+    code paths as host collectives (tests: several ranks on one GPU)."""
+    return os.environ.get("AVR_DIST_BACKEND", "nccl")
+
+
+def _local_device():
+    """This rank's GPU: LOCAL_RANK, modulo the visible devices (one per rank on a node; the
+    multi-process tests put every rank on cuda:0).  device_count does not initialise the GPU."""
+    import torch
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return local % max(1, torch.cuda.device_count())
+
+
+def _coll(dev):
+    """Where collective tensors live: the GPU with RCCL, host memory with gloo."""
+    import torch
+    return dev if _backend() == "nccl" else torch.device("cpu")
+
+
 def _init_dist(world, dev):
     import torch.distributed as dist
     if dist.is_initialized():
         return
+    kw = {"device_id": dev} if _backend() == "nccl" else {}
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(_backend(), **kw)
     else:   # a world-1 RCCL group: the same gather path as N > 1
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        dist.init_process_group(_backend(), rank=0, world_size=1, **kw)
 
 
 def load_traffic(args, kernel):
@@ -532,6 +589,37 @@ def load_traffic(args, kernel):
         return j["kernels"][kernel]["hbm_bytes_per_launch"]
     except Exception:
         return None
+
+
+def p32_extra(batch, args, stream, mk, n_bytes, C64):
+    """The optional P32 container coder (avrecode-amd:P32: the parallel model's decisions through a
+    32-bit range coder, avr_engine.h PEncoder / PDecoder -- NOT the reference's arithmetic) on the
+    headline batch: the same timed roundtrip steps, bit-exactness, and the container-size delta
+    against the u64 coder.  A labelled extra key; the headline value is the u64 coder's."""
+    import torch
+    import avrecode_amd as avr
+    with torch.cuda.stream(stream):
+        batch.roundtrip_timed(mk(), avr.MODEL_PARALLEL32, stream)   # warm-up
+        stream.synchronize()
+        evs = [mk() for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            batch.roundtrip_timed(evs[k], avr.MODEL_PARALLEL32, stream)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    v = batch.verdicts()
+    C = int(batch.results("c")["out_len"][v == 1].sum())
+    # leave the batch's outputs as the headline's (later legs read nothing from it, but be tidy)
+    with torch.cuda.stream(stream):
+        batch.roundtrip_timed(mk(), avr.MODEL_PARALLEL, stream)
+        stream.synchronize()
+    return {"coder": "P32 (avrecode-amd:P32; 32-bit range coder, truncated quotient; not the reference's arithmetic)",
+            "value": n_bytes * args.steps / elapsed / 1e6, "unit": "MB/s", "ms_per_step": elapsed / args.steps * 1e3,
+            "compress_ms": sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps,
+            "decompress_ms": sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps,
+            "bit_exact": bool((v == 1).all()), "recoded_bytes_C": C,
+            "container_delta_vs_u64": C / max(1, C64) - 1.0}
 
 
 def corpus_sharded(ctx, args, world, rank, dev):
@@ -561,9 +649,11 @@ def corpus_sharded(ctx, args, world, rank, dev):
                 back = ctx.decompress_files(outs)
                 ok = back == datas
             dt = time.perf_counter() - t0
-            t = torch.tensor([dt, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
-            dist.all_reduce(t[0:1], op=dist.ReduceOp.MAX)
-            dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+            mx = torch.tensor([dt], dtype=torch.float64, device=_coll(dev))
+            bad = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=_coll(dev))
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+            t = torch.cat([mx, bad])
         rec[tag] = {"MB_s": total / float(t[0]) / 1e6, "wall_s": float(t[0]), "bit_exact": bool(t[1] == 0)}
         progress(f"corpus {tag} over {world} GPU(s): {rec[tag]['MB_s']:.2f} MB/s")
     return rec
@@ -589,6 +679,7 @@ def main():
     ap.add_argument("--rfiles", type=int, default=256, help="files in the R-mode many-files leg (0: skip)")
     ap.add_argument("--stream-leg-seconds", type=int, default=30,
                     help="N=1 default run: length of the configs[3] stream leg (0: skip)")
+    ap.add_argument("--no-p32", action="store_true", help="skip the P32-coder extra measurement")
     ap.add_argument("--stream-steps", type=int, default=2)
     ap.add_argument("--stream-shard", action="store_true",
                     help="configs[3]: one 4K stream sharded over the GPUs with the RCCL gather (strong scaling)")
@@ -607,11 +698,11 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = _local_device()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        _init_dist(world, dev)
 
     def barrier():
         if world > 1:
@@ -651,8 +742,12 @@ def main():
     bit_exact = bit_exact and bool((batch.verdicts() == 1).all())
     t_comp = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps / 1e3
     t_dec = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps / 1e3
+    # labelled extra, outside the headline's timed region: the same batch through the P32 coder
+    p32 = None
+    if world == 1 and not args.no_p32:
+        p32 = p32_extra(batch, args, stream, mk, len(data), C)
 
-    tot = torch.tensor([elapsed, len(data), 0.0 if bit_exact else 1.0], dtype=torch.float64, device=dev)
+    tot = torch.tensor([elapsed, len(data), 0.0 if bit_exact else 1.0], dtype=torch.float64, device=_coll(dev))
     if world > 1:
         mx = tot[0:1].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -665,7 +760,7 @@ def main():
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         dominant, t_dom = ("compress", t_comp) if t_comp >= t_dec else ("decompress", t_dec)
-        kernel_name = "slices_parallel_kernel<0>" if dominant == "compress" else "slices_parallel_kernel<1>"
+        kernel_name = KERNEL_NAMES[dominant]
         achieved = (S + C) / t_dom / 1e9
         line = {
             "metric": METRIC,
@@ -678,7 +773,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": "u64",
             "data": "synthetic (device generator, seeded)",
             "bit_exact": bit_exact and bad == 0,
             "config": {
@@ -686,7 +781,9 @@ def main():
                 "slices_per_gpu": args.slices,
                 "mb": [args.mb_width, args.mb_height],
                 "qp": list(QPS),
-                "model": "parallel (fresh model per slice)",
+                "model": "parallel (the reference model reset per slice, SURVEY.md 7)",
+                "coder": "arithmetic_code<uint64_t,uint8_t> (the reference's: 64-bit interval, byte digits, "
+                         "p1 = (range / (pos + neg)) * pos exact; arithmetic_code.h:106-126, 232-248)",
                 "input_bytes_per_gpu": len(data),
                 "payload_bytes_S": S,
                 "recoded_bytes_C": C,
@@ -705,6 +802,8 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if p32 is not None:
+            line["p32"] = p32
         progress(f"batch: {line['value']:.1f} MB/s")
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(ctx, args, len(data))

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define AVRECODE_ABI_VERSION 3
+#define AVRECODE_ABI_VERSION 4
 
 typedef enum {
   AVR_OK = 0,
@@ -46,9 +46,16 @@ typedef enum {
 /* Model modes.  REFERENCE = recode.cpp's h264_model exactly (estimators persist across slices,
  * previous-frame and cross-slice contexts); output bytes equal the reference compressor's.
  * Sequential over slices (one wavefront for the whole file).
- * PARALLEL = the same model applied to every slice from a fresh state; slices are independent,
- * one wavefront per slice, shardable across GPUs.  Tagged in Recoded.Metadata.version. */
-typedef enum { AVR_MODEL_REFERENCE = 0, AVR_MODEL_PARALLEL = 1 } avr_model;
+ * PARALLEL = the same model applied to every slice from a fresh state; slices are
+ * independent, one wavefront per slice, shardable across GPUs.  Its decisions go through the
+ * reference's own coder, arithmetic_code<uint64_t, uint8_t> with p1 = (range / (pos + neg)) * pos
+ * (arithmetic_code.h:106-126, 232-248; recode.cpp:315-316, 816-820).  Tagged in
+ * Recoded.Metadata.version as "avrecode-amd:P64".
+ * PARALLEL32 = the parallel model with this library's optional 32-bit range coder (byte digits,
+ * r1 = floor(range * floor(2^32 / tot) / 2^32) * pos; avr_engine.h PEncoder): fewer instructions per
+ * decision, not the reference's arithmetic.  Tagged "avrecode-amd:P32".  Containers of every mode
+ * decompress with avr_decompress_file, which reads the tag. */
+typedef enum { AVR_MODEL_REFERENCE = 0, AVR_MODEL_PARALLEL = 1, AVR_MODEL_PARALLEL32 = 2 } avr_model;
 
 typedef struct avr_ctx avr_ctx;
 
@@ -219,11 +226,23 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
 
 /* Rank 0 of a sharded PARALLEL-model compress: build the Recoded container from per-slice outputs
  * gathered from every rank (compressor::run + find_next_coded_block_and_emit_literal,
- * recode.cpp:1115-1132, 1275-1297).  Host only.  Slice k (avr_parse_stream order) is coded when it
- * is a candidate and status[k] == 0; its re-coded bytes are recoded[offsets[k] .. + lens[k]).
- * The result is byte-identical to avr_compress_file(..., AVR_MODEL_PARALLEL). */
-int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const int32_t* status, const uint8_t* recoded,
-                           const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len);
+ * recode.cpp:1115-1132, 1275-1297).  Host only.  model = AVR_MODEL_PARALLEL or _PARALLEL32 (the
+ * coder the outputs were made with: the container's tag).  Slice k (avr_parse_stream order) is
+ * coded when it is a candidate and status[k] == 0; its re-coded bytes are recoded[offsets[k] ..
+ * + lens[k]), inside recoded_len (AVR_ERR_INVALID_ARGUMENT otherwise).  The result is
+ * byte-identical to avr_compress_file(..., model).  avr_assemble_container parses `file` again;
+ * avr_assemble_container_parsed takes avr_parse_stream's descs and arena for it instead (the parse
+ * a sharded caller already holds: no second pass over a multi-GB stream). */
+int avr_assemble_container(const uint8_t* file, size_t n, int model, int n_slices, const int32_t* status,
+                           const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets, const uint32_t* lens,
+                           uint8_t** out, size_t* out_len);
+int avr_assemble_container_parsed(const uint8_t* file, size_t n, int model, const avr_slice_desc* descs, int n_slices,
+                                  const uint8_t* arena, size_t arena_len, const int32_t* status,
+                                  const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets,
+                                  const uint32_t* lens, uint8_t** out, size_t* out_len);
+/* The model mode a Recoded container was written with (its Metadata.version): AVR_MODEL_*.
+ * AVR_ERR_FORMAT for bytes that are not a Recoded message or name another avrecode-amd format. */
+int avr_container_model(const uint8_t* avrc, size_t n, int* model);
 
 /* Sharded PARALLEL-model decompress (decompressor::run, recode.cpp:1312-1357, split over ranks).
  * avr_plan_decompress: the container's coded slices as a decompress batch, host only -- *descs
@@ -234,11 +253,14 @@ int avr_assemble_container(const uint8_t* file, size_t n, int n_slices, const in
  * avr_splice_container (rank 0): the original file from the container's literals and slice k's
  * regenerated bytes regen[offsets[k] .. + lens[k]) (avr_decompress_slices output before the
  * last-byte patch, which this applies, recode.cpp:1345-1356); status[k] != 0 fails the file with
- * AVR_ERR_FORMAT.  Byte-identical to avr_decompress_file. */
+ * AVR_ERR_FORMAT; a slice whose bytes lie outside regen_len or exceed its descriptor's out_capacity
+ * gives AVR_ERR_INVALID_ARGUMENT.  Byte-identical to avr_decompress_file.  A sharded caller
+ * decompresses the batch with the container's model (avr_container_model). */
 int avr_plan_decompress(const uint8_t* avrc, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
                         size_t* arena_len, size_t* work_len, int* max_mb_width, int* max_mb_height);
 int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int32_t* status, const uint8_t* regen,
-                         const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len);
+                         size_t regen_len, const uint64_t* offsets, const uint32_t* lens, uint8_t** out,
+                         size_t* out_len);
 
 /* Container codec check (host only): parse a Recoded protobuf (recode.proto:1-19) with the
  * library's own wire codec -- the one avr_decompress_file uses -- and return (a) its fields as JSON,

@@ -88,7 +88,7 @@ static inline uint64_t rc_p1(uint64_t range, int pos, int neg) {
 void rc_enc_init(ac_enc_t *e, obuf_t *out);
 void rc_dec_init(ac_dec_t *d, const uint8_t *in, size_t n);
 
-/* P-format coder: NOT part of the reference.  The parallel model's container (tag
+/* P-format coder: NOT part of the reference.  The parallel model's optional container (tag
  * "avrecode-amd:P32") is this library's own format and codes the model's decisions with a 32-bit
  * range coder with byte digits (avrecode_amd/csrc/avr_engine.h, PEncoder / PDecoder), restated
  * here: range in [2^24, 2^32) between decisions (0xFFFFFFFF at the start), bin 1 takes the top
@@ -239,7 +239,10 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
 
 /* ------------------------------------------------------------------------------------------ */
 /* The predictor (recode.cpp:615-1059) and the two drivers                                   */
-enum { AVR_MODE_R = 0, AVR_MODE_P = 1 };
+/* R: the reference model.  P: the parallel model (fresh model per slice) on the reference's
+ * arithmetic_code<uint64_t, uint8_t> (tag "avrecode-amd:P64").  P32: the parallel model on the P-format
+ * coder below (tag "avrecode-amd:P32"). */
+enum { AVR_MODE_R = 0, AVR_MODE_P = 1, AVR_MODE_P32 = 2 };
 
 typedef struct avr_model avr_model_t;
 avr_model_t *avr_model_new(void);
@@ -273,8 +276,9 @@ int avr_cabac_regenerate(const avr_slice_hdr_t *h, const uint8_t *payload, size_
                          size_t *bins, size_t *end_bitpos);
 
 /* Per-slice fresh-model compress -> decompress records for CABAC slices [lo, hi) of a file      */
-/* (layout in oracle_recode.c).  Returns the file's CABAC slice count, or -1.                   */
-long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int check_recodable, uint8_t **out,
+/* (layout in oracle_recode.c), on the u64 coder (p32 = 0) or the P32 coder (p32 = 1).          */
+/* Returns the file's CABAC slice count, or -1.                                                  */
+long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int check_recodable, int p32, uint8_t **out,
                          size_t *out_len);
 
 /* protobuf wire codec for recode.proto */
@@ -290,7 +294,8 @@ typedef struct {
   int last_byte_len;
 } avr_pb_block_t;
 void avr_pb_put_block(obuf_t *o, const avr_pb_block_t *b);
-/* model mode recorded in Recoded.metadata.version (R-mode: absent, as the reference writes) */
+/* model mode recorded in Recoded.metadata.version (R-mode: absent, as the reference writes):
+ * AVR_MODE_R / _P / _P32, or -1 for another "avrecode-amd:" format */
 int avr_pb_mode(const uint8_t *in, size_t n);
 /* parses a Recoded message; returns block count, *blocks malloc'd (pointers into in) */
 int avr_pb_parse(const uint8_t *in, size_t n, avr_pb_block_t **blocks);

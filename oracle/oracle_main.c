@@ -1,12 +1,13 @@
 /*
  * Oracle CLI (mirrors recode.cpp:1627-1659 main).  TEST INFRASTRUCTURE ONLY.
  *
- *   recode_oracle compress   [-p] <input> [output]
- *   recode_oracle decompress      <input> [output]
- *   recode_oracle roundtrip  [-p] <input> [output]
+ *   recode_oracle compress   [-p|-p32] <input> [output]
+ *   recode_oracle decompress           <input> [output]
+ *   recode_oracle roundtrip  [-p|-p32] <input> [output]
  *   recode_oracle slices          <input>          per-slice parse / regeneration report
  *
- * -p selects the parallel model (fresh model per slice); default is the reference model.
+ * -p selects the parallel model (fresh model per slice) on arithmetic_code<uint64_t, uint8_t>, -p32 the
+ * parallel model on the P-format coder; default is the reference model.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -123,6 +124,7 @@ int main(int argc, char **argv) {
   }
   const char *cmd = argv[a++];
   if (a < argc && !strcmp(argv[a], "-p")) { mode = AVR_MODE_P; a++; }
+  else if (a < argc && !strcmp(argv[a], "-p32")) { mode = AVR_MODE_P32; a++; }
   if (a >= argc) return 1;
   const char *in = argv[a++];
   const char *outp = a < argc ? argv[a] : NULL;

@@ -28,7 +28,8 @@
 avr_stats_t avr_last_stats;
 size_t avr_last_bill[8], avr_last_cabac_bill[8];
 static const int SURROGATE_MARKER_BYTES = 8; /* recode.cpp:27 */
-#define AVR_P_MODE_TAG "avrecode-amd:P32"   /* the parallel model + P-format coder (avr_oracle.h) */
+#define AVR_P_MODE_TAG "avrecode-amd:P64"     /* the parallel model + arithmetic_code<uint64_t, uint8_t> */
+#define AVR_P32_MODE_TAG "avrecode-amd:P32"   /* the parallel model + P-format coder (avr_oracle.h) */
 
 /* ===================================================================== protobuf wire codec */
 static void pb_varint(obuf_t *o, uint64_t v) {
@@ -96,7 +97,8 @@ static int pb_parse_block(const uint8_t *p, const uint8_t *e, avr_pb_block_t *b)
   }
   return 0;
 }
-/* Recoded.metadata.version == AVR_P_MODE_TAG -> P-mode, anything else R-mode */
+/* Recoded.metadata.version: AVR_P_MODE_TAG -> P, AVR_P32_MODE_TAG -> P32, another avrecode-amd tag -> -1,
+ * anything else (none: the reference's containers) R */
 int avr_pb_mode(const uint8_t *in, size_t n) {
   const uint8_t *p = in, *e = in + n;
   int mode = AVR_MODE_R;
@@ -112,7 +114,11 @@ int avr_pb_mode(const uint8_t *in, size_t n) {
         if (pb_rd_varint(&q, qe, &t2)) break;
         if ((t2 & 7) != 2) { if (pb_skip(&q, qe, (int)(t2 & 7))) break; continue; }
         if (pb_rd_varint(&q, qe, &l2) || (uint64_t)(qe - q) < l2) break;
-        if ((t2 >> 3) == 1) mode = (l2 == strlen(AVR_P_MODE_TAG) && !memcmp(q, AVR_P_MODE_TAG, l2)) ? AVR_MODE_P : AVR_MODE_R;
+        if ((t2 >> 3) == 1)
+          mode = (l2 == strlen(AVR_P_MODE_TAG) && !memcmp(q, AVR_P_MODE_TAG, l2))       ? AVR_MODE_P
+                 : (l2 == strlen(AVR_P32_MODE_TAG) && !memcmp(q, AVR_P32_MODE_TAG, l2)) ? AVR_MODE_P32
+                 : (l2 >= 13 && !memcmp(q, "avrecode-amd:", 13))                          ? -1
+                                                                                        : AVR_MODE_R;
         q += l2;
       }
     }
@@ -478,10 +484,11 @@ static int slice_recodable(const slice_t *s) {
   return ok;
 }
 
-/* a fresh parallel model: its container uses the P-format coder */
-static avr_model_t *model_new_p(void) {
+/* a fresh parallel model (recode.cpp:1057 estimators, nothing carried over); p32: its container
+ * uses the P-format coder instead of arithmetic_code<uint64_t, uint8_t> */
+static avr_model_t *model_new_p(int p32) {
   avr_model_t *m = avr_model_new();
-  m->p32 = 1;
+  m->p32 = p32;
   return m;
 }
 
@@ -532,19 +539,19 @@ int avr_compress_slice_p(const avr_slice_hdr_t *h, const uint8_t *payload, size_
   s.h = *h;
   s.payload = payload;
   s.rbsp_len = n + h->cabac_start;
-  avr_model_t *m = model_new_p();
+  avr_model_t *m = model_new_p(0);
   int r = compress_slice_with_model(m, &s, recoded, bins);
   avr_model_free(m);
   return r;
 }
-static int decompress_slice_with_model_fresh(const slice_t *s, const uint8_t *rc, size_t n, obuf_t *cabac) {
-  avr_model_t *m = model_new_p();
+static int decompress_slice_with_model_fresh(const slice_t *s, const uint8_t *rc, size_t n, obuf_t *cabac, int p32) {
+  avr_model_t *m = model_new_p(p32);
   int r = decompress_slice_with_model(m, &s->h, s->picture_id, rc, n, cabac);
   avr_model_free(m);
   return r;
 }
 int avr_decompress_slice_p(const avr_slice_hdr_t *h, const uint8_t *rc, size_t n, obuf_t *cabac) {
-  avr_model_t *m = model_new_p();
+  avr_model_t *m = model_new_p(0);
   int r = decompress_slice_with_model(m, h, 0, rc, n, cabac);
   avr_model_free(m);
   return r;
@@ -560,7 +567,7 @@ int avr_decompress_slice_p(const avr_slice_hdr_t *h, const uint8_t *rc, size_t n
 static void put_u32(obuf_t *o, uint32_t v) {
   for (int k = 0; k < 4; k++) ob_put(o, (uint8_t)(v >> (8 * k)));
 }
-long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int check_recodable, uint8_t **out,
+long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int check_recodable, int p32, uint8_t **out,
                          size_t *out_len) {
   avr_nal_t *nals;
   int nn = avr_demux(file, n, &nals);
@@ -579,7 +586,7 @@ long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int ch
       size_t bins = 0;
       int rcs = -30;
       if (s.h.supported) {
-        avr_model_t *m = model_new_p();
+        avr_model_t *m = model_new_p(p32);
         rcs = compress_slice_with_model(m, &s, &rc, &bins);
         avr_model_free(m);
       } else {
@@ -589,7 +596,7 @@ long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int ch
       put_u32(&o, (uint32_t)bins);
       put_u32(&o, (uint32_t)rc.len);
       ob_append(&o, rc.data, rc.len);
-      int rds = rcs == 0 ? decompress_slice_with_model_fresh(&s, rc.data, rc.len, &cab) : -31;
+      int rds = rcs == 0 ? decompress_slice_with_model_fresh(&s, rc.data, rc.len, &cab, p32) : -31;
       if (rcs != 0) ob_init(&cab);
       put_u32(&o, (uint32_t)rds);
       put_u32(&o, (uint32_t)cab.len);
@@ -617,12 +624,13 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
   avr_model_t *model = mode == AVR_MODE_R ? avr_model_new() : NULL;
   obuf_t o;
   ob_init(&o);
-  if (mode == AVR_MODE_P) {
-    /* Recoded.Metadata.version (recode.proto:3) tags the parallel model; R-mode writes none,
-     * exactly like the reference (which never sets metadata). */
+  if (mode != AVR_MODE_R) {
+    /* Recoded.Metadata.version (recode.proto:3) tags the parallel model and its coder; R-mode writes
+     * none, exactly like the reference (which never sets metadata). */
+    const char *tag = mode == AVR_MODE_P32 ? AVR_P32_MODE_TAG : AVR_P_MODE_TAG;
     obuf_t md;
     ob_init(&md);
-    pb_bytes(&md, 1, (const uint8_t *)AVR_P_MODE_TAG, strlen(AVR_P_MODE_TAG));
+    pb_bytes(&md, 1, (const uint8_t *)tag, strlen(tag));
     pb_bytes(&o, 1, md.data, md.len);
     ob_free(&md);
   }
@@ -645,7 +653,7 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
       lit.literal_len = gap;
       avr_pb_put_block(&o, &lit);
       prev_end += gap + s.size;
-      avr_model_t *m = mode == AVR_MODE_R ? model : model_new_p();
+      avr_model_t *m = mode == AVR_MODE_R ? model : model_new_p(mode == AVR_MODE_P32);
       obuf_t rc;
       size_t bins = 0;
       int r = compress_slice_with_model(m, &s, &rc, &bins);
@@ -742,7 +750,9 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
   stream_state_t *st = (stream_state_t *)calloc(1, sizeof(stream_state_t));
   st->x264_build = -1;
   avr_model_t *model = avr_model_new();
-  int mode_r = avr_pb_mode(in, n) == AVR_MODE_R;
+  const int mode = avr_pb_mode(in, n);
+  int mode_r = mode == AVR_MODE_R;
+  if (mode < 0) ret = -10;   /* another avrecode-amd format */
   size_t unused_bill[8] = {0};
   memset(avr_last_cabac_bill, 0, sizeof(avr_last_cabac_bill));
   int next_coded = 0;
@@ -757,7 +767,7 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
     if (b->has_cabac) {
       avr_model_t *m = model;
       avr_model_t *fresh = NULL;
-      if (!mode_r) m = fresh = model_new_p();
+      if (!mode_r) m = fresh = model_new_p(mode == AVR_MODE_P32);
       obuf_t cab;
       int r = decompress_slice_with_model(m, &s.h, s.picture_id, b->cabac, b->cabac_len, &cab);
       if (fresh) {

@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-ARGS=${PMC_ARGS:---slices 1024 --steps 1 --warmup 0 --no-cpu-baseline --no-files --no-corpus}
+ARGS=${PMC_ARGS:---slices 1024 --steps 1 --warmup 0 --no-cpu-baseline --no-files --no-corpus --no-p32}
 mkdir -p gpurun_out/pmc_$TAG
 timeout -k 10 60 rocprofv3 -L > gpurun_out/pmc_$TAG/counters.txt 2>&1 || true
 k=0

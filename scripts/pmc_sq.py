@@ -10,10 +10,9 @@ import json
 import os
 from collections import defaultdict
 
-# progressive-slice kernels ("<0, false>" since the field-capable instantiations, which return at
-# once on a progressive batch; "<0>" before)
-KERNELS = {"slices_parallel_kernel<0>": "compress", "slices_parallel_kernel<1>": "decompress",
-           "slices_parallel_kernel<0, false>": "compress", "slices_parallel_kernel<1, false>": "decompress"}
+# progressive-slice kernels of the u64 coder (template <MODE, FLD, P32> since round 4; the
+# field-capable instantiations return at once on a progressive batch)
+KERNELS = {"slices_parallel_kernel<0, false, false>": "compress", "slices_parallel_kernel<1, false, false>": "decompress"}
 
 
 def main():

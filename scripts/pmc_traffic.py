@@ -14,6 +14,9 @@ import json
 import os
 from collections import defaultdict
 
+# template <MODE, FLD, P32> since round 4 (bench.py KERNEL_NAMES)
+KERNELS = ("slices_parallel_kernel<0, false, false>", "slices_parallel_kernel<1, false, false>")
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -25,11 +28,11 @@ def main():
     vals = defaultdict(lambda: defaultdict(list))
     for p in glob.glob(os.path.join(a.src, "pass*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
-            name = r["Kernel_Name"]
-            # the field-capable kernels (", true>") return at once on a progressive batch
-            if "slices_parallel_kernel<" not in name or ", true>" in name:
+            # the progressive-slice kernels of the u64 coder only (the field-capable instantiations
+            # return at once on a progressive batch; the P32 ones are another container format)
+            k = next((k for k in KERNELS if k in r["Kernel_Name"]), None)
+            if k is None:
                 continue
-            k = "slices_parallel_kernel<%s>" % name.split("slices_parallel_kernel<")[1][0]
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))

@@ -71,7 +71,7 @@ def oracle_cli(cmd, path, mode="R", out=None):
     _, cli = build_oracle()
     with tempfile.TemporaryDirectory() as td:
         o = Path(td) / "out.bin"
-        args = [str(cli), cmd] + (["-p"] if mode == "P" else []) + [str(path), str(o)]
+        args = [str(cli), cmd] + {"R": [], "P": ["-p"], "P32": ["-p32"]}[mode] + [str(path), str(o)]
         r = subprocess.run(args, capture_output=True)
         if r.returncode != 0:
             raise RuntimeError(f"recode_oracle {cmd} failed: {r.stderr.decode()}")
@@ -80,8 +80,9 @@ def oracle_cli(cmd, path, mode="R", out=None):
         return o.read_bytes()
 
 
-def slices_p(data: bytes, lo: int = 0, hi: int = 1 << 62, check_recodable: bool = True):
-    """Per-slice fresh-model (P-mode) compress -> decompress through the oracle.
+def slices_p(data: bytes, lo: int = 0, hi: int = 1 << 62, check_recodable: bool = True, p32: bool = False):
+    """Per-slice fresh-model (P-mode) compress -> decompress through the oracle, on the reference's
+    arithmetic_code<uint64_t, uint8_t> (p32 False, MODEL_PARALLEL) or the P32 coder (MODEL_PARALLEL32).
 
     Returns (total_slices, records); each record is a dict with recodable, status_c, bins, recoded,
     status_d, regen (avr_oracle_slices_p, oracle/oracle_recode.c)."""
@@ -89,10 +90,11 @@ def slices_p(data: bytes, lo: int = 0, hi: int = 1 << 62, check_recodable: bool 
     L = lib()
     f = L.avr_oracle_slices_p
     f.restype = ctypes.c_long
-    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_long, ctypes.c_long, ctypes.c_int,
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_long, ctypes.c_long, ctypes.c_int, ctypes.c_int,
                   ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
     out, olen = ctypes.c_void_p(), ctypes.c_size_t()
-    total = f(data, len(data), lo, hi, 1 if check_recodable else 0, ctypes.byref(out), ctypes.byref(olen))
+    total = f(data, len(data), lo, hi, 1 if check_recodable else 0, 1 if p32 else 0, ctypes.byref(out),
+              ctypes.byref(olen))
     if total < 0:
         raise RuntimeError("avr_oracle_slices_p: demux failed")
     raw = ctypes.string_at(out.value, olen.value) if olen.value else b""

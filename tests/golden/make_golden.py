@@ -7,8 +7,8 @@ Run in the build container (needs /root/reference):  python tests/golden/make_go
   arithmetic_code.h compiled as-is (oracle/_ref/ref_arith, built by `make -C oracle ref`).
 * container.json: Recoded messages serialised by the Python protobuf runtime from a descriptor
   built by hand from recode.proto (proto2) -- pins the hand-written wire codecs.
-* fixtures.json / fields.json: sizes / SHA-256 of the oracle's .avrc for the fixture files, both
-  model modes (regression pins).
+* fixtures.json / fields.json: sizes / SHA-256 of the oracle's .avrc for the fixture files, every
+  model mode (R, P on the u64 coder, P32; regression pins).
 
 The files hold data only (inputs and expected outputs); no reference source is stored.
 """
@@ -162,7 +162,7 @@ def container_golden():
                                "length_parity": bool(sz & 1), "last_byte": "%02x" % rng.randrange(256)})
             else:
                 blocks.append({"size": rng.randint(0, 1 << 40), "skip_coded": True})
-        case(blocks, version=rng.choice([None, "avrecode-amd:P"]))
+        case(blocks, version=rng.choice([None, "avrecode-amd:P", "avrecode-amd:P64", "avrecode-amd:P32"]))
     return cases
 
 
@@ -175,14 +175,14 @@ def main():
     (GOLD / "container.json").write_text(json.dumps(container_golden()))
     fx = []
     for name in ["realshort.mp4", "cockatoo.mp4"]:
-        for mode in ["R", "P"]:
+        for mode in ["R", "P", "P32"]:
             data = oracle_cli("compress", ROOT / "tests" / "fixtures" / name, mode=mode)
             fx.append({"file": name, "mode": mode, "avrc_len": len(data), "avrc_sha256": hashlib.sha256(data).hexdigest()})
     (GOLD / "fixtures.json").write_text(json.dumps(fx, indent=1))
     # fields.json: the field-coded fixtures' containers (the entries' descriptions are kept)
     fields = json.loads((GOLD / "fields.json").read_text())
     for e in fields["files"]:
-        for mode in ["R", "P"]:
+        for mode in ["R", "P", "P32"]:
             data = oracle_cli("compress", ROOT / "tests" / "fixtures" / e["file"], mode=mode)
             e[mode] = {"avrc_len": len(data), "avrc_sha256": hashlib.sha256(data).hexdigest()}
     (GOLD / "fields.json").write_text(json.dumps(fields, indent=1) + "\n")

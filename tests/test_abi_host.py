@@ -59,21 +59,29 @@ def test_parse_stream_agrees_with_oracle(name):
             assert patch_restores(r["regen"], payload), k
 
 
-def _oracle_outputs(data):
-    _, recs = slices_p(data)
+def _oracle_outputs(data, p32=False):
+    _, recs = slices_p(data, p32=p32)
     st = np.array([0 if r["recodable"] else -1 for r in recs], np.int32)
     return st, [r["recoded"] if r["recodable"] else b"" for r in recs]
 
 
+@pytest.mark.parametrize("parsed", [False, True], ids=["reparse", "parsed"])
+@pytest.mark.parametrize("mode", ["P", "P32"])
 @pytest.mark.parametrize("name", ["realshort.mp4", "cockatoo.mp4"])
-def test_assemble_container_matches_golden(name):
+def test_assemble_container_matches_golden(name, mode, parsed):
+    """Rank 0's assembly from the oracle's per-slice outputs gives the golden container of the
+    mode (the u64 coder's "avrecode-amd:P64" or the P32 coder's "avrecode-amd:P32"), with the file
+    parsed again or from the parse rank 0 already holds (avr_assemble_container_parsed)."""
     data = (FIX / name).read_bytes()
-    st, blobs = _oracle_outputs(data)
+    st, blobs = _oracle_outputs(data, p32=mode == "P32")
     lens = np.array([len(b) for b in blobs], np.uint32)
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
-    c = avr.assemble_container(data, st, b"".join(blobs), offs, lens)
-    g = GOLD[(name, "P")]
+    model = avr.MODEL_PARALLEL32 if mode == "P32" else avr.MODEL_PARALLEL
+    c = avr.assemble_container(data, st, b"".join(blobs), offs, lens, model=model,
+                               ps=avr.parse_stream(data) if parsed else None)
+    g = GOLD[(name, mode)]
     assert len(c) == g["avrc_len"] and hashlib.sha256(c).hexdigest() == g["avrc_sha256"]
+    assert avr.container_model(c) == model
 
 
 def test_assemble_container_rejects_bad_arguments():
@@ -82,6 +90,24 @@ def test_assemble_container_rejects_bad_arguments():
         avr.assemble_container(data, np.zeros(3, np.int32), b"", np.zeros(3, np.uint64), np.zeros(3, np.uint32))
     with pytest.raises(avr.AvrError):
         avr.parse_stream(b"not a video")
+    # a coded slice's bytes outside the gathered buffer, and the reference model (no assembly)
+    st, blobs = _oracle_outputs(data)
+    lens = np.array([len(b) for b in blobs], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    blob = b"".join(blobs)
+    with pytest.raises(avr.AvrError):
+        avr.assemble_container(data, st, blob[:-1], offs, lens)
+    with pytest.raises(avr.AvrError):
+        avr.assemble_container(data, st, blob, offs, lens, model=avr.MODEL_REFERENCE)
+
+
+def test_container_model_of_each_format():
+    from _oracle import oracle_cli
+    for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL), ("P32", avr.MODEL_PARALLEL32)):
+        assert avr.container_model(oracle_cli("compress", FIX / "realshort.mp4", mode=mode)) == model
+    with pytest.raises(avr.AvrError):
+        avr.container_model(b"\x0a\x10\x0a\x0eavrecode-amd:P")   # the round-2 format: refused
+    assert avr.container_model(b"\x0a\x0c\x0a\x0aother:tag1") == avr.MODEL_REFERENCE   # a foreign tag
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
@@ -189,6 +215,9 @@ def test_plan_and_splice_restore_the_file(name):
     lens2 = np.array([len(p) for p in short], np.uint32)
     offs2 = np.concatenate([[0], np.cumsum(lens2)[:-1]]).astype(np.uint64)
     assert avr.splice_container(avrc, st, b"".join(short), offs2, lens2) == data
+    # a slice's bytes past the end of the gathered buffer are refused, not read
+    with pytest.raises(avr.AvrError):
+        avr.splice_container(avrc, st, b"".join(pays)[:-1], offs, lens)
     st[len(st) // 2] = -9
     with pytest.raises(avr.AvrError):
         avr.splice_container(avrc, st, b"".join(pays), offs, lens)

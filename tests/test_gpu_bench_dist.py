@@ -1,0 +1,53 @@
+"""bench.py's N > 1 code paths, executed before the driver's multi-GPU run meets them.
+
+`python -m torch.distributed.run --nproc-per-node 2 bench.py --gpus 2 ...` exactly as the driver
+launches it, at tiny sizes, with the collectives on gloo (AVR_DIST_BACKEND=gloo: both ranks share
+this box's one GPU, and RCCL will not put two ranks on one device):
+* the default mode: every rank's weak-scaling batch (headline), the max-over-ranks reduction, the
+  corpus dealt over the ranks (corpus_sharded);
+* --stream-shard (BASELINE configs[3]): the stream cut over the ranks, the gather to rank 0 and its
+  container assembly.
+Each run must print one JSON line with n_gpus 2 and bit_exact true.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from _oracle import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_two_ranks(extra):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, AVR_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2"] + extra
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_default_mode_two_ranks():
+    line = _run_two_ranks(["--steps", "1", "--warmup", "1", "--slices", "8", "--mb-width", "40", "--mb-height", "24",
+                           "--corpus-scale", "0.05"])
+    assert line["n_gpus"] == 2 and line["bit_exact"] is True
+    assert line["scaling"] == "weak" and line["value"] > 0
+    assert line["corpus"]["n_gpus"] == 2
+    assert line["corpus"]["R"]["bit_exact"] is True and line["corpus"]["P"]["bit_exact"] is True
+
+
+def test_bench_stream_shard_two_ranks():
+    line = _run_two_ranks(["--stream-shard", "--stream-seconds", "1", "--stream-mb", "20", "12", "--steps", "1",
+                           "--warmup", "1"])
+    assert line["n_gpus"] == 2 and line["bit_exact"] is True
+    assert line["scaling"] == "strong" and line["config"]["slices"] == 30
+    assert set(line["config"]["step_phases_s_rank0"]) == {"kernels_s", "results_d2h_s", "gather_s", "assemble_s"}
