@@ -1650,6 +1650,25 @@ struct avr_hooks_slice {
   int coding_type = 0;
 };
 
+// Streaming compress session: incremental demux + parse of the bytes fed so far.  Only what is new
+// is parsed: an Annex-B NAL unit once the next start code (00 00 00 / 00 00 01, demux_annexb's rule)
+// has been fed -- the unit in progress provisionally when a decoder already asks for its slice (a
+// later feed that extends it fails the session) -- and an MP4 sample once the moov box and the
+// whole sample are in.  Slices come out in decode order exactly as parse_file gives them.
+struct StreamIngest {
+  avr::StreamParser sp;
+  int kind = 0;                 // 0 undecided (< 8 bytes), 1 Annex-B, 2 MP4
+  // Annex-B
+  size_t scan = 0;              // where the search for the next boundary / start code resumes
+  bool in_nal = false;          // a NAL unit started at nal_begin (after its start code)
+  size_t nal_begin = 0;
+  size_t prov_end = 0;          // the unit in progress was parsed provisionally through here (0: not)
+  // MP4
+  bool have_layout = false;
+  avr::Mp4Layout layout;
+  size_t next_sample = 0;
+};
+
 struct avr_hooks_session {
   avr_ctx* c = nullptr;
   bool decompress = false;
@@ -1671,9 +1690,15 @@ struct avr_hooks_session {
   bool fs_have = false, fs_pending = false;
   int fs_num = 0, fs_w = 0, fs_h = 0, fs_slice = -1;
   int pend_num = 0, pend_w = 0, pend_h = 0;
-  // streaming compress (avr_hooks_compress_stream_begin): `original` grows by avr_hooks_feed; pf is
-  // the parse of the bytes fed so far, redone at an init_decoder after a feed (dirty)
-  bool streaming = false, dirty = false;
+  // streaming compress (avr_hooks_compress_stream_begin): `original` grows by avr_hooks_feed; pf holds
+  // the slices parsed from it so far (ing: incremental), traced[i] = slice i's device work is done --
+  // its bin trace and, for the parallel model, its final re-coded block (blocks / block_status: the
+  // container is assembled from them at avr_hooks_end without another device pass)
+  bool streaming = false;
+  StreamIngest ing;
+  std::vector<char> traced;
+  std::vector<std::vector<uint8_t>> blocks;
+  std::vector<int32_t> block_status;
   int model = 0;
   std::string err;
   void fail_once(const std::string& m) {
@@ -1770,18 +1795,143 @@ int run_traces(avr_hooks_session* hs) {
   return trace_slices(hs, which);
 }
 
-// Streaming session: parse the bytes fed so far.  Slice indices are stable (a longer prefix only
-// adds slices or completes the last one); per-slice state grows with the parse.
-int stream_reparse(avr_hooks_session* hs) {
-  ParsedFile pf;
-  if (int r = parse_file(hs->c, hs->original.data(), hs->original.size(), &pf)) return r;
-  hs->pf = std::move(pf);
+// Streaming session: one NAL unit of the fed bytes through the stream parser (a slice joins pf).
+void ingest_nal(avr_hooks_session* hs, size_t off, size_t size) {
+  avr::SliceInfo si;
+  if (!hs->ing.sp.next(hs->original.data() + off, size, &si)) return;
+  si.nal_offset = off;
+  si.nal_size = size;
+  hs->pf.slices.push_back(std::move(si));
+}
+
+// Parse what the fed bytes newly complete.  final: the stream has ended (avr_hooks_end: the unit in
+// progress ends with it).  want: the number of slices a decoder needs now -- when the complete units
+// do not reach it, the Annex-B unit in progress is taken provisionally.
+int ingest(avr_hooks_session* hs, bool final, size_t want) {
+  StreamIngest& g = hs->ing;
+  const uint8_t* f = hs->original.data();
+  const size_t n = hs->original.size();
+  if (!g.kind) {
+    if (n < 8 && !final) return AVR_OK;
+    g.kind = avr::is_mp4(f, n) ? 2 : 1;
+  }
+  if (g.kind == 2) {
+    if (!g.have_layout) {
+      const int r = avr::mp4_layout(f, n, &g.layout);
+      if (r < 0 || (r == 0 && final)) return fail(hs->c, AVR_ERR_FORMAT, "hooks: not an MP4/avcC H.264 stream");
+      if (r == 0) return AVR_OK;   // the moov box is not in yet (a moov-last file: not before the end)
+      g.have_layout = true;
+      for (const avr::NalRef& nr : g.layout.param_sets) ingest_nal(hs, nr.offset, nr.size);
+    }
+    std::vector<avr::NalRef> nals;
+    for (; g.next_sample < g.layout.samples.size(); g.next_sample++) {
+      const avr::NalRef& smp = g.layout.samples[g.next_sample];
+      if (smp.offset > n || smp.size > n - smp.offset) {
+        if (final) return fail(hs->c, AVR_ERR_FORMAT, "hooks: an MP4 sample lies past the end of the stream");
+        break;   // not complete yet
+      }
+      nals.clear();
+      avr::mp4_sample_nals(f, smp, g.layout.len_size, &nals);
+      for (const avr::NalRef& nr : nals) ingest_nal(hs, nr.offset, nr.size);
+    }
+    return AVR_OK;
+  }
+  // Annex-B (demux_annexb's rules, resumed where the last call stopped)
+  auto is_sc = [&](size_t j) { return j + 3 <= n && f[j] == 0 && f[j + 1] == 0 && f[j + 2] == 1; };
+  auto unit_end = [&](size_t begin, size_t end) {   // trailing zero bytes belong to the next start code
+    while (end > begin && f[end - 1] == 0) end--;
+    return end;
+  };
+  for (;;) {
+    if (!g.in_nal) {
+      size_t i = g.scan;
+      while (i + 3 <= n && !is_sc(i)) i++;
+      if (i + 3 > n) {
+        g.scan = i;
+        break;
+      }
+      g.in_nal = true;
+      g.nal_begin = g.scan = i + 3;
+    }
+    size_t j = g.scan;
+    while (j + 3 <= n && !(f[j] == 0 && f[j + 1] == 0 && (f[j + 2] == 1 || f[j + 2] == 0))) j++;
+    if (j + 3 > n) {
+      g.scan = j;
+      break;
+    }
+    // the unit in progress is complete: [nal_begin, j) without trailing zeros
+    const size_t end = unit_end(g.nal_begin, j);
+    if (g.prov_end) {
+      if (end != g.prov_end)
+        return fail(hs->c, AVR_ERR_FORMAT, "hooks: a slice was decoded before its NAL unit was complete");
+      g.prov_end = 0;
+    } else if (end > g.nal_begin) {
+      ingest_nal(hs, g.nal_begin, end - g.nal_begin);
+    }
+    g.in_nal = false;
+    g.scan = j;
+  }
+  // the unit in progress: at the end of the stream it is complete; before it, it is parsed
+  // provisionally when the decoder needs a slice the complete units do not hold
+  if (g.in_nal && (final || hs->pf.slices.size() < want)) {
+    const size_t end = unit_end(g.nal_begin, n);
+    if (g.prov_end && end != g.prov_end)
+      return fail(hs->c, AVR_ERR_FORMAT, "hooks: a slice was decoded before its NAL unit was complete");
+    if (!g.prov_end && end > g.nal_begin) {
+      ingest_nal(hs, g.nal_begin, end - g.nal_begin);
+      g.prov_end = end;
+    }
+    if (final) g.in_nal = false, g.prov_end = 0;
+  }
+  return AVR_OK;
+}
+
+// Per-slice state for the slices parsed so far.
+void grow_session(avr_hooks_session* hs) {
   const size_t n = hs->pf.slices.size();
   hs->coded.resize(n, 0);
   hs->bins.resize(n);
   hs->maps.resize(n);
   hs->slices.resize(n);   // no slice object is live here (init_decoder closed it first)
-  hs->dirty = false;
+  hs->traced.resize(n, 0);
+  hs->blocks.resize(n);
+  hs->block_status.resize(n, AVR_SLICE_NO_ROUNDTRIP);
+}
+
+// Streaming session: the device work of slice i and of every parsed slice after it not done yet
+// (trace-ahead: the slices a feed completed go to the device together) -- their decode-order bin
+// traces, and for the parallel model their final re-coded blocks (compress + the per-slice device
+// roundtrip check, as avr_compress_file runs it).
+int stream_device_work(avr_hooks_session* hs, size_t i) {
+  std::vector<int> which;
+  for (size_t k = i; k < hs->pf.slices.size(); k++)
+    if (!hs->traced[k]) {
+      hs->traced[k] = 1;
+      if (recodable_candidate(hs->pf.slices[k])) which.push_back((int)k);
+    }
+  if (which.empty()) return AVR_OK;
+  if (int r = trace_slices(hs, which)) return r;
+  if (!parallel_model(hs->model)) return AVR_OK;
+  Plan plan;
+  for (const int k : which) {
+    const avr::SliceInfo& s = hs->pf.slices[k];
+    avr_slice_desc d = desc_from_header(s);
+    append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
+    d.payload_size = (uint32_t)s.size;
+    d.read_limit = (uint32_t)s.read_limit;
+    d.out_capacity = (uint32_t)(s.size * 2 + 256);
+    plan.max_w = std::max(plan.max_w, ring_cols(d));
+    plan.descs.push_back(d);
+  }
+  std::vector<avr_slice_result> res;
+  std::vector<uint8_t> outb;
+  if (int r = run_plan(hs->c, 0, false, plan, &res, &outb, /*verify=*/true, coder_flag(hs->model))) return r;
+  for (size_t q = 0; q < which.size(); q++) {
+    const int k = which[q];
+    hs->block_status[k] = res[q].status;
+    if (res[q].status == 0)
+      hs->blocks[k].assign(outb.begin() + plan.descs[q].out_offset, outb.begin() + plan.descs[q].out_offset + res[q].out_len);
+  }
   return AVR_OK;
 }
 
@@ -1812,10 +1962,15 @@ void close_live(avr_hooks_session* hs) {
     hs->fail_once("hooks: slice " + std::to_string(h->index) + " was decoded without a frame_spec for its picture");
 }
 
-// frame_spec of slice i: the model's frames (update_frame_spec, recode.cpp:824-843) must turn over
-// exactly where the device's pictures do -- frame_num (or the size) changes between two calls iff
-// the slices belong to different pictures (the device's decode-order picture counter, which the
-// two fields of a frame share, as they share frame_num) -- and the size must be the picture's.
+// frame_spec of slice i: the model's frames (update_frame_spec, recode.cpp:824-843) turn over where
+// the device's pictures do (its decode-order picture counter, which the two fields of a frame
+// share, as they share frame_num), and the size must be the picture's.  A caller that starts a new
+// frame inside one of the device's pictures is refused.  A caller whose frame_num stays the same
+// while the device starts a new picture is accepted only where the two pictures' slice headers
+// carry the same frame_num: the fork passes that syntax element, and consecutive pictures share it
+// after a non-reference picture (e.g. B(frame_num 4, nal_ref_idc 0) then P(4)) -- the model keeps
+// its per-picture frames there (frame_spec takes a picture counter).  Any other
+// repeat is a caller whose frames differ from the pictures it decodes.
 void check_frame_spec(avr_hooks_session* hs, int i, int frame_num, int w, int h) {
   const avr::SliceInfo& s = hs->pf.slices[i];
   const std::string where = "hooks: slice " + std::to_string(i) + ": frame_spec(" + std::to_string(frame_num) + ", " +
@@ -1829,7 +1984,8 @@ void check_frame_spec(avr_hooks_session* hs, int i, int frame_num, int w, int h)
     const avr::SliceInfo& p = hs->pf.slices[hs->fs_slice];
     const bool caller_new = frame_num != hs->fs_num || w != hs->fs_w || h != hs->fs_h;
     const bool device_new = s.picture_id != p.picture_id || w != hs->fs_w || h != hs->fs_h;
-    if (caller_new != device_new)
+    const bool syntax_repeat = !caller_new && device_new && s.h.frame_num == p.h.frame_num;
+    if (caller_new != device_new && !syntax_repeat)
       hs->fail_once(where + (device_new ? " keeps the frame of slice " : " starts a new frame after slice ") +
                     std::to_string(hs->fs_slice) + ", the device's parse " +
                     (device_new ? "starts a new picture" : "stays in the same picture"));
@@ -1924,7 +2080,6 @@ int avr_hooks_feed(avr_hooks_session* hs, const uint8_t* bytes, size_t n) {
   } catch (const std::bad_alloc&) {
     return AVR_ERR_OUT_OF_MEMORY;
   }
-  if (n) hs->dirty = true;
   return AVR_OK;
 }
 
@@ -1932,10 +2087,15 @@ void* avr_hook_init_decoder(void* opaque, void* /*cabac_context*/, const uint8_t
   avr_hooks_session* hs = (avr_hooks_session*)opaque;
   if (!hs) return nullptr;
   close_live(hs);
-  if (hs->streaming && (hs->dirty || hs->next_slice >= hs->pf.slices.size())) {
+  if (hs->streaming) {
     // the slice the decoder starts is in the bytes its demuxer has read (read_packet feeds them
-    // before the packet is decoded): parse them, then trace this slice alone on the device
-    if (int r = stream_reparse(hs)) {
+    // before the packet is decoded): parse what is new
+    int r = guarded(hs->c, [&] {
+      const int e = ingest(hs, false, hs->next_slice + 1);
+      grow_session(hs);
+      return e;
+    });
+    if (r) {
       hs->fail_once("hooks: the bytes fed so far do not parse (" + std::to_string(r) + "): " + hs->c->err);
       hs->next_slice++;
       return nullptr;
@@ -1959,7 +2119,7 @@ void* avr_hook_init_decoder(void* opaque, void* /*cabac_context*/, const uint8_t
     // find_next_coded_block (recode.cpp:1139-1145, 1275-1297) on the slice's own bytes: a slice the
     // device can re-code gets hooks; the container (avr_hooks_end) may still store it skip_coded
     hs->coded[i] = memcmp(buf, s.payload(), s.size) == 0 && recodable_candidate(s) ? 1 : 0;
-    if (hs->coded[i] && trace_slices(hs, {(int)i}) != AVR_OK) {
+    if (hs->coded[i] && guarded(hs->c, [&] { return stream_device_work(hs, i); }) != AVR_OK) {
       hs->fail_once("hooks: device trace of slice " + std::to_string(i) + " failed: " + hs->c->err);
       return nullptr;
     }
@@ -2118,16 +2278,38 @@ int avr_hooks_end(avr_hooks_session* hs, uint8_t** out, size_t* out_len) {
   if (!hs || !out || !out_len) return AVR_ERR_INVALID_ARGUMENT;
   close_live(hs);
   if (hs->streaming) {
-    // the whole file is in: its slice count, and the container (the model runs over every slice,
-    // recode.cpp:1102-1125)
-    if (hs->dirty || hs->pf.slices.empty()) {
-      if (int r = stream_reparse(hs)) return r;
-    }
+    // the whole file is in: its last slices, and the container (recode.cpp:1102-1125).  The
+    // parallel model's blocks are final as each slice was traced (slices independent): the container
+    // is assembled from them.  The reference model's estimators chain across slices, so its
+    // container comes from one compress of the whole file.
+    if (int r = guarded(hs->c, [&] {
+          const int e = ingest(hs, true, 0);
+          grow_session(hs);
+          if (!e && hs->err.empty() && parallel_model(hs->model)) return stream_device_work(hs, 0);
+          return e;
+        }))
+      return r;
     if (hs->err.empty()) {
       uint8_t* avrc = nullptr;
       size_t avrc_len = 0;
-      if (int r = avr_compress_file(hs->c, hs->original.data(), hs->original.size(), hs->model, &avrc, &avrc_len))
+      if (parallel_model(hs->model)) {
+        if (int r = guarded(hs->c, [&] {
+              std::vector<char> ok(hs->pf.slices.size(), 0);
+              std::vector<std::pair<const uint8_t*, size_t>> blobs(hs->pf.slices.size(), {nullptr, 0});
+              for (size_t i = 0; i < ok.size(); i++) {
+                ok[i] = recodable_candidate(hs->pf.slices[i]) && hs->block_status[i] == 0;
+                blobs[i] = {hs->blocks[i].data(), hs->blocks[i].size()};
+              }
+              const std::vector<SliceView> sv = views_of(hs->pf);
+              return emit_container(hs->original.data(), hs->original.size(), sv,
+                                    segment(hs->original.data(), hs->original.size(), sv, ok), blobs, hs->model,
+                                    &avrc, &avrc_len);
+            }))
+          return r;
+      } else if (int r = avr_compress_file(hs->c, hs->original.data(), hs->original.size(), hs->model, &avrc,
+                                           &avrc_len)) {
         return r;
+      }
       hs->result.assign(avrc, avrc + avrc_len);
       free(avrc);
     }
@@ -2144,3 +2326,40 @@ int avr_hooks_end(avr_hooks_session* hs, uint8_t** out, size_t* out_len) {
 }
 
 void avr_hooks_destroy(avr_hooks_session* hs) { delete hs; }
+
+// Debug (tests, host only; not part of include/avrecode.h): the slices a streaming session's
+// incremental parser finds when `file` is fed in pieces ending at cuts[0] < ... < cuts[ncuts - 1] = n
+// (incremental = 1; after each piece the parser is asked for one slice more than it holds when
+// provisional = 1, as a decoder's next init_decoder would), or that parse_file finds in the whole
+// file (incremental = 0).  out: 4 u64 per slice (NAL offset, NAL size, payload size, picture id).
+// Returns the slice count (at most cap written), or < 0.
+extern "C" int avr_debug_stream_slices(const uint8_t* file, size_t n, const uint64_t* cuts, int ncuts, int incremental,
+                                       int provisional, uint64_t* out, int cap) {
+  if (!file || (incremental && (!cuts || ncuts <= 0)) || (!out && cap)) return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(nullptr, [&]() -> int {
+    avr_hooks_session hs;
+    hs.streaming = true;
+    if (incremental) {
+      size_t fed = 0;
+      for (int k = 0; k < ncuts; k++) {
+        const size_t end = std::min<size_t>(n, cuts[k]);
+        if (end > fed) hs.original.insert(hs.original.end(), file + fed, file + end);
+        fed = std::max(fed, end);
+        if (int r = ingest(&hs, false, 0)) return r;
+        if (provisional)
+          if (int r = ingest(&hs, false, hs.pf.slices.size() + 1)) return r;
+      }
+      if (fed < n) hs.original.insert(hs.original.end(), file + fed, file + n);
+      if (int r = ingest(&hs, true, 0)) return r;
+    } else if (int r = parse_file(nullptr, file, n, &hs.pf)) {
+      return r;
+    }
+    const int cnt = (int)hs.pf.slices.size();
+    for (int i = 0; i < cnt && i < cap; i++) {
+      const avr::SliceInfo& si = hs.pf.slices[i];
+      out[4 * i] = si.nal_offset, out[4 * i + 1] = si.nal_size, out[4 * i + 2] = si.size;
+      out[4 * i + 3] = (uint64_t)si.picture_id;
+    }
+    return cnt;
+  });
+}

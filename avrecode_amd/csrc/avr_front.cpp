@@ -390,12 +390,16 @@ void walk_track(const uint8_t* f, size_t off, size_t lim, Track* t, int depth) {
   }
 }
 
-bool demux_mp4(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
+}  // namespace
+
+int mp4_layout(const uint8_t* f, size_t n, Mp4Layout* L) {
+  *L = Mp4Layout();
   Track video;
-  bool found = false;
+  bool found = false, moov = false;
   Box b;
   for (size_t off = 0; read_box(f, off, n, &b); off = b.end) {
     if (b.type != fourcc("moov")) continue;
+    moov = true;
     Box tb;
     for (size_t c = b.body; read_box(f, c, b.end, &tb); c = tb.end) {
       if (tb.type != fourcc("trak")) continue;
@@ -404,9 +408,10 @@ bool demux_mp4(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
       if (t.video && t.avcc && !found) video = t, found = true;
     }
   }
-  if (!found || !video.stsz || !video.stco || !video.stsc || video.avcc_len < 7) return false;
+  if (!moov) return 0;   // not within [0, n) (yet)
+  if (!found || !video.stsz || !video.stco || !video.stsc || video.avcc_len < 7) return -1;
   const uint8_t* a = f + video.avcc;
-  const int len_size = (a[4] & 3) + 1;
+  L->len_size = (a[4] & 3) + 1;
   size_t p = 5;
   for (int pass = 0; pass < 2; pass++) {
     if (p >= video.avcc_len) break;
@@ -414,39 +419,56 @@ bool demux_mp4(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
     for (int i = 0; i < cnt && p + 2 <= video.avcc_len; i++) {
       size_t l = (size_t)a[p] << 8 | a[p + 1];
       p += 2;
-      if (p + l > video.avcc_len) return false;
-      nals->push_back({video.avcc + p, l});
+      if (p + l > video.avcc_len) return -1;
+      L->param_sets.push_back({video.avcc + p, l});
       p += l;
     }
   }
-  if (video.stsz_len < 12 || video.stco_len < 8 || video.stsc_len < 8) return false;
+  if (video.stsz_len < 12 || video.stco_len < 8 || video.stsc_len < 8) return -1;
   const uint8_t *stsz = f + video.stsz, *stco = f + video.stco, *stsc = f + video.stsc;
   const uint32_t fixed = rd32(stsz + 4), nsamples = rd32(stsz + 8), nchunks = rd32(stco + 4), nstsc = rd32(stsc + 4);
-  if (!fixed && 12 + 4ull * nsamples > video.stsz_len) return false;
-  if (8 + (video.co64 ? 8ull : 4ull) * nchunks > video.stco_len || 8 + 12ull * nstsc > video.stsc_len) return false;
+  if (!fixed && 12 + 4ull * nsamples > video.stsz_len) return -1;
+  if (8 + (video.co64 ? 8ull : 4ull) * nchunks > video.stco_len || 8 + 12ull * nstsc > video.stsc_len) return -1;
   uint32_t sample = 0;
   for (uint32_t e = 0; e < nstsc && sample < nsamples; e++) {
     const uint32_t first = rd32(stsc + 8 + 12 * e), per = rd32(stsc + 12 + 12 * e);
     const uint32_t next_first = e + 1 < nstsc ? rd32(stsc + 8 + 12 * (e + 1)) : nchunks + 1;
     // chunk numbers are 1-based and increase from entry to entry (ISO/IEC 14496-12 8.7.4)
-    if (first == 0 || next_first <= first) return false;
+    if (first == 0 || next_first <= first) return -1;
     const uint32_t last = next_first - 1;
     for (uint32_t c = first; c <= last && c <= nchunks && sample < nsamples; c++) {
       size_t coff = video.co64 ? (size_t)rd64(stco + 8 + 8 * (c - 1)) : rd32(stco + 8 + 4 * (c - 1));
       for (uint32_t s = 0; s < per && sample < nsamples; s++, sample++) {
         size_t ssz = fixed ? fixed : rd32(stsz + 12 + 4 * sample);
-        if (coff > n || ssz > n - coff) return false;
-        for (size_t q = coff, qe = coff + ssz; q + (size_t)len_size <= qe;) {
-          size_t l = 0;
-          for (int k = 0; k < len_size; k++) l = l << 8 | f[q + k];
-          q += (size_t)len_size;
-          if (!l || q + l > qe) break;
-          nals->push_back({q, l});
-          q += l;
-        }
+        if (coff > SIZE_MAX / 2 || ssz > SIZE_MAX / 2) return -1;
+        L->samples.push_back({coff, ssz});
         coff += ssz;
       }
     }
+  }
+  return 1;
+}
+
+void mp4_sample_nals(const uint8_t* f, const NalRef& smp, int len_size, std::vector<NalRef>* nals) {
+  for (size_t q = smp.offset, qe = smp.offset + smp.size; q + (size_t)len_size <= qe;) {
+    size_t l = 0;
+    for (int k = 0; k < len_size; k++) l = l << 8 | f[q + k];
+    q += (size_t)len_size;
+    if (!l || q + l > qe) break;
+    nals->push_back({q, l});
+    q += l;
+  }
+}
+
+namespace {
+
+bool demux_mp4(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
+  Mp4Layout L;
+  if (mp4_layout(f, n, &L) != 1) return false;
+  *nals = L.param_sets;
+  for (const NalRef& smp : L.samples) {
+    if (smp.offset > n || smp.size > n - smp.offset) return false;
+    mp4_sample_nals(f, smp, L.len_size, nals);
   }
   return true;
 }
@@ -468,11 +490,14 @@ void demux_annexb(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
 
 }  // namespace
 
+bool is_mp4(const uint8_t* file, size_t n) {
+  return n >= 8 && (rd32(file + 4) == fourcc("ftyp") || rd32(file + 4) == fourcc("moov") ||
+                    rd32(file + 4) == fourcc("mdat") || rd32(file + 4) == fourcc("free"));
+}
+
 bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals) {
   nals->clear();
-  const bool mp4 = n >= 8 && (rd32(file + 4) == fourcc("ftyp") || rd32(file + 4) == fourcc("moov") ||
-                              rd32(file + 4) == fourcc("mdat") || rd32(file + 4) == fourcc("free"));
-  if (mp4) return demux_mp4(file, n, nals) && !nals->empty();
+  if (is_mp4(file, n)) return demux_mp4(file, n, nals) && !nals->empty();
   demux_annexb(file, n, nals);
   return !nals->empty();   // nothing H.264 in it: av_decoder::run throws (recode.cpp:92-93)
 }

@@ -48,6 +48,18 @@ struct NalRef {
 
 // MP4 (avcC) or Annex-B; returns false on a malformed container.
 bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals);
+bool is_mp4(const uint8_t* file, size_t n);
+// The video track's layout in an MP4 file: the avcC parameter sets and every sample's (offset,
+// size) in decode order, from the moov box's sample tables -- what the mov demuxer knows before
+// its first packet.  Returns 1, 0 when no complete moov box lies within [0, n) (a prefix of a
+// moov-last file), -1 for a malformed one.  Samples may lie past n (a moov-first file's prefix).
+struct Mp4Layout {
+  std::vector<NalRef> param_sets, samples;
+  int len_size = 4;
+};
+int mp4_layout(const uint8_t* file, size_t n, Mp4Layout* layout);
+// the length-prefixed NAL units of one sample
+void mp4_sample_nals(const uint8_t* file, const NalRef& sample, int len_size, std::vector<NalRef>* nals);
 
 // Stateful walk over a NAL sequence (parameter sets, x264 SEI, picture boundaries).
 class StreamParser {

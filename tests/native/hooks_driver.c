@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/avrecode.h"
 #include "../../oracle/avr_oracle.h"
@@ -22,6 +23,11 @@
  *   3  the k-th mb_xy reports x ^ 1
  *   4  the k-th begin_sub_mb / end_sub_mb pair reports scan8 index ^ 1 */
 static int g_perturb, g_k;
+/* frame_spec's first argument: the driver's decode-order picture counter (default), or the slice
+ * header's frame_num as the fork passes it (hooks_set_frame_num_syntax(1)), which consecutive
+ * pictures share after a non-reference picture */
+static int g_syntax_fn;
+void hooks_set_frame_num_syntax(int on) { g_syntax_fn = on; }
 static long g_maps, g_mbs, g_subs, g_sub_bad;
 static int g_delayed;   /* a begin_coding_type(SIG_MAP) waiting for the next bin */
 static void *g_session;
@@ -29,9 +35,29 @@ static void *g_session;
  * before each slice's init_decoder the driver feeds through the end of that slice's NAL unit, in two
  * pieces, as a demuxer's read_packet would (recode.cpp:1127-1131) */
 static const uint8_t *g_file;
-static size_t g_fed;
+static size_t g_fed, g_file_len;
 static int g_feed_err;
+/* hooks_set_feed_chunk(k): the demuxer reads fixed k-byte pieces (the last one shorter), so a
+ * slice's bytes arrive with whatever follows them in its piece (0: exactly through the NAL unit) */
+static size_t g_chunk;
+void hooks_set_feed_chunk(size_t k) { g_chunk = k; }
+/* per-slice wall time of the last drive() (feed + init_decoder + the slice's walk), seconds */
+static double *g_times;
+static long g_ntimes, g_captimes;
+int hooks_slice_times(double *out, int cap) {
+  for (long i = 0; i < g_ntimes && i < cap; i++) out[i] = g_times[i];
+  return (int)g_ntimes;
+}
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + t.tv_nsec * 1e-9;
+}
 static void feed_to(size_t end) {
+  if (g_file && g_chunk) {
+    end = (end + g_chunk - 1) / g_chunk * g_chunk;
+    if (end > g_file_len) end = g_file_len;
+  }
   if (!g_file || end <= g_fed) return;
   size_t mid = g_fed + (end - g_fed) / 2;
   if (avr_hooks_feed((avr_hooks_session *)g_session, g_file + g_fed, mid - g_fed) != AVR_OK) g_feed_err = 1;
@@ -94,6 +120,7 @@ static long drive(const uint8_t *stream, size_t n) {
   avr_slice_hdr_t prev;
   long walked = 0;
   memset(&prev, 0, sizeof(prev));
+  g_ntimes = 0;
   for (int i = 0; i < nn; i++) {
     const uint8_t *nal = stream + nals[i].offset;
     size_t len = nals[i].size;
@@ -127,7 +154,8 @@ static long drive(const uint8_t *stream, size_t n) {
     size_t bits = avr_rbsp_bit_length(rbsp, rl);
     size_t end = (bits + 7) / 8;
     size_t size = end > h.cabac_start ? end - h.cabac_start : 0;
-    m_frame_spec(NULL, picture_id, h.mb_width, h.mb_height);
+    const double t0 = now_s();
+    m_frame_spec(NULL, g_syntax_fn ? h.frame_num : picture_id, h.mb_width, h.mb_height);
     feed_to(nals[i].offset + nals[i].size);
     void *slice = avr_hook_init_decoder(g_session, NULL, rbsp + h.cabac_start, (int)size);
     if (slice) {
@@ -136,6 +164,11 @@ static long drive(const uint8_t *stream, size_t n) {
       if (avr_walk_slice(&h, &hk, picture_id) != 0) { free(rbsp); walked = -2; break; }
       walked++;
     }
+    if (g_ntimes == g_captimes) {
+      g_captimes = g_captimes ? 2 * g_captimes : 1024;
+      g_times = (double *)realloc(g_times, sizeof(double) * (size_t)g_captimes);
+    }
+    g_times[g_ntimes++] = now_s() - t0;
     free(rbsp);
   }
   free(ps);
@@ -171,11 +204,23 @@ int hooks_compress_stream(const uint8_t *file, size_t n, int model, uint8_t **ou
   if (r) { avr_destroy(c); return r; }
   g_session = s;
   g_file = file;
+  g_file_len = n;
   g_fed = 0;
   g_feed_err = 0;
   /* MP4 read through a non-seekable read_packet (recode.cpp:84-90): the mov demuxer reads up to
-   * the moov box before the first packet -- for moov-last files, the whole file */
-  if (n >= 8 && memcmp(file + 4, "ftyp", 4) == 0) feed_to(n);
+   * the moov box before the first packet -- for moov-last files, the whole file; a moov-first
+   * ("faststart") file then streams sample by sample */
+  if (n >= 8 && memcmp(file + 4, "ftyp", 4) == 0) {
+    size_t off = 0, moov_end = n;
+    while (off + 8 <= n) {
+      size_t sz = (size_t)file[off] << 24 | (size_t)file[off + 1] << 16 | (size_t)file[off + 2] << 8 | file[off + 3];
+      if (sz < 8 || sz > n - off) break;
+      if (!memcmp(file + off + 4, "moov", 4)) { moov_end = off + sz; break; }
+      if (!memcmp(file + off + 4, "mdat", 4)) break;   /* media first: the moov box is last */
+      off += sz;
+    }
+    feed_to(moov_end);
+  }
   *walked = drive(file, n);
   feed_to(n);
   g_file = NULL;

@@ -157,3 +157,87 @@ def test_hooks_reject_misplaced_model_events(mode, k, what):
     assert r == -3, (what, r)
     r, avrc, _ = _call("hooks_compress", data, len(data), 1)   # unperturbed: accepted
     assert r == 0 and hashlib.sha256(avrc).hexdigest() == GOLD[("realshort.mp4", "P")]["avrc_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,model", [("R", 0), ("P", 1)])
+def test_hooks_accept_slice_header_frame_num(mode, model):
+    """A caller that passes frame_spec the slice header's frame_num, as the fork does: cockatoo.mp4
+    has B pictures with nal_ref_idc 0, after which two consecutive pictures share frame_num (B 4, P 4;
+    B 5, P 5; ...).  The session accepts that repeat (the device's pictures still turn the model's
+    frames over) and gives the pinned container; a repeat where the headers' frame_num
+    differ stays refused (test_hooks_reject_misplaced_model_events, perturbation 2)."""
+    L, _ = _driver()
+    L.hooks_set_frame_num_syntax.argtypes = [ctypes.c_int]
+    data = (FIX / "cockatoo.mp4").read_bytes()
+    try:
+        L.hooks_set_frame_num_syntax(1)
+        r, avrc, walked = _call("hooks_compress", data, len(data), model)
+    finally:
+        L.hooks_set_frame_num_syntax(0)
+    assert r == 0, r
+    assert hashlib.sha256(avrc).hexdigest() == GOLD[("cockatoo.mp4", mode)]["avrc_sha256"]
+
+
+def _stream_with(fn, data, model, chunk):
+    L, _ = _driver()
+    L.hooks_set_feed_chunk.argtypes = [ctypes.c_size_t]
+    try:
+        L.hooks_set_feed_chunk(chunk)
+        return _call(fn, data, len(data), model)
+    finally:
+        L.hooks_set_feed_chunk(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [4096, 32768])
+@pytest.mark.parametrize("name", ["paff_ipp.264", "mbaff_ib.264", "realshort_faststart.mp4"])
+def test_hooks_streaming_fixed_size_reads(name, chunk):
+    """A streaming session fed in fixed-size reads (read_packet's buffer, not NAL boundaries), for
+    Annex-B streams and a moov-first MP4 (its samples stream after the moov box): the
+    container equals the oracle's for the same file, parallel model."""
+    import tempfile
+    from pathlib import Path
+    from _oracle import oracle_cli
+    from test_stream_ingest import INPUTS
+    data = INPUTS[name]
+    r, avrc, walked = _stream_with("hooks_compress_stream", data, 1, chunk)
+    assert r == 0, r
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / name
+        f.write_bytes(data)
+        assert avrc == oracle_cli("compress", f, mode="P")
+    r, back, walked_d = _call("hooks_decompress", avrc, len(avrc))
+    assert r == 0 and back == data and walked_d == walked > 0
+
+
+@pytest.mark.gpu
+def test_hooks_streaming_1000_slices_flat():
+    """1,000 slices (a tiled IP stream of small pictures, Annex-B) through a streaming session fed
+    NAL unit by NAL unit: each init_decoder parses only the new unit and traces (and, parallel
+    model, codes) only the new slice, so the per-slice host time stays flat -- the median of the
+    last 100 slices within 1.5x of the first 100 (the whole-prefix re-parse grew linearly) -- and
+    the container equals the oracle's."""
+    import statistics
+    import tempfile
+    from pathlib import Path
+
+    import avrecode_amd as avr
+    from _oracle import oracle_cli
+    with avr.Context(0) as ctx:
+        data = ctx.synthesize(avr.SynthParams(mb_width=12, mb_height=8, slice_type=0, slice_qp=28, seed=77,
+                                              gop_length=25, repeat=40), 25)
+    assert len(avr.parse_stream(data).descs) == 1000
+    r, avrc, walked = _stream_with("hooks_compress_stream", data, 1, 0)
+    assert r == 0 and walked == 1000, (r, walked)
+    L, _ = _driver()
+    L.hooks_slice_times.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int]
+    buf = (ctypes.c_double * 1000)()
+    assert L.hooks_slice_times(buf, 1000) == 1000
+    t = list(buf)
+    first, last = statistics.median(t[:100]), statistics.median(t[-100:])
+    assert last <= 1.5 * first, (first, last)
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / "s.264"
+        f.write_bytes(data)
+        assert avrc == oracle_cli("compress", f, mode="P")
