@@ -161,7 +161,8 @@ static long drive(const uint8_t *stream, size_t n) {
     if (slice) {
       avr_hooks_t hk = {slice, fwd_get, fwd_bypass, fwd_terminate, m_frame_spec, m_mb_xy,
                         m_begin_sub, m_end_sub, m_begin_ct, m_end_ct};
-      if (avr_walk_slice(&h, &hk, picture_id) != 0) { free(rbsp); walked = -2; break; }
+      /* the walker's own frame_spec call (the fork's, at the slice start) passes the same value */
+      if (avr_walk_slice(&h, &hk, g_syntax_fn ? h.frame_num : picture_id) != 0) { free(rbsp); walked = -2; break; }
       walked++;
     }
     if (g_ntimes == g_captimes) {
