@@ -290,6 +290,12 @@ AVR_FI void follow_prio(Shared* sh, uint32_t* cur) {
   }
 }
 
+AVR_FI uint64_t readlane64(uint64_t v, uint32_t j) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
+  return (uint64_t)hi << 32 | lo;
+}
+
 // v_writelane_b32 (clang has no builtin for it; the LLVM intrinsic by its name)
 extern "C" __device__ int avr_llvm_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
@@ -646,7 +652,7 @@ struct Walker {
     } else if (MODE == MODE_DECOMPRESS) {
       bins++;
       const uint32_t e = __builtin_amdgcn_readlane(rc_v, L);
-      const int b = rd_get(rd, in, p1(e));
+      const int b = rdec(e);
       rc_v = wlane(rc_v, L, est_update(e, b, 0x60));
       push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
       return b;
@@ -675,6 +681,41 @@ struct Walker {
       return __umulhi(rd.range, ((cu32*)G->hot.rcp32)[tot]) * pos;   // the P-format rule
     }
   }
+  // One decision of the model's coder with estimator e (recode.cpp:1435-1449).
+#ifdef AVR_EXP_VQ
+  // u64 coder: lane L holds floor(range / (L + kVqBase)) for the current range, computed on the
+  // vector unit right after each decision -- off the next decision's critical path, which then
+  // needs one v_readlane pair instead of a scalar load of the reciprocal and the 64-bit product.
+  // Totals below kVqBase (a fresh estimator's first uses) take the scalar path.
+  static constexpr uint32_t kVqBase = 34;
+  uint32_t vq_mlo, vq_mhi, vq_sh;   // lane L: HotTables::div[L + kVqBase]
+  uint64_t vq;                      // lane L: floor(range / (L + kVqBase))
+  AVR_FI void vq_init() {
+    const uint64_t* dv = &G->hot.div[__lane_id() + kVqBase][0];
+    vq_mlo = (uint32_t)dv[0];
+    vq_mhi = (uint32_t)(dv[0] >> 32);
+    vq_sh = (uint32_t)dv[1];
+    vq_update();
+  }
+  AVR_FI void vq_update() {
+    const uint64_t q = __umul64hi(rd.range, (uint64_t)vq_mhi << 32 | vq_mlo) >> vq_sh;
+    uint32_t lo = (uint32_t)q, hi = (uint32_t)(q >> 32);
+    asm volatile("" : "+v"(lo), "+v"(hi));   // computed here, right after the decision
+    vq = (uint64_t)hi << 32 | lo;
+  }
+  AVR_FI int rdec(uint32_t e) {
+    if constexpr (!P32) {
+      const uint32_t pos = (e & 0xff) + 1, tot = (e & 0xff) + (e >> 8) + 2;
+      const uint64_t r1 = tot >= kVqBase ? readlane64(vq, tot - kVqBase) * pos : p1(e);
+      const int b = rd_get(rd, in, r1);
+      vq_update();
+      return b;
+    }
+    return rd_get(rd, in, p1(e));
+  }
+#else
+  AVR_FI int rdec(uint32_t e) { return rd_get(rd, in, p1(e)); }
+#endif
   // CABAC state record of state byte s: VGPR table (two v_readlane) or, with AVR_CABAC_SMEM, a
   // scalar load
   AVR_FI CabacRec crec(uint32_t s) const {
@@ -756,7 +797,7 @@ struct Walker {
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = __builtin_amdgcn_readlane(mc_v, L);
-      const int b = rd_get(rd, in, p1(e));
+      const int b = rdec(e);
       mc_v = wlane(mc_v, L, est_update(e, b, 0x60));
       push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
       return b;
@@ -782,7 +823,7 @@ struct Walker {
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[ctx];
-      const int b = rd_get(rd, in, p1(e));
+      const int b = rdec(e);
       sh->est[ctx] = (uint16_t)est_update(e, b, 0x60);
       push((uint32_t)b | OPK_DECISION << 1 | (uint32_t)ctx << 3);
       return b;
@@ -801,7 +842,7 @@ struct Walker {
       return b;
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = byp_e;   // the bypass estimator lives in a scalar register
-      const int b = rd_get(rd, in, p1(e));
+      const int b = rdec(e);
       byp_e = est_update(e, b, 0x60);
       push((uint32_t)b | OPK_BYPASS << 1);
       return b;
@@ -824,7 +865,7 @@ struct Walker {
       }
     } else if (MODE == MODE_DECOMPRESS) {
       const uint32_t e = sh->est[1025];
-      b = rd_get(rd, in, p1(e));
+      b = rdec(e);
       sh->est[1025] = (uint16_t)est_update(e, b, 0x60);
       push((uint32_t)b | OPK_TERMINATE << 1);
     } else {
@@ -1147,7 +1188,7 @@ struct Walker {
         } else {
           e = est_load(sh, est_g, idx, &slot);
         }
-        const int b = rd_get(rd, in, p1(e));
+        const int b = rdec(e);
         est_store(sh, est_g, idx, slot, est_update(e, b, 0x60));
         so_far |= b << k;
       }
@@ -1167,7 +1208,7 @@ struct Walker {
       } else {
         uint32_t slot;
         const uint32_t e = est_load(sh, est_g, idx, &slot);
-        b = rd_get(rd, in, p1(e));
+        b = rdec(e);
         est_store(sh, est_g, idx, slot, est_update(e, b, 0x60));
       }
       if (b) so_far |= cur_bit;
@@ -1264,7 +1305,7 @@ struct Walker {
           const int idx = seb + (zo * stride + nnz_m) * stride + cnt;   // sig_est_index
           uint32_t slot;
           uint32_t e = est_load(sh, est_g, idx, &slot);
-          int b = rd_get(rd, in, p1(e));
+          int b = rdec(e);
           est_store(sh, est_g, idx, slot, est_update(e, b, 0x50));
           bins++;
           push(sop + ((uint32_t)sc << 3) + (uint32_t)b);
@@ -1989,6 +2030,9 @@ AVR_FI void begin_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, 
     cd_init(w.cd, w.in);
   } else if (MODE == MODE_DECOMPRESS) {
     rd_init(w.rd, w.in);
+#ifdef AVR_EXP_VQ
+    if constexpr (!P32) w.vq_init();
+#endif
   } else {
     ce_init(w.ce);
     w.rng = d->payload_offset * 0x9E3779B97F4A7C15ull + 0x1234567ull + (uint64_t)d->picture_id;
@@ -2061,12 +2105,6 @@ AVR_FI uint32_t vgpr_zero() {
   asm volatile("v_mov_b32 %0, 0" : "=v"(z));
   return z;
 }
-AVR_FI uint64_t readlane64(uint64_t v, uint32_t j) {
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, j);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
-  return (uint64_t)hi << 32 | lo;
-}
-
 // The modeler wave (compress): the estimator recurrences (recode.cpp:816-820, 1030-1047),
 // lane-parallel over each batch of ring-0 ops (lane j = op j):
 //  1. every lane loads its op's estimator at once: per-context ones from Shared::est, SIG/NZ
