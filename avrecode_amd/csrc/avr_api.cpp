@@ -1428,7 +1428,7 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
     d.out_offset = work;
     d.out_capacity = (uint32_t)(s.size * 2 + 256);
     work += ((uint64_t)d.out_capacity + 15) & ~15ull;
-    plan.max_w = std::max(plan.max_w, ring_cols(d));
+    if (d.coded) plan.max_w = std::max(plan.max_w, ring_cols(d));   // uncoded slices are never walked
     mh = std::max(mh, d.mb_height);
     plan.descs.push_back(d);
   }

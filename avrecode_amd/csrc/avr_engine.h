@@ -528,19 +528,11 @@ struct RecodedDecoder {
   uint64_t low, range;
   uint32_t next_digit;  // last aligned digit read
   uint32_t next;        // next byte index
-#ifdef AVR_EXP_PF
-  uint32_t pf;          // byte `next`, read from LDS one renormalisation ahead (as PDecoder)
-#endif
 };
 __device__ __forceinline__ void rd_consume(RecodedDecoder& d, InStream& in) {
   // the byte comes from LDS in a vector register: move it to a scalar one so that low stays a
   // scalar register (otherwise every bin pays vector<->scalar transfers on low)
-#ifdef AVR_EXP_PF
-  uint32_t b = __builtin_amdgcn_readfirstlane(d.pf);
-  d.pf = in_byte(in, ++d.next);
-#else
   uint32_t b = __builtin_amdgcn_readfirstlane(in_byte(in, d.next++));
-#endif
   uint32_t digit = ((d.next_digit & 1) << 7) | (b >> 1);
   d.next_digit = b;
   d.low = (d.low << 8) | digit;
@@ -549,9 +541,6 @@ __device__ __forceinline__ void rd_consume(RecodedDecoder& d, InStream& in) {
 __device__ __forceinline__ void rd_init(RecodedDecoder& d, InStream& in) {  // arith:218-230
   d.next = 0;
   d.next_digit = in_byte(in, d.next++);
-#ifdef AVR_EXP_PF
-  d.pf = in_byte(in, d.next);
-#endif
   d.low = d.next_digit >> 1;
   d.range = 128;
   #pragma clang loop unroll(disable)
