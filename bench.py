@@ -670,7 +670,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r03")
+    ap.add_argument("--round", default="r04")
     ap.add_argument("--file-reps", type=int, default=3, help="timed reps of a whole-file call under 2 s")
     ap.add_argument("--no-files", action="store_true", help="skip the whole-file roundtrips")
     ap.add_argument("--no-clip", action="store_true", help="skip the configs[1] clip in the file roundtrips")
