@@ -198,13 +198,29 @@ __host__ __device__ inline int op_class_pip_c(uint32_t c) { return c == 1 ? PIPC
 __host__ __device__ inline int op_class_pip_d(uint32_t c) { return c == 1 ? PIPC_SIG_MAP : c == 2 ? PIPC_SIG_EOB : PIPC_UNKNOWN; }
 constexpr uint32_t OP_FINISH = 1u << 30;
 constexpr uint32_t OP_END = 1u << 31;
-enum { OPK_DECISION = 0, OPK_BYPASS = 1, OPK_TERMINATE = 2 };
+enum { OPK_DECISION = 0, OPK_BYPASS = 1, OPK_TERMINATE = 2, OPK_MACRO = 3 };
 
 constexpr uint32_t OPM_CACHE = 2, OPM_THR50 = 4;
 AVR_FI uint32_t op_model(int bin, uint32_t flags, uint32_t idx) { return (uint32_t)bin | flags | idx << 3; }
 AVR_FI uint32_t op_recode(int bin, uint32_t est) {
   const uint32_t pos = (est & 0xff) + 1, tot = pos + (est >> 8) + 1;
   return (uint32_t)bin | pos << 1 | tot << 8;
+}
+// Decompress macro ops (kind OPK_MACRO, progressive walkers): the coder expands them into the bins
+// and contexts the walker would have sent one by one.
+//   map segment (bit 3 = 0): ctxBlockCat bits 4-7, segment (16 scan positions) bits 8-9, positions
+//     coded in it - 1 bits 10-13, bit 14 = the map ended on a last_significant_coeff_flag of 1 at
+//     its highest significant position (else: a full segment, or the map ran to max - 1), bits
+//     15-30 significant_coeff_flag of each position;
+//   level (bit 3 = 1): ctxBlockCat bits 4-7, sign bit 8, min(coeff_abs_level_minus1 + 1, 15) bits
+//     9-12 (15: the prefix only; the escape suffix and the sign follow as bypass ops).
+// A map's last segment resets the coder's level counters (gt1 / eq1 of residual_block_cabac).
+AVR_FI uint32_t op_map(int cat, int seg, int npos, int ended, uint32_t mask) {
+  return OPK_MACRO << 1 | (uint32_t)cat << 4 | (uint32_t)seg << 8 | (uint32_t)(npos - 1) << 10 |
+         (uint32_t)ended << 14 | mask << 15;
+}
+AVR_FI uint32_t op_level(int cat, int absl, int sign) {
+  return OPK_MACRO << 1 | 8u | (uint32_t)cat << 4 | (uint32_t)sign << 8 | (uint32_t)absl << 9;
 }
 // Ring counters: plain LDS accesses.  LDS is one memory per CU and executes each wave's accesses
 // in program order, so a counter store issued after the entry stores cannot be seen before them;
@@ -411,7 +427,7 @@ AVR_FI void ring_retire(Shared* sh, int r, uint32_t tail) { st_volatile(&sh->fif
 
 // SIG / NZ estimators: probe the LDS hash table (see kEtabBits).  Returns the estimator and in
 // *slot where est_store writes it back (0: the HBM table).  Called by a whole wave.
-AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32_t* slot) {
+AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32_t* slot, bool claim = false) {
   const uint32_t p = (idx * kEstKeyMul) & ((1u << 19) - 1);
   const uint32_t home = p >> 7, tag = p & 127;
   const uint32_t lane = __lane_id();
@@ -432,6 +448,8 @@ AVR_FI uint32_t est_load(Shared* sh, const uint16_t* est_g, uint32_t idx, uint32
   if (free_v) {
     const uint32_t j = (uint32_t)__builtin_ctzll(free_v);
     *slot = (0x8000u | j << 7 | tag) << 16 | (home + j);
+    // a caller that defers its store claims the slot now (a later key of the window must not take it)
+    if (claim && lane == j) sh->etab[home + j] = *slot & 0xffff0000u;
     return 0;
   }
   // HBM: slot 1 marks the entry's first store (to be logged), 0 a stored one
@@ -667,6 +685,22 @@ struct Walker {
     }
   }
 
+  // decompress: a residual bin / a bypass bin without its coder op (the macro ops below carry it)
+  AVR_FI int rdec_lane(uint32_t L) {
+    bins++;
+    const uint32_t e = __builtin_amdgcn_readlane(rc_v, L);
+    const int b = rdec(e);
+    rc_v = wlane(rc_v, L, est_update(e, b, 0x60));
+    return b;
+  }
+  AVR_FI int rdec_bypass() {
+    bins++;
+    const uint32_t e = byp_e;
+    const int b = rdec(e);
+    byp_e = est_update(e, b, 0x60);
+    return b;
+  }
+
   // recoded-decoder probability (recode.cpp:816-820).  The reciprocal comes by a scalar load
   // from the constant table (s_load_dwordx4 into SGPRs, scalar-cache hit): fewer instructions on
   // the walker than three v_readlane pairs and selects from a VGPR table (measured 10 % slower).
@@ -682,40 +716,7 @@ struct Walker {
     }
   }
   // One decision of the model's coder with estimator e (recode.cpp:1435-1449).
-#ifdef AVR_EXP_VQ
-  // u64 coder: lane L holds floor(range / (L + kVqBase)) for the current range, computed on the
-  // vector unit right after each decision -- off the next decision's critical path, which then
-  // needs one v_readlane pair instead of a scalar load of the reciprocal and the 64-bit product.
-  // Totals below kVqBase (a fresh estimator's first uses) take the scalar path.
-  static constexpr uint32_t kVqBase = 34;
-  uint32_t vq_mlo, vq_mhi, vq_sh;   // lane L: HotTables::div[L + kVqBase]
-  uint64_t vq;                      // lane L: floor(range / (L + kVqBase))
-  AVR_FI void vq_init() {
-    const uint64_t* dv = &G->hot.div[__lane_id() + kVqBase][0];
-    vq_mlo = (uint32_t)dv[0];
-    vq_mhi = (uint32_t)(dv[0] >> 32);
-    vq_sh = (uint32_t)dv[1];
-    vq_update();
-  }
-  AVR_FI void vq_update() {
-    const uint64_t q = __umul64hi(rd.range, (uint64_t)vq_mhi << 32 | vq_mlo) >> vq_sh;
-    uint32_t lo = (uint32_t)q, hi = (uint32_t)(q >> 32);
-    asm volatile("" : "+v"(lo), "+v"(hi));   // computed here, right after the decision
-    vq = (uint64_t)hi << 32 | lo;
-  }
-  AVR_FI int rdec(uint32_t e) {
-    if constexpr (!P32) {
-      const uint32_t pos = (e & 0xff) + 1, tot = (e & 0xff) + (e >> 8) + 2;
-      const uint64_t r1 = tot >= kVqBase ? readlane64(vq, tot - kVqBase) * pos : p1(e);
-      const int b = rd_get(rd, in, r1);
-      vq_update();
-      return b;
-    }
-    return rd_get(rd, in, p1(e));
-  }
-#else
   AVR_FI int rdec(uint32_t e) { return rd_get(rd, in, p1(e)); }
-#endif
   // CABAC state record of state byte s: VGPR table (two v_readlane) or, with AVR_CABAC_SMEM, a
   // scalar load
   AVR_FI CabacRec crec(uint32_t s) const {
@@ -1289,6 +1290,13 @@ struct Walker {
       auto map_loop = [&](auto K) {
         constexpr int k = decltype(K)::value;
         constexpr int stride = k == 2 ? 64 : 16;
+        uint32_t mk = 0;   // progressive walker: the significance bits of this 16-position segment
+        // 4x4-class maps key each position's estimator by the position itself, so no key repeats
+        // within the map: the LDS write-backs wait in two VGPRs (lane = position) for one store
+        // after the loop (a new key claims its slot at once, est_load).  Chroma DC and 8x8 maps
+        // reuse keys within the map and store at once.
+        constexpr bool defer = k == 0;
+        uint32_t dslot_v = 0, de_v = 0;
         for (pos = 0; pos < max - 1; pos++) {
           int sc, lc, zo;
           if constexpr (k == 2) {
@@ -1304,18 +1312,39 @@ struct Walker {
           }
           const int idx = seb + (zo * stride + nnz_m) * stride + cnt;   // sig_est_index
           uint32_t slot;
-          uint32_t e = est_load(sh, est_g, idx, &slot);
+          uint32_t e = est_load(sh, est_g, idx, &slot, defer);
           int b = rdec(e);
-          est_store(sh, est_g, idx, slot, est_update(e, b, 0x50));
+          const uint32_t ne = est_update(e, b, 0x50);
+          if (defer && (slot >> 31)) {
+            dslot_v = wlane(dslot_v, (uint32_t)pos, slot);
+            de_v = wlane(de_v, (uint32_t)pos, ne);
+          } else {
+            est_store(sh, est_g, idx, slot, ne);
+          }
           bins++;
-          push(sop + ((uint32_t)sc << 3) + (uint32_t)b);
+          if constexpr (FLD) push(sop + ((uint32_t)sc << 3) + (uint32_t)b);
+          else mk |= (uint32_t)b << (pos & 15);
           if (b) {
             cnt++;
             int last = nnz_m == cnt;   // derived EOB (recode.cpp:1437-1438)
             bins++;
-            push(lop + ((uint32_t)lc << 3) + (uint32_t)last);
+            if constexpr (FLD) push(lop + ((uint32_t)lc << 3) + (uint32_t)last);
             if (last) break;
           }
+          if constexpr (!FLD && k == 2) {
+            if ((pos & 15) == 15) {
+              push(op_map(cat, pos >> 4, 16, 0, mk));
+              mk = 0;
+            }
+          }
+        }
+        if constexpr (defer) {
+          if (dslot_v >> 31) sh->etab[dslot_v & 0xffff] = (dslot_v & 0xffff0000u) | de_v;
+          wave_sync();
+        }
+        if constexpr (!FLD) {
+          const int ended = pos < max - 1;
+          push(op_map(cat, pos >> 4, (pos & 15) + ended, ended, mk));
         }
       };
       if (max == 64) map_loop(std::integral_constant<int, 2>());
@@ -1369,6 +1398,33 @@ struct Walker {
       const int ab = (int)opaque_u32((uint32_t)T->abs_base[cat]);   // scalar: the coder ops' base
       int gt1 = 0, eq1 = 0;
       PROF_BEGIN(t6);
+      if constexpr (MODE == MODE_DECOMPRESS && !FLD) {
+        // one coder op per coefficient (op_level): the coder derives the level bins' contexts
+        for (int i = cnt - 1; i >= 0 && !err; i--) {
+          int absl;
+          const int i0 = gt1 ? 0 : min(4, 1 + eq1);
+          if (!rdec_lane(32 + i0)) {
+            absl = 1;
+          } else {
+            const int i1 = 5 + min(4 - (cat == 3), gt1);
+            absl = 2;
+            while (absl < 15 && rdec_lane(32 + i1)) absl++;
+          }
+          if (absl < 15) {
+            push(op_level(cat, absl, rdec_bypass()));
+          } else {   // escape: the prefix as one op, suffix and sign bin by bin
+            push(op_level(cat, 15, 0));
+            int k = 0;
+            while (bypass(SE_LEVEL_SUFFIX, k)) {
+              if (++k > 30) { err = AVR_SLICE_BAD_LEVEL; break; }
+            }
+            while (k-- > 0) bypass(SE_LEVEL_SUFFIX, 100);
+            bypass(SE_OTHER, 0);
+          }
+          if (absl == 1) eq1++;
+          else gt1++;
+        }
+      } else
       for (int i = cnt - 1; i >= 0 && !err; i--) {
         int absl;
         const int i0 = gt1 ? 0 : min(4, 1 + eq1);
@@ -2030,9 +2086,6 @@ AVR_FI void begin_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, 
     cd_init(w.cd, w.in);
   } else if (MODE == MODE_DECOMPRESS) {
     rd_init(w.rd, w.in);
-#ifdef AVR_EXP_VQ
-    if constexpr (!P32) w.vq_init();
-#endif
   } else {
     ce_init(w.ce);
     w.rng = d->payload_offset * 0x9E3779B97F4A7C15ull + 0x1234567ull + (uint64_t)d->picture_id;
@@ -2273,6 +2326,8 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
     vtab_load(vt, T);
   }
   const int r = MODE == MODE_COMPRESS ? 1 : 0;
+  uint32_t gt1 = 0, eq1 = 0;   // decompress: level counters of the block in progress (op_level)
+  const uint32_t numc = d->chroma_array_type == 2 ? 2u : 1u;   // chroma DC: NumC8x8
   uint32_t tail = 0;
   uint64_t waited = 0;
 #ifdef AVR_PROFILE
@@ -2324,40 +2379,85 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
       }
       asm volatile("; MARK_CODER_END");
     } else {
-      if (billing) {   // the generic coder's emission counts beside the re-encode, op by op
+      // billing: the generic coder's emission counts beside the re-encode, bin by bin
+      auto run = [&](auto BILL) {
+        constexpr bool bl = decltype(BILL)::value;
+        auto put_dec = [&](int b, uint32_t ctx, uint32_t cls) {
+          uint8_t* stp = &sh->state[ctx];
+          if constexpr (bl) {
+            const uint32_t st = *stp;
+            const uint32_t bytes = cb_decision(cbill, b, st, vtab_rec(vt, st));
+            if (bytes) bill[op_class_pip_d(cls)] += bytes;
+          }
+          ce_decision_v(ce, o, b, stp, vt);
+        };
+        auto put_byp = [&](int b, uint32_t cls) {
+          if constexpr (bl) {
+            const uint32_t bytes = cb_bypass(cbill, b);
+            if (bytes) bill[op_class_pip_d(cls)] += bytes;
+          }
+          ce_bypass(ce, o, b);
+        };
         for (uint32_t j = 0; j < n; j++) {
           const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
           if (op & OP_END) { done = true; break; }
           const int b = op & 1;
           const uint32_t kind = (op >> 1) & 3;
-          uint32_t bytes;
+          const uint32_t cls = (op >> OPC_SHIFT_D) & 3;
           if (kind == OPK_DECISION) {
-            uint8_t* stp = &sh->state[(op >> 3) & 1023];
-            const uint32_t st = *stp;
-            bytes = cb_decision(cbill, b, st, vtab_rec(vt, st));
-            ce_decision_v(ce, o, b, stp, vt);
+            put_dec(b, (op >> 3) & 1023, cls);
           } else if (kind == OPK_BYPASS) {
-            bytes = cb_bypass(cbill, b);
-            ce_bypass(ce, o, b);
+            put_byp(b, cls);
+          } else if (kind == OPK_MACRO) {
+            const uint32_t cat = (op >> 4) & 15;
+            if (op & 8) {   // op_level: coeff_abs_level_minus1 prefix (+ sign), residual_block_cabac's contexts
+              const uint32_t sg = (op >> 8) & 1, absl = (op >> 9) & 15;
+              const uint32_t ab = (uint32_t)T->abs_base[cat];
+              put_dec(absl > 1, ab + (gt1 ? 0u : min(4u, 1 + eq1)), 0);
+              if (absl > 1) {
+                const uint32_t c1 = ab + 5 + min(4u - (cat == 3), gt1);
+                for (uint32_t a = 2; a < 15; a++) {
+                  const int more = a < absl;
+                  put_dec(more, c1, 0);
+                  if (!more) break;
+                }
+              }
+              if (absl < 15) put_byp((int)sg, 0);
+              if (absl == 1) eq1++;
+              else gt1++;
+            } else {        // op_map: significant / last_significant_coeff_flag of one segment
+              const uint32_t start = ((op >> 8) & 3) * 16, npos = ((op >> 10) & 15) + 1, ended = (op >> 14) & 1;
+              const uint32_t mask = op >> 15, lastq = ended ? npos - 1 : 16u;
+              const uint32_t sb = (uint32_t)T->sig_base[cat], lb = (uint32_t)T->last_base[cat];
+              const bool c8 = cat == 5 || cat == 9 || cat == 13;
+              for (uint32_t q = 0; q < npos; q++) {
+                const uint32_t p = start + q;
+                uint32_t sc, lc;
+                if (c8) {
+                  sc = T->sig8x8[p];
+                  lc = T->last8x8[p];
+                } else if (cat == 3) {
+                  sc = lc = min(p / numc, 2u);
+                } else {
+                  sc = lc = p;
+                }
+                const int sig = (mask >> q) & 1;
+                put_dec(sig, sb + sc, 1);
+                if (sig) put_dec(q == lastq, lb + lc, 2);
+              }
+              if (npos != 16 || ended) gt1 = eq1 = 0;   // the map's last segment: its block's levels follow
+            }
           } else {
-            bytes = cb_terminate(cbill, b);
+            if constexpr (bl) {
+              const uint32_t bytes = cb_terminate(cbill, b);
+              if (bytes) bill[op_class_pip_d(cls)] += bytes;
+            }
             ce_terminate(ce, o, b);
           }
-          if (bytes) bill[op_class_pip_d((op >> OPC_SHIFT_D) & 3)] += bytes;
         }
-      } else for (uint32_t j = 0; j < n; j++) {
-        const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
-        if (op & OP_END) { done = true; break; }
-        const int b = op & 1;
-        const uint32_t kind = (op >> 1) & 3;
-#ifndef AVR_EXP_NOCODER
-        if (kind == OPK_DECISION) ce_decision_v(ce, o, b, &sh->state[(op >> 3) & 1023], vt);
-        else if (kind == OPK_BYPASS) ce_bypass(ce, o, b);
-        else ce_terminate(ce, o, b);
-#else
-        (void)b; (void)kind;   // experiment: the walker alone (output invalid)
-#endif
-      }
+      };
+      if (billing) run(std::true_type());
+      else run(std::false_type());
     }
     tail += n;
     ring_retire(sh, r, tail);
