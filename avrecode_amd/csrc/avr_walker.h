@@ -207,20 +207,25 @@ AVR_FI uint32_t op_recode(int bin, uint32_t est) {
   return (uint32_t)bin | pos << 1 | tot << 8;
 }
 // Decompress macro ops (kind OPK_MACRO, progressive walkers): the coder expands them into the bins
-// and contexts the walker would have sent one by one.
-//   map segment (bit 3 = 0): ctxBlockCat bits 4-7, segment (16 scan positions) bits 8-9, positions
-//     coded in it - 1 bits 10-13, bit 14 = the map ended on a last_significant_coeff_flag of 1 at
-//     its highest significant position (else: a full segment, or the map ran to max - 1), bits
-//     15-30 significant_coeff_flag of each position;
-//   level (bit 3 = 1): ctxBlockCat bits 4-7, sign bit 8, min(coeff_abs_level_minus1 + 1, 15) bits
-//     9-12 (15: the prefix only; the escape suffix and the sign follow as bypass ops).
-// A map's last segment resets the coder's level counters (gt1 / eq1 of residual_block_cabac).
-AVR_FI uint32_t op_map(int cat, int seg, int npos, int ended, uint32_t mask) {
-  return OPK_MACRO << 1 | (uint32_t)cat << 4 | (uint32_t)seg << 8 | (uint32_t)(npos - 1) << 10 |
-         (uint32_t)ended << 14 | mask << 15;
+// and contexts the walker would have sent one by one.  Bits 3-4 select the op:
+//   0 map segment: ctxBlockCat bits 5-8, positions coded in this 16-position segment - 1 bits 9-12,
+//     bit 13 = the map ended on a last_significant_coeff_flag of 1 at its highest significant
+//     position (else: a full segment, or the map ran to max - 1), bits 14-29 the
+//     significant_coeff_flag of each position.  The coder tracks the segment's first position; a
+//     map's last segment resets it and the level counters (gt1 / eq1 of residual_block_cabac);
+//   1 level: ctxBlockCat bits 5-8, sign bit 9, min(coeff_abs_level_minus1 + 1, 15) bits 10-13 (15:
+//     the prefix only; the escape's suffix and the sign follow as bypass ops);
+//   2 mvd component: vertical bit 5 (ctxIdxOffset 47, else 40), ctxIdxInc of the first bin bits 6-7,
+//     sign bit 8, min(|mvd|, 9) bits 9-12 (9: the prefix only; the UEG3 suffix and the sign follow
+//     as bypass ops).
+AVR_FI uint32_t op_map(int cat, int npos, int ended, uint32_t mask) {
+  return OPK_MACRO << 1 | (uint32_t)cat << 5 | (uint32_t)(npos - 1) << 9 | (uint32_t)ended << 13 | mask << 14;
 }
 AVR_FI uint32_t op_level(int cat, int absl, int sign) {
-  return OPK_MACRO << 1 | 8u | (uint32_t)cat << 4 | (uint32_t)sign << 8 | (uint32_t)absl << 9;
+  return OPK_MACRO << 1 | 1u << 3 | (uint32_t)cat << 5 | (uint32_t)sign << 9 | (uint32_t)absl << 10;
+}
+AVR_FI uint32_t op_mvd(int comp, int inc, int amvd, int sign) {
+  return OPK_MACRO << 1 | 2u << 3 | (uint32_t)comp << 5 | (uint32_t)inc << 6 | (uint32_t)sign << 8 | (uint32_t)amvd << 9;
 }
 // Ring counters: plain LDS accesses.  LDS is one memory per CU and executes each wave's accesses
 // in program order, so a counter store issued after the entry stores cannot be seen before them;
@@ -691,6 +696,14 @@ struct Walker {
     const uint32_t e = __builtin_amdgcn_readlane(rc_v, L);
     const int b = rdec(e);
     rc_v = wlane(rc_v, L, est_update(e, b, 0x60));
+    return b;
+  }
+  AVR_FI int rdec_mc(int ctx) {   // a macroblock-layer context bin (kMcBase .. + 63)
+    bins++;
+    const uint32_t L = (uint32_t)(ctx - kMcBase);
+    const uint32_t e = __builtin_amdgcn_readlane(mc_v, L);
+    const int b = rdec(e);
+    mc_v = wlane(mc_v, L, est_update(e, b, 0x60));
     return b;
   }
   AVR_FI int rdec_bypass() {
@@ -1333,7 +1346,7 @@ struct Walker {
           }
           if constexpr (!FLD && k == 2) {
             if ((pos & 15) == 15) {
-              push(op_map(cat, pos >> 4, 16, 0, mk));
+              push(op_map(cat, 16, 0, mk));
               mk = 0;
             }
           }
@@ -1344,7 +1357,7 @@ struct Walker {
         }
         if constexpr (!FLD) {
           const int ended = pos < max - 1;
-          push(op_map(cat, pos >> 4, (pos & 15) + ended, ended, mk));
+          push(op_map(cat, (pos & 15) + ended, ended, mk));
         }
       };
       if (max == 64) map_loop(std::integral_constant<int, 2>());
@@ -1582,6 +1595,30 @@ struct Walker {
     const int base = comp ? 47 : 40;
     const int amvd = mvd_nb(list, comp, x4, y4, 1) + mvd_nb(list, comp, x4, y4, 0);
     const int inc = amvd < 3 ? 0 : amvd <= 32 ? 1 : 2;
+    if constexpr (MODE == MODE_DECOMPRESS && !FLD) {   // one op_mvd (+ an escape's bins)
+      if (!rdec_mc(base + inc)) {
+        push(op_mvd(comp, inc, 0, 0));
+        return 0;
+      }
+      int mvd = 1, ctx = base + 3;
+      while (mvd < 9 && rdec_mc(ctx)) {
+        if (mvd < 4) ctx++;
+        mvd++;
+      }
+      if (mvd < 9) {
+        push(op_mvd(comp, inc, mvd, rdec_bypass()));
+        return mvd;
+      }
+      push(op_mvd(comp, inc, 9, 0));
+      int k = 3;
+      while (bypass(SE_MVD_SUFFIX, k - 3)) {
+        mvd += 1 << k;
+        if (++k > 24) { err = AVR_SLICE_BAD_MVD; return 0; }
+      }
+      while (k--) mvd += bypass(SE_MVD_SUFFIX, 100) << k;
+      bypass(SE_OTHER, 0);
+      return mvd < 70 ? mvd : 70;
+    }
     if (!bin(SE_OTHER, 0, base + inc)) return 0;
     int mvd = 1, ctx = base + 3;
     while (mvd < 9 && bin(SE_OTHER, 0, ctx)) {
@@ -2327,6 +2364,7 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
   }
   const int r = MODE == MODE_COMPRESS ? 1 : 0;
   uint32_t gt1 = 0, eq1 = 0;   // decompress: level counters of the block in progress (op_level)
+  uint32_t mpos = 0;           // decompress: first position of the next op_map segment
   const uint32_t numc = d->chroma_array_type == 2 ? 2u : 1u;   // chroma DC: NumC8x8
   uint32_t tail = 0;
   uint64_t waited = 0;
@@ -2409,29 +2447,14 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
           } else if (kind == OPK_BYPASS) {
             put_byp(b, cls);
           } else if (kind == OPK_MACRO) {
-            const uint32_t cat = (op >> 4) & 15;
-            if (op & 8) {   // op_level: coeff_abs_level_minus1 prefix (+ sign), residual_block_cabac's contexts
-              const uint32_t sg = (op >> 8) & 1, absl = (op >> 9) & 15;
-              const uint32_t ab = (uint32_t)T->abs_base[cat];
-              put_dec(absl > 1, ab + (gt1 ? 0u : min(4u, 1 + eq1)), 0);
-              if (absl > 1) {
-                const uint32_t c1 = ab + 5 + min(4u - (cat == 3), gt1);
-                for (uint32_t a = 2; a < 15; a++) {
-                  const int more = a < absl;
-                  put_dec(more, c1, 0);
-                  if (!more) break;
-                }
-              }
-              if (absl < 15) put_byp((int)sg, 0);
-              if (absl == 1) eq1++;
-              else gt1++;
-            } else {        // op_map: significant / last_significant_coeff_flag of one segment
-              const uint32_t start = ((op >> 8) & 3) * 16, npos = ((op >> 10) & 15) + 1, ended = (op >> 14) & 1;
-              const uint32_t mask = op >> 15, lastq = ended ? npos - 1 : 16u;
+            const uint32_t sub = (op >> 3) & 3, cat = (op >> 5) & 15;
+            if (sub == 0) {   // op_map: significant / last_significant_coeff_flag of one segment
+              const uint32_t npos = ((op >> 9) & 15) + 1, ended = (op >> 13) & 1;
+              const uint32_t mask = op >> 14, lastq = ended ? npos - 1 : 16u;
               const uint32_t sb = (uint32_t)T->sig_base[cat], lb = (uint32_t)T->last_base[cat];
               const bool c8 = cat == 5 || cat == 9 || cat == 13;
               for (uint32_t q = 0; q < npos; q++) {
-                const uint32_t p = start + q;
+                const uint32_t p = mpos + q;
                 uint32_t sc, lc;
                 if (c8) {
                   sc = T->sig8x8[p];
@@ -2445,7 +2468,38 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
                 put_dec(sig, sb + sc, 1);
                 if (sig) put_dec(q == lastq, lb + lc, 2);
               }
-              if (npos != 16 || ended) gt1 = eq1 = 0;   // the map's last segment: its block's levels follow
+              if (npos != 16 || ended) {   // the map's last segment: its block's levels follow
+                mpos = 0;
+                gt1 = eq1 = 0;
+              } else {
+                mpos += 16;
+              }
+            } else if (sub == 1) {   // op_level: coeff_abs_level_minus1 prefix (+ sign)
+              const uint32_t sg = (op >> 9) & 1, absl = (op >> 10) & 15;
+              const uint32_t ab = (uint32_t)T->abs_base[cat];
+              put_dec(absl > 1, ab + (gt1 ? 0u : min(4u, 1 + eq1)), 0);
+              if (absl > 1) {
+                const uint32_t c1 = ab + 5 + min(4u - (cat == 3), gt1);
+                for (uint32_t a = 2; a < 15; a++) {
+                  const int more = a < absl;
+                  put_dec(more, c1, 0);
+                  if (!more) break;
+                }
+              }
+              if (absl < 15) put_byp((int)sg, 0);
+              if (absl == 1) eq1++;
+              else gt1++;
+            } else {   // op_mvd: mvd_lX[][][comp] prefix (+ sign), 9.3.3.1.1.7 / 9.3.3.1.2
+              const uint32_t base = (op & 32) ? 47u : 40u, sg = (op >> 8) & 1, am = (op >> 9) & 15;
+              put_dec(am > 0, base + ((op >> 6) & 3), 0);
+              if (am > 0) {
+                for (uint32_t m = 1; m < 9; m++) {
+                  const int more = m < am;
+                  put_dec(more, base + min(m + 2, 6u), 0);
+                  if (!more) break;
+                }
+                if (am < 9) put_byp((int)sg, 0);
+              }
             }
           } else {
             if constexpr (bl) {
