@@ -515,6 +515,14 @@ def stream_cpu_baseline(data, ps, budget_s):
                       f"parallel-model compress + decompress, one thread, {t_tot:.1f} s"}
 
 
+_JSON_OUT = sys.stdout
+
+
+def emit(obj):
+    """The bench line: the only text on the process's stdout (see the __main__ block)."""
+    print(json.dumps(obj), file=_JSON_OUT, flush=True)
+
+
 def main_stream_shard(args):
     """`--stream-shard`: configs[3] alone at the full (or --stream-seconds) length, N GPUs."""
     import torch
@@ -532,7 +540,7 @@ def main_stream_shard(args):
     args.stream_steps = args.steps
     rec = stream_shard_leg(ctx, args, args.stream_seconds, world, rank, dev, with_cpu=False)
     if rank == 0:
-        print(json.dumps(rec), flush=True)
+        emit(rec)
     dist.barrier()
     dist.destroy_process_group()
     ctx.close()
@@ -826,7 +834,7 @@ def main():
         if rank == 0:
             line["corpus"] = rec
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
@@ -834,4 +842,9 @@ def main():
 
 
 if __name__ == "__main__":
+    # Native libraries (RCCL prints its version banner at init) write to file descriptor 1: point it
+    # at stderr and keep the original stdout for the one JSON line.
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     main()
