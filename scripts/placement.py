@@ -45,6 +45,11 @@ def main():
         k = (args.slices - j + len(qps) - 1) // len(qps)
         parts.append(ctx.synthesize(avr.SynthParams(mb_width=120, mb_height=68, slice_type=2, slice_qp=qp,
                                                     chroma_format_idc=1, transform_8x8_mode=1, seed=j), k))
+    groups, g0 = [], 0   # (qp, first slice, end) of each contiguous QP group
+    for j, qp in enumerate(qps):
+        k = (args.slices - j + len(qps) - 1) // len(qps)
+        groups.append((qp, g0, g0 + k))
+        g0 += k
     ps = avr.parse_stream(b"".join(parts))
     b = DeviceBatch(ctx, ps)
     b.roundtrip(avr.MODEL_PARALLEL)
@@ -84,6 +89,12 @@ def main():
                "walker_ns_per_bin_min_mean_max": [round(float(x), 1) for x in
                                                   ((rt * 10 / bins).min(), (rt * 10 / bins).mean(), (rt * 10 / bins).max())],
                "span_ms": round(span, 1),
+               # the batch's tail: each slice's walker lifetime against the launch's span (one
+               # walker per slice, all resident at once): busy = sum of lifetimes / (slices x span)
+               "walker_ms_min_median_mean_max": [round(float(x) / 1e5, 2) for x in
+                                                 (rt.min(), np.median(rt), rt.mean(), rt.max())],
+               "walker_busy_fraction": round(float(rt.sum()) / (n * max(span * 1e5, 1.0)), 3),
+               "walker_ms_by_qp": {str(q): round(float(rt[g0:g1].mean()) / 1e5, 2) for q, g0, g1 in groups},
                "cus_used": len(cus), "slices_per_cu": dict(collections.Counter(len(v) for v in cus.values())),
                "walkers_per_simd": dict(collections.Counter(walkers_per_simd.values())),
                "roles_per_simd": dict(collections.Counter(tuple(sorted(v)) for v in simd_roles.values()).most_common(8)),
