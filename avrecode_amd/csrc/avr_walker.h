@@ -2390,7 +2390,11 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
 // finish, recode.cpp:1074, 1092-1094), gathering each op's reciprocal record with its lane;
 // decompress retires ring 0 (cabac::encoder::put / put_bypass / put_terminate,
 // recode.cpp:1443-1474, cabac_code.h:33-67).
-template <int MODE, bool P32>
+// SEQ: the reference model's per-file kernels (one slice chain per CU, where the coder can hold the
+// walker up): the level / mvd prefixes on one context with the state in a register, and the map
+// loops unswitched by block kind.  The slice batch keeps the plain loops (measured: the variants
+// cost the batch 0.3-0.8 % and gain R-mode 1-2 %, profiles/r04o_coder2_ab.log, r04q_crunmvd_ab.log).
+template <int MODE, bool P32, bool SEQ = false>
 AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out, uint32_t flags) {
   const bool billing = (flags & kFlagBill) != 0;
   uint32_t bill[6] = {0, 0, 0, 0, 0, 0};
@@ -2486,6 +2490,23 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
           }
           ce_decision_v(ce, o, b, stp, vt);
         };
+        // n ones then (if zero) a zero on one context, class 0 (level / mvd prefixes)
+        auto put_run = [&](uint32_t ctx, uint32_t n, bool zero) {
+          uint8_t* stp = &sh->state[ctx];
+          uint32_t st = *stp;
+          for (uint32_t k = 0; k < n + (zero ? 1u : 0u); k++) {
+            const int b = k < n;
+            const CabacRec r = vtab_rec(vt, st);
+            if constexpr (bl) {
+              const uint32_t bytes = cb_decision(cbill, b, st, r);
+              if (bytes) bill[0] += bytes;
+            }
+            uint32_t ns;
+            ce_encode(ce, o, b, st, r, &ns);
+            st = ns;
+          }
+          *stp = (uint8_t)st;
+        };
         auto put_byp = [&](int b, uint32_t cls) {
           if constexpr (bl) {
             const uint32_t bytes = cb_bypass(cbill, b);
@@ -2509,21 +2530,48 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
               const uint32_t npos = ((op >> 9) & 15) + 1, ended = (op >> 13) & 1;
               const uint32_t mask = op >> 14, lastq = ended ? npos - 1 : 16u;
               const uint32_t sb = (uint32_t)T->sig_base[cat], lb = (uint32_t)T->last_base[cat];
-              const bool c8 = cat == 5 || cat == 9 || cat == 13;
-              for (uint32_t q = 0; q < npos; q++) {
-                const uint32_t p = mpos + q;
-                uint32_t sc, lc;
-                if (c8) {
-                  sc = T->sig8x8[p];
-                  lc = T->last8x8[p];
-                } else if (cat == 3) {
-                  sc = lc = min(p / numc, 2u);
-                } else {
-                  sc = lc = p;
+              // one loop per block kind (K: 0 4x4-class, 1 chroma DC, 2 8x8), as the walker's
+              auto seg_loop = [&](auto K) {
+                constexpr int k = decltype(K)::value;
+                for (uint32_t q = 0; q < npos; q++) {
+                  const uint32_t p = mpos + q;
+                  uint32_t sc, lc;
+                  if constexpr (k == 2) {
+                    sc = T->sig8x8[p];
+                    lc = T->last8x8[p];
+                  } else if constexpr (k == 1) {
+                    sc = lc = min(p / numc, 2u);
+                  } else {
+                    sc = lc = p;
+                  }
+                  const int sig = (mask >> q) & 1;
+                  put_dec(sig, sb + sc, 1);
+                  if (sig) put_dec(q == lastq, lb + lc, 2);
                 }
-                const int sig = (mask >> q) & 1;
-                put_dec(sig, sb + sc, 1);
-                if (sig) put_dec(q == lastq, lb + lc, 2);
+              };
+              if constexpr (!SEQ) {
+                const bool c8 = cat == 5 || cat == 9 || cat == 13;
+                for (uint32_t q = 0; q < npos; q++) {
+                  const uint32_t p = mpos + q;
+                  uint32_t sc, lc;
+                  if (c8) {
+                    sc = T->sig8x8[p];
+                    lc = T->last8x8[p];
+                  } else if (cat == 3) {
+                    sc = lc = min(p / numc, 2u);
+                  } else {
+                    sc = lc = p;
+                  }
+                  const int sig = (mask >> q) & 1;
+                  put_dec(sig, sb + sc, 1);
+                  if (sig) put_dec(q == lastq, lb + lc, 2);
+                }
+              } else if (cat == 5 || cat == 9 || cat == 13) {
+                seg_loop(std::integral_constant<int, 2>());
+              } else if (cat == 3) {
+                seg_loop(std::integral_constant<int, 1>());
+              } else {
+                seg_loop(std::integral_constant<int, 0>());
               }
               if (npos != 16 || ended) {   // the map's last segment: its block's levels follow
                 mpos = 0;
@@ -2537,10 +2585,14 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
               put_dec(absl > 1, ab + (gt1 ? 0u : min(4u, 1 + eq1)), 0);
               if (absl > 1) {
                 const uint32_t c1 = ab + 5 + min(4u - (cat == 3), gt1);
-                for (uint32_t a = 2; a < 15; a++) {
-                  const int more = a < absl;
-                  put_dec(more, c1, 0);
-                  if (!more) break;
+                if constexpr (SEQ) {
+                  put_run(c1, absl - 2, absl < 15);   // one context: its state stays in a register
+                } else {
+                  for (uint32_t a = 2; a < 15; a++) {
+                    const int more = a < absl;
+                    put_dec(more, c1, 0);
+                    if (!more) break;
+                  }
                 }
               }
               if (absl < 15) put_byp((int)sg, 0);
@@ -2550,10 +2602,23 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
               const uint32_t base = (op & 32) ? 47u : 40u, sg = (op >> 8) & 1, am = (op >> 9) & 15;
               put_dec(am > 0, base + ((op >> 6) & 3), 0);
               if (am > 0) {
-                for (uint32_t m = 1; m < 9; m++) {
+                // bins m = 1, 2, 3 on contexts base + 3, 4, 5, then m = 4 .. 8 on base + 6
+                uint32_t m = 1;
+                for (; m < 4; m++) {
                   const int more = m < am;
-                  put_dec(more, base + min(m + 2, 6u), 0);
+                  put_dec(more, base + m + 2, 0);
                   if (!more) break;
+                }
+                if (m == 4) {
+                  if constexpr (SEQ) {
+                    put_run(base + 6, min(am, 9u) - 4, am < 9);
+                  } else {
+                    for (; m < 9; m++) {
+                      const int more = m < am;
+                      put_dec(more, base + 6, 0);
+                      if (!more) break;
+                    }
+                  }
                 }
                 if (am < 9) put_byp((int)sg, 0);
               }
@@ -2807,7 +2872,7 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
     const int wave = tid >> 6;
     if (wave == 0) walker_slice(w, d, in, &res[s]);
     else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
-    else coder_slice<MODE, false>(w.sh, w.T, d, out, flags);
+    else coder_slice<MODE, false, true>(w.sh, w.T, d, out, flags);
     __syncthreads();
     if (tid == 0) finish_slice<MODE>(w.sh, d, &res[s]);
     __syncthreads();
