@@ -1700,6 +1700,17 @@ struct avr_hooks_session {
   std::vector<std::vector<uint8_t>> blocks;
   std::vector<int32_t> block_status;
   int model = 0;
+  // decompress of a parallel-model container, on demand: the container's plan (every coded slice's
+  // re-coded block) is made at begin, and a slice is regenerated on the device -- with the coded
+  // slices after it that are not yet, up to kLazyBatch -- when init_decoder reaches it; its bins
+  // are traced from the regenerated payload (recode.cpp:1435-1449 decodes each bin as FFmpeg asks)
+  bool lazy = false;
+  DecJob job;
+  Plan dplan;
+  std::vector<int> plan_of;          // per slice: its dplan index (-1: not coded)
+  std::vector<int> block_of;         // per slice: its container block
+  std::vector<char> regen_done;
+  std::vector<std::vector<uint8_t>> regen;   // per slice: its regenerated payload (last-byte patched)
   std::string err;
   void fail_once(const std::string& m) {
     if (err.empty()) err = m;
@@ -1726,8 +1737,6 @@ int trace_slices(avr_hooks_session* hs, const std::vector<int>& which) {
     append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
     d.payload_size = (uint32_t)s.size;
     d.read_limit = (uint32_t)s.read_limit;
-    // 2 bytes per bin; H.264 bounds the bins of a slice by ~32/3 per payload byte plus a
-    // per-macroblock allowance (7.4.2.2), well inside this
     // 2 bytes per bin (H.264 bounds a slice's bins by ~32/3 per payload byte plus a per-macroblock
     // allowance, 7.4.2.2) and 12 bytes of map events per residual block (<= 51 per macroblock)
     d.out_capacity = (uint32_t)std::min<uint64_t>(
@@ -1935,6 +1944,49 @@ int stream_device_work(avr_hooks_session* hs, size_t i) {
   return AVR_OK;
 }
 
+// Lazy decompress session: regenerate the coded slices from i on that are not yet (at most
+// kLazyBatch, one device launch), patch each by the last-byte rule (recode.cpp:1345-1356) and put
+// the regenerated payload in place of the surrogate one; trace = also trace them (init_decoder).
+constexpr size_t kLazyBatch = 32;
+int lazy_device_work(avr_hooks_session* hs, size_t i, bool trace, size_t batch = kLazyBatch) {
+  std::vector<int> which;
+  for (size_t k = i; k < hs->pf.slices.size() && which.size() < batch; k++)
+    if (hs->coded[k] && !hs->regen_done[k]) which.push_back((int)k);
+  if (which.empty()) return AVR_OK;
+  Plan sub;
+  for (const int k : which) {
+    avr_slice_desc d = hs->dplan.descs[hs->plan_of[k]];
+    append_aligned(&sub.arena, hs->dplan.arena.data() + d.payload_offset, d.payload_size, 16, &d.payload_offset);
+    sub.max_w = std::max(sub.max_w, ring_cols(d));
+    sub.descs.push_back(d);
+  }
+  std::vector<avr_slice_result> res;
+  std::vector<uint8_t> outb;
+  if (int r = run_plan(hs->c, 1, false, sub, &res, &outb, false, coder_flag(hs->model))) return r;
+  for (size_t q = 0; q < which.size(); q++) {
+    const int k = which[q];
+    if (res[q].status != 0)
+      return fail(hs->c, AVR_ERR_FORMAT, "slice " + std::to_string(k) + " failed to decode (" +
+                                             std::to_string(res[q].status) + ")");
+    std::vector<uint8_t>& g = hs->regen[k];
+    g.assign(outb.begin() + sub.descs[q].out_offset, outb.begin() + sub.descs[q].out_offset + res[q].out_len);
+    const avr::PbBlock& b = hs->job.blocks[hs->block_of[k]];
+    if (b.has_parity && b.has_last_byte && !b.last_byte.empty()) {   // as splice_job
+      if ((int)b.length_parity != (int)(g.size() & 1)) g.push_back((uint8_t)b.last_byte[0]);
+      else if (!g.empty()) g.back() = (uint8_t)b.last_byte[0];
+    }
+    // the regenerated payload in place of the surrogate one; the NAL's bytes after the payload
+    // (from the literal that follows the block) stay, as does the parse's read limit
+    avr::SliceInfo& s = hs->pf.slices[k];
+    if (g.size() != s.size || s.rbsp.size() < s.h.cabac_start + s.size)
+      return fail(hs->c, AVR_ERR_FORMAT, "slice " + std::to_string(k) + " regenerated " + std::to_string(g.size()) +
+                                             " bytes for a " + std::to_string(s.size) + "-byte payload");
+    std::copy(g.begin(), g.end(), s.rbsp.begin() + s.h.cabac_start);
+    hs->regen_done[k] = 1;
+  }
+  return trace ? trace_slices(hs, which) : AVR_OK;
+}
+
 // which slices of the file a container re-codes: the i-th non-literal block is slice i's
 bool coded_from_container(const std::vector<avr::PbBlock>& blocks, size_t n_slices, std::vector<char>* coded) {
   coded->assign(n_slices, 0);
@@ -2032,6 +2084,47 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
   std::unique_ptr<avr_hooks_session> hs(new avr_hooks_session);
   hs->c = c;
   hs->decompress = true;
+  {
+    std::vector<avr::PbBlock> probe;
+    std::string version;
+    const int m = avr::pb_parse(avrc, n, &probe, &version) ? avr::model_of_version(version) : 0;
+    if (parallel_model(m) && !getenv("AVR_HOOKS_EAGER")) {
+      // the parallel model's slices are independent: plan the container now, regenerate on demand
+      if (int r = guarded(c, [&]() -> int {
+            hs->lazy = true;
+            hs->model = m;
+            hs->original.assign(avrc, avrc + n);   // the container (the job's blocks point into it)
+            if (int e = decompress_setup(c, hs->original.data(), hs->original.size(), &hs->job, &hs->dplan)) return e;
+            hs->stream = hs->job.stream;
+            if (int e = parse_file(c, hs->stream.data(), hs->stream.size(), &hs->pf)) return e;
+            if (!coded_from_container(hs->job.blocks, hs->pf.slices.size(), &hs->coded))
+              return fail(c, AVR_ERR_FORMAT, "hooks: container blocks do not match the file's slices");
+            const size_t ns = hs->pf.slices.size();
+            hs->plan_of.assign(ns, -1);
+            hs->block_of.assign(ns, -1);
+            size_t i = 0;
+            for (size_t bi = 0; bi < hs->job.blocks.size(); bi++) {
+              if (hs->job.blocks[bi].has_literal) continue;
+              hs->block_of[i] = (int)bi;
+              if (hs->job.blocks[bi].has_cabac) hs->plan_of[i] = hs->job.desc_of_block[bi];
+              i++;
+            }
+            for (size_t k = 0; k < ns; k++)
+              if (hs->coded[k] && hs->plan_of[k] < 0) return fail(c, AVR_ERR_FORMAT, "hooks: a coded block has no plan slice");
+            hs->regen_done.assign(ns, 0);
+            hs->regen.assign(ns, {});
+            hs->bins.assign(ns, {});
+            hs->maps.assign(ns, {});
+            hs->slices.resize(ns);
+            return AVR_OK;
+          }))
+        return r;
+      if (stream) *stream = hs->stream.data();
+      if (stream_len) *stream_len = hs->stream.size();
+      *out = hs.release();
+      return AVR_OK;
+    }
+  }
   uint8_t* orig = nullptr;
   size_t orig_len = 0;
   if (int r = avr_decompress_file(c, avrc, n, &orig, &orig_len)) return r;
@@ -2125,6 +2218,10 @@ void* avr_hook_init_decoder(void* opaque, void* /*cabac_context*/, const uint8_t
     }
   }
   if (!hs->coded[i]) return nullptr;  // not re-coded: decode natively (recode.cpp:1139-1145)
+  if (hs->lazy && !hs->regen_done[i] && guarded(hs->c, [&] { return lazy_device_work(hs, i, true); }) != AVR_OK) {
+    hs->fail_once("hooks: device decode of slice " + std::to_string(i) + " failed: " + hs->c->err);
+    return nullptr;
+  }
   if (hs->decompress) {
     // recognize_coded_block (recode.cpp:1546-1573)
     uint8_t mk[8];
@@ -2314,6 +2411,27 @@ int avr_hooks_end(avr_hooks_session* hs, uint8_t** out, size_t* out_len) {
       free(avrc);
     }
   }
+  if (hs->lazy && hs->err.empty()) {
+    // the original file: literals and regenerated slices in block order (decompressor::run's output,
+    // recode.cpp:1338-1357), slices no init_decoder reached regenerated now
+    if (int r = guarded(hs->c, [&]() -> int {
+          if (int e = lazy_device_work(hs, 0, false, hs->pf.slices.size())) return e;
+          std::vector<uint8_t> o;
+          o.reserve(hs->stream.size());
+          size_t i = 0;
+          for (const avr::PbBlock& b : hs->job.blocks) {
+            if (b.has_literal) {
+              o.insert(o.end(), b.literal, b.literal + b.literal_len);
+              continue;
+            }
+            if (b.has_cabac) o.insert(o.end(), hs->regen[i].begin(), hs->regen[i].end());
+            i++;
+          }
+          hs->result.swap(o);
+          return AVR_OK;
+        }))
+      return r;
+  }
   if (hs->next_slice != hs->pf.slices.size())
     hs->fail_once("hooks: " + std::to_string(hs->next_slice) + " of " + std::to_string(hs->pf.slices.size()) +
                   " slices were decoded");
@@ -2326,6 +2444,17 @@ int avr_hooks_end(avr_hooks_session* hs, uint8_t** out, size_t* out_len) {
 }
 
 void avr_hooks_destroy(avr_hooks_session* hs) { delete hs; }
+
+// Debug (tests, host only; not part of include/avrecode.h): how many slices a decompress session
+// has regenerated on the device so far (a lazy parallel-model session: those init_decoder reached,
+// in batches; -1: an eager session, which regenerated the whole file at begin).
+extern "C" int avr_debug_hooks_regenerated(const avr_hooks_session* hs) {
+  if (!hs || !hs->decompress) return AVR_ERR_INVALID_ARGUMENT;
+  if (!hs->lazy) return -1;
+  int k = 0;
+  for (const char d : hs->regen_done) k += d ? 1 : 0;
+  return k;
+}
 
 // Debug (tests, host only; not part of include/avrecode.h): the slices a streaming session's
 // incremental parser finds when `file` is fed in pieces ending at cuts[0] < ... < cuts[ncuts - 1] = n

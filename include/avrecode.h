@@ -299,7 +299,12 @@ typedef enum {
 int avr_hooks_compress_begin(avr_ctx* ctx, const uint8_t* file, size_t n, int model, avr_hooks_session** out);
 /* decompressor(input, out) (recode.cpp:1312-1336): avrc = a Recoded container.  *stream is what
  * read_packet feeds the decoder (literals + surrogate blocks, recode.cpp:1359-1409), valid until
- * avr_hooks_destroy. */
+ * avr_hooks_destroy.  A parallel-model container (avrecode-amd:P64 / P32) is decoded on demand, as
+ * the reference decodes each slice when the decoder reaches it (recode.cpp:1411-1520): begin only
+ * plans it; an avr_hook_init_decoder that reaches a slice not yet regenerated regenerates it on
+ * the device together with at most 31 coded slices after it, and avr_hooks_end regenerates the
+ * rest for the output file.  A reference-model container is regenerated whole at begin (its
+ * estimators chain across slices).  AVR_HOOKS_EAGER=1 in the environment: always whole. */
 int avr_hooks_decompress_begin(avr_ctx* ctx, const uint8_t* avrc, size_t n, avr_hooks_session** out,
                                const uint8_t** stream, size_t* stream_len);
 /* Streaming compress: the caller's demuxer hands the file's bytes to the session as it reads them

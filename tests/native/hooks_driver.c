@@ -9,6 +9,7 @@
  * Built by tests/test_hooks.py into tests/native/_build/libhooks_driver.so.
  */
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -47,6 +48,14 @@ static long g_ntimes, g_captimes;
 int hooks_slice_times(double *out, int cap) {
   for (long i = 0; i < g_ntimes && i < cap; i++) out[i] = g_times[i];
   return (int)g_ntimes;
+}
+/* per slice of the last drive(): avr_debug_hooks_regenerated after its init_decoder (decompress) */
+int avr_debug_hooks_regenerated(const avr_hooks_session *hs);
+static long *g_regen;
+static long g_nregen, g_capregen;
+int hooks_slice_regen(long *out, int cap) {
+  for (long i = 0; i < g_nregen && i < cap; i++) out[i] = g_regen[i];
+  return (int)g_nregen;
 }
 static double now_s(void) {
   struct timespec t;
@@ -121,6 +130,7 @@ static long drive(const uint8_t *stream, size_t n) {
   long walked = 0;
   memset(&prev, 0, sizeof(prev));
   g_ntimes = 0;
+  g_nregen = 0;
   for (int i = 0; i < nn; i++) {
     const uint8_t *nal = stream + nals[i].offset;
     size_t len = nals[i].size;
@@ -158,6 +168,11 @@ static long drive(const uint8_t *stream, size_t n) {
     m_frame_spec(NULL, g_syntax_fn ? h.frame_num : picture_id, h.mb_width, h.mb_height);
     feed_to(nals[i].offset + nals[i].size);
     void *slice = avr_hook_init_decoder(g_session, NULL, rbsp + h.cabac_start, (int)size);
+    if (g_nregen == g_capregen) {
+      g_capregen = g_capregen ? 2 * g_capregen : 1024;
+      g_regen = (long *)realloc(g_regen, sizeof(long) * (size_t)g_capregen);
+    }
+    g_regen[g_nregen++] = avr_debug_hooks_regenerated(g_session);
     if (slice) {
       avr_hooks_t hk = {slice, fwd_get, fwd_bypass, fwd_terminate, m_frame_spec, m_mb_xy,
                         m_begin_sub, m_end_sub, m_begin_ct, m_end_ct};
@@ -245,6 +260,7 @@ int hooks_decompress(const uint8_t *avrc, size_t n, uint8_t **out, size_t *out_l
   g_session = s;
   *walked = drive(stream, stream_len);
   r = avr_hooks_end(s, out, out_len);
+  if (r) fprintf(stderr, "hooks_decompress: %s\n", avr_last_error(c));
   avr_hooks_destroy(s);
   avr_destroy(c);
   return *walked < 0 ? -100 + (int)*walked : r;

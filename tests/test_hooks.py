@@ -41,7 +41,7 @@ def driver_path():
 def test_hooks_driver_builds_and_links():
     """CPU: the driver compiles against include/avrecode.h and links every avr_hook_* symbol."""
     L = ctypes.CDLL(str(driver_path()))
-    assert L.hooks_compress and L.hooks_decompress and L.hooks_compress_stream
+    assert L.hooks_compress and L.hooks_decompress and L.hooks_compress_stream and L.hooks_slice_regen
 
 
 def _driver():
@@ -80,6 +80,36 @@ def test_hooks_compress_then_decompress(name, mode, model):
     assert r == 0, r
     assert walked_d == walked
     assert back == data
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", [0, 1, 2], ids=["R", "P64", "P32"])
+def test_hooks_decompress_on_demand(model):
+    """A parallel-model container through the hooks is decoded on demand, as the reference's
+    decompressor decodes each slice when FFmpeg reaches it (recode.cpp:1411-1520): nothing is
+    regenerated before the first init_decoder, each init_decoder that reaches a slice not yet
+    regenerated runs one device batch (that slice and at most 31 coded slices after it), and
+    avr_hooks_end still returns the original file.  A reference-model container is regenerated
+    whole at begin (its estimators chain across slices): the debug count reads -1 there."""
+    data = (FIX / "cockatoo.mp4").read_bytes()
+    r, avrc, walked = _call("hooks_compress", data, len(data), model)
+    assert r == 0, r
+    r, back, walked_d = _call("hooks_decompress", avrc, len(avrc))
+    assert r == 0, r
+    assert back == data and walked_d == walked
+    L, _ = _driver()
+    buf = (ctypes.c_long * 4096)()
+    n = L.hooks_slice_regen(buf, 4096)
+    regen = list(buf[:n])
+    assert n == 280   # cockatoo's slices, one init_decoder each
+    if model == 0:
+        assert set(regen) == {-1}
+        return
+    assert 0 < regen[0] <= 32
+    assert regen == sorted(regen)
+    assert regen[-1] == walked   # every re-coded slice, the last ones reached at the end
+    steps = [b - a for a, b in zip(regen, regen[1:]) if b != a]
+    assert steps and max(steps) <= 32 and len(steps) >= walked // 32 - 1
 
 
 @pytest.mark.gpu
