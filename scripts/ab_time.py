@@ -31,6 +31,12 @@ with avr.Context(0) as ctx:
         t0 = time.perf_counter(); r = ctx.decompress(avrc); ts.append(time.perf_counter() - t0)
         assert r == data
     out['rmode_cockatoo_decompress_s'] = min(ts)
+    if sys.argv[5] == '1':   # the configs[1] clip in the reference model (one wavefront walks it)
+        import argparse, bench
+        clip = bench.make_clip(ctx, argparse.Namespace(mb_width=120, mb_height=68, seed=0))
+        t0 = time.perf_counter(); a = ctx.compress(clip, avr.MODEL_REFERENCE); out['rmode_clip_compress_s'] = time.perf_counter() - t0
+        t0 = time.perf_counter(); r = ctx.decompress(a); out['rmode_clip_decompress_s'] = time.perf_counter() - t0
+        assert r == clip
     if sys.argv[4] == '1':   # P-mode whole files (latency regime: few slices per CU)
         import argparse, bench
         clip = bench.make_clip(ctx, argparse.Namespace(mb_width=120, mb_height=68, seed=0))
@@ -65,12 +71,13 @@ def main():
     libs = sys.argv[1:]
     batch = os.environ.get("AB_BATCH", "1")
     pfiles = os.environ.get("AB_PFILES", "0")
+    rclip = os.environ.get("AB_RCLIP", "0")
     reps = os.environ.get("AB_REPS", "2")
     res = {l: [] for l in libs}
     for rnd in range(2):
         for lib in (libs if rnd == 0 else libs[::-1]):
             env = dict(os.environ, AVR_LIBRARY=str(Path(lib).resolve()))
-            p = subprocess.run([sys.executable, "-c", CHILD, str(ROOT), reps, batch, pfiles], env=env, capture_output=True,
+            p = subprocess.run([sys.executable, "-c", CHILD, str(ROOT), reps, batch, pfiles, rclip], env=env, capture_output=True,
                                text=True, timeout=600)
             if p.returncode != 0:
                 print(p.stdout, p.stderr[-3000:])
