@@ -54,7 +54,7 @@ EXPORTED_SYMBOLS = (
     "avr_hook_get_bypass", "avr_hook_get_terminate", "avr_hook_skip_bytes", "avr_hook_frame_spec", "avr_hook_mb_xy",
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
     "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables", "avr_last_phase_times",
-    "avr_plan_decompress", "avr_splice_container",
+    "avr_plan_decompress", "avr_splice_container", "avr_roundtrip_files",
 )
 
 # avr_slice_desc / avr_slice_result (include/avrecode.h), C layout
@@ -182,6 +182,7 @@ def lib() -> ctypes.CDLL:
     L.avr_container_describe.argtypes = [vp, sz, pp, pp, psz]
     L.avr_compress_files.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp]
     L.avr_decompress_files.argtypes = [vp, i32, vp, vp, vp, vp, vp]
+    L.avr_roundtrip_files.argtypes = [vp, i32, vp, vp, i32, vp, vp, vp, vp]
     L.avr_neighbor_tables.argtypes = [vp, vp]
     L.avr_plan_decompress.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
     L.avr_splice_container.argtypes = [vp, sz, i32, vp, vp, sz, vp, vp, pp, psz]
@@ -420,7 +421,7 @@ class Context:
             stats[f] = {CODING_TYPES[i]: int(v) for i, v in enumerate(stats[f]) if v}
         return _take(out, olen.value), stats
 
-    def _files(self, fn, datas, *extra):
+    def _files(self, fn, datas, *extra, tail=()):
         n = len(datas)
         keep = [_buf(d) for d in datas]
         ptrs = (ctypes.c_void_p * max(1, n))(*[k[0].value for k in keep])
@@ -428,7 +429,7 @@ class Context:
         outs = (ctypes.c_void_p * max(1, n))()
         olens = (ctypes.c_size_t * max(1, n))()
         st = (ctypes.c_int32 * max(1, n))()
-        self._check(fn(self._h, n, ptrs, lens, *extra, outs, olens, st), fn.__name__)
+        self._check(fn(self._h, n, ptrs, lens, *extra, outs, olens, st, *tail), fn.__name__)
         res = []
         failed = [k for k in range(n) if st[k] != AVR_OK]
         # the context keeps one error message: it belongs to a failed file only when there is one
@@ -454,6 +455,13 @@ class Context:
     def decompress_files(self, datas) -> list:
         """avr_decompress_files: the original file (bytes) or AvrError per container."""
         return self._files(lib().avr_decompress_files, datas)
+
+    def roundtrip_files(self, datas, model: int = MODEL_REFERENCE) -> tuple[list, dict]:
+        """avr_roundtrip_files: (one container (bytes) or AvrError per input file, {"compress_s",
+        "decompress_s"}: wall seconds of the batched compress and decompress calls)."""
+        times = (ctypes.c_double * 2)()
+        res = self._files(lib().avr_roundtrip_files, datas, model, tail=(times,))
+        return res, {"compress_s": times[0], "decompress_s": times[1]}
 
     # ------------------------------------------------------- device-resident slice batches
     # All tensor arguments are torch tensors on this context's device (uint8 buffers, and uint8

@@ -1340,6 +1340,85 @@ static int roundtrip_file(avr_ctx* c, const uint8_t* in, size_t n, int model, ui
   return AVR_OK;
 }
 
+// roundtrip_file's two attempts over a corpus: each attempt is one batched compress_files and one
+// batched decompress_files over the files still open.
+static int roundtrip_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* in_len, int model,
+                           uint8_t** out, size_t* out_len, int32_t* status, double* times) {
+  for (int f = 0; f < nf; f++) out[f] = nullptr, out_len[f] = 0, status[f] = AVR_ERR_ROUNDTRIP;
+  double tc = 0, td = 0;
+  std::vector<int> open(nf);
+  for (int f = 0; f < nf; f++) open[f] = f;
+  const bool force_verify = getenv("AVR_ROUNDTRIP_FORCE_VERIFY") != nullptr;   // tests: the second path
+  for (int attempt = parallel_model(model) ? 0 : 1; attempt < 2 && !open.empty(); attempt++) {
+    const int k = (int)open.size();
+    std::vector<const uint8_t*> ins(k);
+    std::vector<size_t> lens(k), clen(k, 0), dlen(k, 0);
+    std::vector<uint8_t*> comp(k, nullptr), dec(k, nullptr);
+    std::vector<int32_t> cst(k, AVR_OK), dst(k, AVR_OK);
+    for (int j = 0; j < k; j++) ins[j] = in[open[j]], lens[j] = in_len[open[j]];
+    auto free_all = [&] {
+      for (int j = 0; j < k; j++) free(comp[j]), free(dec[j]);
+    };
+    const double t0 = now_s();
+    if (int r = compress_files(c, k, ins.data(), lens.data(), model, comp.data(), clen.data(), cst.data(), nullptr,
+                               /*verify=*/attempt > 0)) {
+      free_all();
+      return r;
+    }
+    const double t1 = now_s();
+    // decompress the containers that came out (a file whose compress failed keeps its status)
+    std::vector<int> idx;
+    std::vector<const uint8_t*> cin;
+    std::vector<size_t> cn;
+    for (int j = 0; j < k; j++)
+      if (cst[j] == AVR_OK) idx.push_back(j), cin.push_back(comp[j]), cn.push_back(clen[j]);
+    std::vector<uint8_t*> dout(idx.size(), nullptr);
+    std::vector<size_t> dn(idx.size(), 0);
+    std::vector<int32_t> ds(idx.size(), AVR_OK);
+    if (!idx.empty()) {
+      if (int r = decompress_files(c, (int)idx.size(), cin.data(), cn.data(), dout.data(), dn.data(), ds.data())) {
+        for (uint8_t* p : dout) free(p);
+        free_all();
+        return r;
+      }
+    }
+    for (size_t q = 0; q < idx.size(); q++) dec[idx[q]] = dout[q], dlen[idx[q]] = dn[q], dst[idx[q]] = ds[q];
+    const double t2 = now_s();
+    tc += t1 - t0;
+    td += t2 - t1;
+    std::vector<int> again;
+    for (int j = 0; j < k; j++) {
+      const int f = open[j];
+      const bool same = cst[j] == AVR_OK && dst[j] == AVR_OK && dlen[j] == in_len[f] &&
+                        (in_len[f] == 0 || memcmp(dec[j], in[f], in_len[f]) == 0);
+      free(out[f]);
+      out[f] = nullptr, out_len[f] = 0;
+      if (same && !(attempt == 0 && force_verify)) {
+        out[f] = comp[j], out_len[f] = clen[j], comp[j] = nullptr;
+        status[f] = AVR_OK;
+      } else if (attempt == 0) {
+        again.push_back(f);
+      } else {
+        status[f] = cst[j] != AVR_OK ? cst[j] : AVR_ERR_ROUNDTRIP;
+      }
+    }
+    free_all();
+    open.swap(again);
+  }
+  if (times) times[0] = tc, times[1] = td;
+  for (int f = 0; f < nf; f++)
+    if (status[f] != AVR_OK) fail(c, status[f], "file " + std::to_string(f) + ": compress-decompress roundtrip failed");
+  return AVR_OK;
+}
+int avr_roundtrip_files(avr_ctx* c, int n_files, const uint8_t* const* in, const size_t* in_len, int model,
+                        uint8_t** out, size_t* out_len, int32_t* status, double* times) {
+  if (!c || n_files < 0 || (n_files && (!in || !in_len || !out || !out_len || !status)) || !valid_model(model))
+    return AVR_ERR_INVALID_ARGUMENT;
+  for (int f = 0; f < n_files; f++)
+    if (!in[f]) return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(c, [&] { return roundtrip_files(c, n_files, in, in_len, model, out, out_len, status, times); });
+}
+
 static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int max_w, int max_h,
                  const uint8_t* d_in, uint8_t* d_out, avr_slice_result* d_res, int model, void* stream) {
   if (!c || n < 0 || (n && (!d_desc || !d_in || !d_out || !d_res)) || max_w <= 0 || max_h <= 0 || !valid_model(model))

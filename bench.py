@@ -277,8 +277,10 @@ def file_roundtrips(ctx, args):
 def corpus_section(ctx, args):
     """BASELINE configs[4]: a mixed I/P/B corpus (avrecode_amd/workloads.py: 720p/1080p/4K,
     1/2/4/8/17 slices per frame, IBBP and IP GOPs, 4:2:0/4:2:2/4:4:4, plus the two fixtures) as ONE
-    batch through avr_compress_files + avr_decompress_files, both model modes, every file checked
-    byte-exact.  MB/s = corpus bytes / (compress + decompress wall time, median of reps);
+    batch through avr_roundtrip_files (batched compress + decompress + byte compare of every file,
+    the reference's roundtrip over a corpus; the parallel model's per-slice device check runs only
+    for a file whose first container does not come back), both model modes.
+    MB/s = corpus bytes / (the whole call's wall time, median of reps);
     compression ratio = container bytes / input bytes, P-mode against R-mode (the reference model).
     CPU beside it: the oracle's R-mode roundtrip of every file, one core."""
     import tempfile
@@ -293,16 +295,14 @@ def corpus_section(ctx, args):
         walls, tc, td = [], [], []
         for it in range(1 + args.file_reps):
             t0 = time.perf_counter()
-            outs = ctx.compress_files(datas, model)
-            t1 = time.perf_counter()
-            back = ctx.decompress_files(outs)
+            outs, times = ctx.roundtrip_files(datas, model)   # compress, decompress, compare every file
             t2 = time.perf_counter()
-            assert back == datas, f"corpus {tag}: decompress did not restore every file"
+            assert all(isinstance(o, bytes) for o in outs), f"corpus {tag}: a file did not come back: {outs}"
             if it == 0 and t2 - t0 < 2.0:
                 continue   # warm-up
             walls.append(t2 - t0)
-            tc.append(t1 - t0)
-            td.append(t2 - t1)
+            tc.append(times["compress_s"])
+            td.append(times["decompress_s"])
             if t2 - t0 >= 2.0:
                 break
         progress(f"corpus {tag}: {total / walls[0] / 1e6:.2f} MB/s")

@@ -124,6 +124,16 @@ int avr_last_phase_times(const avr_ctx* ctx, avr_phase_times* out);
 /* compress, decompress, compare (recode.cpp:1594-1624).  Returns AVR_ERR_ROUNDTRIP on mismatch. */
 int avr_roundtrip_file(avr_ctx* ctx, const uint8_t* in, size_t n, int model, uint8_t** compressed,
                        size_t* compressed_len, avr_file_stats* stats);
+/* avr_roundtrip_file over a corpus, with the device work of all files batched as in
+ * avr_compress_files / avr_decompress_files: every file compressed (the parallel model without its
+ * per-slice device check), every container decompressed and compared with its input; the files
+ * that do not come back are compressed again with the check, decompressed and compared again.
+ * out[f] / out_len[f]: file f's container (malloc'd, avr_free; NULL when it failed), status[f]: its
+ * result (AVR_ERR_ROUNDTRIP when even the checked container does not restore it).  times (optional,
+ * 2 entries): wall seconds of the compress and the decompress calls, summed over attempts.  Returns
+ * AVR_OK unless the batch as a whole failed. */
+int avr_roundtrip_files(avr_ctx* ctx, int n_files, const uint8_t* const* in, const size_t* in_len, int model,
+                        uint8_t** out, size_t* out_len, int32_t* status, double* times);
 
 /* ------------------------------------------------------- slice batches (device-resident data) */
 /* One CABAC slice: the (buf, size) FFmpeg hands to AVCodecHooks.cabac.init_decoder

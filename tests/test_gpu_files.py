@@ -79,6 +79,24 @@ def test_mixed_models_and_error_isolation(ctx):
     assert outs[0] == r[0] and outs[2] == r[2] and isinstance(outs[1], avr.AvrError)
 
 
+@pytest.mark.parametrize("force_verify", [False, True])
+@pytest.mark.parametrize("mode,model", MODELS + (("P32", avr.MODEL_PARALLEL32),))
+def test_roundtrip_files(ctx, monkeypatch, mode, model, force_verify):
+    """avr_roundtrip_files: the unchecked first pass (or, forced, the checked second one) gives
+    every file the container avr_compress_files gives it, and a file that cannot be compressed
+    fails alone."""
+    if force_verify:
+        monkeypatch.setenv("AVR_ROUNDTRIP_FORCE_VERIFY", "1")
+    files = _small_corpus(ctx)
+    datas = [d for _, d in files]
+    want = ctx.compress_files(datas, model)
+    outs, times = ctx.roundtrip_files(datas + [b"not h264 at all"], model)
+    assert outs[:-1] == want, mode
+    assert isinstance(outs[-1], avr.AvrError)
+    assert times["compress_s"] > 0 and times["decompress_s"] > 0
+    assert ctx.decompress_files(outs[:-1]) == datas
+
+
 def test_corpus_generator_structure(ctx):
     files = workloads.corpus(ctx, scale=0.25, fixtures=False)
     assert [n for n, _ in files] == [c[0] for c in workloads.CORPUS]
