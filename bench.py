@@ -632,8 +632,8 @@ def p32_extra(batch, args, stream, mk, n_bytes, C64):
 
 def corpus_sharded(ctx, args, world, rank, dev):
     """BASELINE configs[4] on N GPUs: the corpus's files dealt whole to the ranks (shard.deal_files,
-    LPT by bytes) and each rank's files run as one batch per model (avr_compress_files +
-    avr_decompress_files, byte-checked).  No collective in the timed region; MB/s = corpus bytes /
+    LPT by bytes) and each rank's files run as one batch per model (avr_roundtrip_files: compress,
+    decompress and byte compare, as the N = 1 corpus leg).  No collective in the timed region; MB/s = corpus bytes /
     max-over-ranks wall time.  The reference model runs here as replicas over files (its only
     split)."""
     import torch
@@ -653,9 +653,8 @@ def corpus_sharded(ctx, args, world, rank, dev):
             t0 = time.perf_counter()
             ok = True
             if datas:
-                outs = ctx.compress_files(datas, model)
-                back = ctx.decompress_files(outs)
-                ok = back == datas
+                outs, _ = ctx.roundtrip_files(datas, model)   # compress, decompress, compare
+                ok = all(isinstance(o, bytes) for o in outs)
             dt = time.perf_counter() - t0
             mx = torch.tensor([dt], dtype=torch.float64, device=_coll(dev))
             bad = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=_coll(dev))
