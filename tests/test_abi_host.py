@@ -303,3 +303,27 @@ def test_take_copies_buffers_past_2gib():
     ctypes.memset(p + n - 7, 0x33, 7)
     b = avr._take(ctypes.c_void_p(p), n)   # frees p
     assert len(b) == n and b[:4] == b"ZZZZ" and b[-8:] == b"Z" + b"\x33" * 7
+
+
+def test_file_batch_calls_reject_bad_arguments_without_a_device():
+    """avr_compress_files / avr_decompress_files / avr_roundtrip_files check their arguments
+    before touching a context: a NULL context, a negative count or a NULL input is
+    AVR_ERR_INVALID_ARGUMENT (-1), on any host."""
+    import ctypes
+    L = avr.lib()
+    buf = ctypes.create_string_buffer(b"x" * 16)
+    ins = (ctypes.c_void_p * 1)(ctypes.cast(buf, ctypes.c_void_p).value)
+    lens = (ctypes.c_size_t * 1)(16)
+    outs = (ctypes.c_void_p * 1)()
+    olens = (ctypes.c_size_t * 1)()
+    st = (ctypes.c_int32 * 1)()
+    times = (ctypes.c_double * 2)()
+    assert L.avr_roundtrip_files(None, 1, ins, lens, avr.MODEL_PARALLEL, outs, olens, st, times) == -1
+    assert L.avr_compress_files(None, 1, ins, lens, avr.MODEL_PARALLEL, outs, olens, st) == -1
+    assert L.avr_decompress_files(None, 1, ins, lens, outs, olens, st) == -1
+    fake = ctypes.c_void_p(1)   # never dereferenced: the argument checks fail first
+    assert L.avr_roundtrip_files(fake, -1, ins, lens, avr.MODEL_PARALLEL, outs, olens, st, times) == -1
+    assert L.avr_roundtrip_files(fake, 1, ins, lens, 7, outs, olens, st, times) == -1
+    assert L.avr_roundtrip_files(fake, 1, ins, lens, avr.MODEL_PARALLEL, outs, olens, None, times) == -1
+    nul = (ctypes.c_void_p * 1)()
+    assert L.avr_roundtrip_files(fake, 1, nul, lens, avr.MODEL_PARALLEL, outs, olens, st, times) == -1
