@@ -10,6 +10,7 @@
  *   avr_decompress_file  decompressor(...).run()         recode.cpp:1312-1357, 1359-1409, 1527-1573
  *   avr_roundtrip_file   roundtrip(input, out)           recode.cpp:1594-1624
  *   avr_compress_files / avr_decompress_files  the two runs above over a corpus of files at once
+ *   avr_roundtrip_files  roundtrip() over a corpus of files at once
  *   avr_compress_slices  compressor::cabac_decoder x N    recode.cpp:1134-1268 (+ h264_model 615-1059,
  *                        (one CABAC slice per wavefront)  h264_symbol::execute 1061-1100,
  *                                                         arithmetic_code.h encoder 89-203)
@@ -124,8 +125,8 @@ int avr_last_phase_times(const avr_ctx* ctx, avr_phase_times* out);
 /* compress, decompress, compare (recode.cpp:1594-1624).  Returns AVR_ERR_ROUNDTRIP on mismatch. */
 int avr_roundtrip_file(avr_ctx* ctx, const uint8_t* in, size_t n, int model, uint8_t** compressed,
                        size_t* compressed_len, avr_file_stats* stats);
-/* avr_roundtrip_file over a corpus, with the device work of all files batched as in
- * avr_compress_files / avr_decompress_files: every file compressed (the parallel model without its
+/* avr_roundtrip_file (roundtrip(), recode.cpp:1594-1624) over a corpus, with the device work of
+ * all files batched as in avr_compress_files / avr_decompress_files: every file compressed (the parallel model without its
  * per-slice device check), every container decompressed and compared with its input; the files
  * that do not come back are compressed again with the check, decompressed and compared again.
  * out[f] / out_len[f]: file f's container (malloc'd, avr_free; NULL when it failed), status[f]: its
