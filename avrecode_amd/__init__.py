@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "avr_create", "avr_destroy", "avr_last_error", "avr_free", "avr_compress_file", "avr_decompress_file",
     "avr_roundtrip_file", "avr_compress_slices", "avr_decompress_slices", "avr_pack_outputs",
     "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream",
-    "avr_assemble_container", "avr_assemble_container_parsed", "avr_container_model", "avr_synthesize_stream",
+    "avr_assemble_container", "avr_assemble_container_parsed", "avr_assemble_container_into", "avr_container_model", "avr_synthesize_stream",
     "avr_container_describe", "avr_compress_files", "avr_decompress_files",
     "avr_hooks_compress_begin", "avr_hooks_compress_stream_begin", "avr_hooks_feed",
     "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
@@ -65,13 +65,14 @@ SLICE_DESC = np.dtype([
     ("mb_width", "<i4"), ("mb_height", "<i4"), ("num_ref_idx_l0", "<i4"), ("num_ref_idx_l1", "<i4"),
     ("chroma_array_type", "<i4"), ("transform_8x8_mode", "<i4"), ("direct_8x8_inference", "<i4"),
     ("x264_build", "<i4"), ("picture_id", "<i4"), ("coded", "<i4"), ("structure", "<i4"),
+    ("file_offset", "<u8"),
 ], align=True)
 SLICE_RESULT = np.dtype([("out_len", "<u4"), ("status", "<i4"), ("bins", "<u4"), ("mbs", "<u4"),
                          ("bill", "<u4", (6,))], align=True)
 # avr_pip_coding_type (CodingType, recode.cpp:616): the index of avr_file_stats.bill / cabac_bill
 CODING_TYPES = ("PIP_UNKNOWN", "PIP_UNREACHABLE", "PIP_SIGNIFICANCE_MAP", "PIP_SIGNIFICANCE_EOB",
                 "PIP_SIGNIFICANCE_NZ", "PIP_RESIDUALS")
-assert SLICE_DESC.itemsize == 88 and SLICE_RESULT.itemsize == 40
+assert SLICE_DESC.itemsize == 96 and SLICE_RESULT.itemsize == 40
 
 
 class AvrError(RuntimeError):
@@ -177,6 +178,7 @@ def lib() -> ctypes.CDLL:
     L.avr_parse_stream.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
     L.avr_assemble_container.argtypes = [vp, sz, i32, i32, vp, vp, sz, vp, vp, pp, psz]
     L.avr_assemble_container_parsed.argtypes = [vp, sz, i32, vp, i32, vp, sz, vp, vp, sz, vp, vp, pp, psz]
+    L.avr_assemble_container_into.argtypes = [vp, sz, i32, vp, i32, vp, sz, vp, vp, sz, vp, vp, vp, sz, psz]
     L.avr_container_model.argtypes = [vp, sz, pi]
     L.avr_synthesize_stream.argtypes = [vp, ctypes.POINTER(_SynthParams), i32, pp, psz]
     L.avr_container_describe.argtypes = [vp, sz, pp, pp, psz]
@@ -220,16 +222,28 @@ def _take(p: ctypes.c_void_p, n: int) -> bytes:
         L.avr_free(p)
 
 
+class _LibBuffer:
+    """A malloc'd library buffer exposed to numpy without a copy; freed (avr_free) when the last
+    array viewing it is gone (numpy keeps this object as every view's base)."""
+
+    def __init__(self, p: int, n: int):
+        self._p = p
+        self.__array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (p, False), "version": 3}
+
+    def __del__(self):
+        if self._p:
+            lib().avr_free(ctypes.c_void_p(self._p))
+            self._p = 0
+
+
 def _take_array(p: ctypes.c_void_p, n: int) -> np.ndarray:
-    """A library buffer as a numpy uint8 array: one copy, then the buffer is freed."""
-    L = lib()
-    try:
-        a = np.empty(n, dtype=np.uint8)
-        if n:
-            ctypes.memmove(a.ctypes.data, p.value, n)
-        return a
-    finally:
-        L.avr_free(p)
+    """A library buffer as a numpy uint8 array, without copying it (a 4 GB parse or container is not
+    copied again); the buffer is freed with the array."""
+    if not n or not p.value:
+        if p.value:
+            lib().avr_free(p)
+        return np.zeros(0, dtype=np.uint8)
+    return np.asarray(_LibBuffer(p.value, n))
 
 
 @dataclass
@@ -308,31 +322,53 @@ def splice_container(avrc, status: np.ndarray, regen, offsets: np.ndarray, lens:
     return _take(out, olen.value)
 
 
+def container_bound(n_file: int, n_slices: int, recoded_bytes: int) -> int:
+    """An upper bound on the size of a container assembled from n_slices slices of a file of n_file
+    bytes with recoded_bytes re-coded bytes in all (avr_assemble_container_into's buffer)."""
+    return int(n_file) + int(recoded_bytes) + 64 * (int(n_slices) + 2)
+
+
 def assemble_container(data, status: np.ndarray, recoded, offsets: np.ndarray, lens: np.ndarray,
-                       model: int = MODEL_PARALLEL, ps: "ParsedStream | None" = None) -> bytes:
+                       model: int = MODEL_PARALLEL, ps: "ParsedStream | None" = None, as_array: bool = False,
+                       out: "np.ndarray | None" = None):
     """PARALLEL-model Recoded container from per-slice outputs (avr_assemble_container; with ps =
     parse_stream(data) already in hand, avr_assemble_container_parsed: no second parse).  recoded:
-    bytes or a uint8 array.  model: the coder the outputs were made with.  Host only."""
+    bytes or a uint8 array.  model: the coder the outputs were made with.  as_array: the container
+    as a uint8 array over the library's buffer (no copy into bytes).  out (with ps): a uint8 array
+    the container is written into (avr_assemble_container_into; container_bound() bytes suffice);
+    returns the view of it that holds the container.  Host only."""
     L = lib()
     p, n, keep = _buf(data)
     st = np.ascontiguousarray(status, dtype=np.int32)
     of = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lens, dtype=np.uint32)
     rp, rn, keep2 = _buf(recoded)
-    out, olen = ctypes.c_void_p(), ctypes.c_size_t()
+    res, olen = ctypes.c_void_p(), ctypes.c_size_t()
+    if out is not None:
+        if ps is None or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            raise ValueError("assemble_container: out needs ps and a contiguous uint8 array")
+        dd = np.ascontiguousarray(ps.descs)
+        if len(dd) != len(st) or len(of) != len(st) or len(ln) != len(st):
+            raise ValueError("assemble_container: status / offsets / lens need one entry per parsed slice")
+        r = L.avr_assemble_container_into(p, n, model, dd.ctypes.data, len(dd), ps.arena.ctypes.data, ps.arena.nbytes,
+                                          st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data, out.ctypes.data,
+                                          out.nbytes, ctypes.byref(olen))
+        if r != AVR_OK:
+            raise AvrError(r, f"avr_assemble_container_into failed (container {olen.value} B, buffer {out.nbytes} B)")
+        return out[:olen.value]
     if ps is not None:
         dd = np.ascontiguousarray(ps.descs)
         if len(dd) != len(st) or len(of) != len(st) or len(ln) != len(st):
             raise ValueError("assemble_container: status / offsets / lens need one entry per parsed slice")
         r = L.avr_assemble_container_parsed(p, n, model, dd.ctypes.data, len(dd), ps.arena.ctypes.data, ps.arena.nbytes,
-                                            st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data, ctypes.byref(out),
+                                            st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data, ctypes.byref(res),
                                             ctypes.byref(olen))
     else:
         r = L.avr_assemble_container(p, n, model, len(st), st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data,
-                                     ctypes.byref(out), ctypes.byref(olen))
+                                     ctypes.byref(res), ctypes.byref(olen))
     if r != AVR_OK:
         raise AvrError(r, "avr_assemble_container failed")
-    return _take(out, olen.value)
+    return _take_array(res, olen.value) if as_array else _take(res, olen.value)
 
 
 def describe_container(avrc) -> tuple[dict, bytes]:

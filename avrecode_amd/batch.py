@@ -5,7 +5,7 @@ HBM layout of a batch (DESIGN.md "Data layout"):
             >= 16 zero bytes after it) -- exactly what init_decoder receives (recode.cpp:143)
   d_work    re-coded output: slice k at desc[k].out_offset, desc[k].out_capacity bytes reserved
   d_regen   regenerated CABAC bytes, laid out like d_in
-  d_desc / d_dec_desc   avr_slice_desc[n] (88 B each) for compress / derived decompress
+  d_desc / d_dec_desc   avr_slice_desc[n] (96 B each) for compress / derived decompress
   d_res_c / d_res_d     avr_slice_result[n] (40 B each); d_verdict int32[n]
 torch only allocates and owns these buffers and supplies the stream; all compute is in
 libavrecode.so.

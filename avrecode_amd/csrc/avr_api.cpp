@@ -9,15 +9,18 @@
 // The hot path has no host implementation: without a GPU every entry point fails with
 // AVR_ERR_DEVICE.
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <array>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/avrecode.h"
@@ -67,6 +70,7 @@ struct avr_ctx {
   std::string err;
   hipStream_t stream = nullptr;
   DevBuf tables, est, frames, frame_meta, in, out, descs, res, packed, offsets, order;
+  DevBuf queue;                                          // largest-first slice queue (launch_slices)
   DevBuf rm_goff, rm_counts, rm_stop, rm_off, rm_ops;   // parallel reference-model compress
   DevBuf regen, dec_descs, res_d, verdict;               // compress-side roundtrip check
   DevBuf file_first, file_op_off;                        // reference model over several files
@@ -85,8 +89,6 @@ struct avr_ctx {
 };
 
 namespace {
-
-constexpr int kMaxSlicesPerLaunch = 4096;
 
 // Model modes (include/avrecode.h): the reference model, and the parallel model on the reference's
 // arithmetic_code<uint64_t, uint8_t> (PARALLEL) or on the optional 32-bit P32 coder (PARALLEL32).
@@ -287,6 +289,7 @@ avr_slice_desc desc_from_header(const avr::SliceInfo& s) {
   d.x264_build = s.h.x264_build;
   d.picture_id = s.picture_id;
   d.coded = 1;
+  d.file_offset = ~(uint64_t)0;
   d.structure = s.h.field_pic ? (s.h.bottom_field ? AVR_STRUCT_BOTTOM_FIELD : AVR_STRUCT_TOP_FIELD)
               : s.h.mbaff ? AVR_STRUCT_MBAFF : AVR_STRUCT_FRAME;
   return d;
@@ -397,7 +400,17 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
   return AVR_OK;
 }
 
-// Upload plan, run the slice kernel over it (in chunks), download results and outputs.
+// Device scratch of a parallel launch of n slices: the estimator tables (one per slice of a resident
+// batch, one per workgroup of a persistent one: avr::est_slots), the CU schedule and the slice queue.
+hipError_t reserve_parallel(avr_ctx* c, int n, int max_w) {
+  const int slots = std::max(1, avr::est_slots(n, max_w));
+  hipError_t e = c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * slots, true);
+  if (e == hipSuccess) e = c->order.reserve(sizeof(int) * (size_t)std::max(1, n));
+  if (e == hipSuccess) e = c->queue.reserve(std::max<size_t>(256, avr::queue_scratch_bytes(n)));
+  return e;
+}
+
+// Upload plan, run the slice kernel over it (one launch, see launch_slices), download results and outputs.
 // verify (parallel compress only): also decompress every slice's output on the device, apply the
 // last-byte rule and compare with the payload (avr_roundtrip_slices); a slice whose output does not
 // regenerate its payload gets status kStatusNoRoundtrip, so no container ever holds a block that
@@ -456,16 +469,11 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
                                   c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), nullptr,
                                   c->stream, sf, flags));
   } else {
-    const int chunk = std::min(n, kMaxSlicesPerLaunch);
-    HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk, true));
-    HIP_TRY(c, c->order.reserve(sizeof(int) * (size_t)chunk));
-    for (int s0 = 0; s0 < n; s0 += chunk) {
-      const int m = std::min(chunk, n - s0);
-      HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>() + s0,
-                                    m, plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(),
-                                    c->res.as<avr_slice_result>() + s0, c->est.as<uint16_t>(), nullptr, nullptr,
-                                    c->order_or_null(), c->stream, avr::SeqFiles(), flags));
-    }
+    HIP_TRY(c, reserve_parallel(c, n, plan.max_w));
+    HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n,
+                                  plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(), c->res.as<avr_slice_result>(),
+                                  c->est.as<uint16_t>(), nullptr, nullptr, c->order_or_null(), c->stream,
+                                  avr::SeqFiles(), flags, c->queue.p));
   }
   std::vector<int32_t> verdict;
   if (verify && mode == 0 && !sequential) {
@@ -477,14 +485,10 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
     avr_slice_result* rd = c->res_d.as<avr_slice_result>();
     HIP_TRY(c, avr::launch_derive_decompress(c->descs.as<avr_slice_desc>(), c->res.as<avr_slice_result>(), n, dd,
                                              c->stream));
-    const int chunk = std::min(n, kMaxSlicesPerLaunch);
-    for (int s0 = 0; s0 < n; s0 += chunk) {
-      const int m = std::min(chunk, n - s0);
-      HIP_TRY(c, avr::launch_slices(1, false, c->tables.as<avr::EngineTables>(), dd + s0, m, plan.max_w,
-                                    c->out.as<uint8_t>(), c->regen.as<uint8_t>(), rd + s0, c->est.as<uint16_t>(),
-                                    nullptr, nullptr, c->order_or_null(), c->stream, avr::SeqFiles(),
-                                    (plan.fields() ? avr::kFlagFields : 0u) | (flags & avr::kFlagP32)));
-    }
+    HIP_TRY(c, avr::launch_slices(1, false, c->tables.as<avr::EngineTables>(), dd, n, plan.max_w, c->out.as<uint8_t>(),
+                                  c->regen.as<uint8_t>(), rd, c->est.as<uint16_t>(), nullptr, nullptr,
+                                  c->order_or_null(), c->stream, avr::SeqFiles(),
+                                  (plan.fields() ? avr::kFlagFields : 0u) | (flags & avr::kFlagP32), c->queue.p));
     HIP_TRY(c, avr::launch_verify(c->descs.as<avr_slice_desc>(), c->res.as<avr_slice_result>(), rd, n,
                                   c->in.as<uint8_t>(), c->regen.as<uint8_t>(), c->verdict.as<int32_t>(), c->stream));
     verdict.resize(n);
@@ -539,39 +543,65 @@ struct SliceView {
   const uint8_t* payload;
   size_t size;
   bool candidate;
+  uint64_t file_pos;   // where the payload stands verbatim in the file (the parse knows), or ~0
 };
 std::vector<SliceView> views_of(const ParsedFile& pf) {
   std::vector<SliceView> v(pf.slices.size());
-  for (size_t i = 0; i < v.size(); i++) v[i] = {pf.slices[i].payload(), pf.slices[i].size, recodable_candidate(pf.slices[i])};
+  for (size_t i = 0; i < v.size(); i++)
+    v[i] = {pf.slices[i].payload(), pf.slices[i].size, recodable_candidate(pf.slices[i]),
+            pf.slices[i].file_payload_offset()};
   return v;
 }
 
-// The positions p of every 00 00 0y trigram (y <= 3) of a file, by y, ascending.  In an escaped
-// H.264 stream these occur only at start codes, emulation-prevention bytes (00 00 03) and container
-// bytes (MP4 lengths and boxes), so the index is small.
+// Every 00 00 0y trigram (y <= 3) of a file, keyed by y and the four bytes after it, then by
+// position.  In an escaped H.264 stream these occur only at start codes, emulation-prevention bytes
+// (00 00 03) and container bytes (MP4 lengths and boxes), so the index is small.
 struct TrigramIndex {
   bool built = false;
-  std::vector<uint64_t> pos[4];
-  void build(const uint8_t* f, size_t n) {
-    built = true;
-    const uint8_t* e = f + n;
-    for (const uint8_t* p = f; p + 2 < e;) {
-      p = (const uint8_t*)memchr(p, 0, (size_t)(e - 2 - p));
+  struct Entry {
+    uint64_t key;   // y << 32 | the next four bytes (big-endian, zeros past the end)
+    uint64_t pos;
+    bool operator<(const Entry& o) const { return key != o.key ? key < o.key : pos < o.pos; }
+  };
+  std::vector<Entry> e;
+  static uint64_t key_at(const uint8_t* f, size_t n, size_t p) {   // trigram at p (p + 2 < n)
+    uint32_t nx = 0;
+    for (int k = 0; k < 4; k++) nx = nx << 8 | (p + 3 + k < n ? f[p + 3 + k] : 0u);
+    return (uint64_t)f[p + 2] << 32 | nx;
+  }
+  // the trigrams starting in [lo, hi)
+  static void scan(const uint8_t* f, size_t n, size_t lo, size_t hi, std::vector<Entry>* out) {
+    const uint8_t* end = f + std::min(hi, n >= 2 ? n - 2 : 0);
+    for (const uint8_t* p = f + lo; p < end;) {
+      p = (const uint8_t*)memchr(p, 0, (size_t)(end - p));
       if (!p) break;
-      if (p[1] == 0 && p[2] <= 3) pos[p[2]].push_back((uint64_t)(p - f));
+      if (p[1] == 0 && p[2] <= 3) out->push_back({key_at(f, n, (size_t)(p - f)), (uint64_t)(p - f)});
       p++;
     }
+  }
+  void build(const uint8_t* f, size_t n) {
+    built = true;
+    // a multi-GB file is scanned in chunks on host threads
+    const unsigned T = n < ((size_t)256 << 20) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::vector<Entry>> part(T);
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; t++) th.emplace_back(scan, f, n, n * t / T, n * (t + 1) / T, &part[t]);
+    scan(f, n, 0, n / T, &part[0]);
+    for (auto& x : th) x.join();
+    for (auto& v : part) e.insert(e.end(), v.begin(), v.end());
+    std::sort(e.begin(), e.end());
   }
 };
 
 // memmem(in + from, n - from, P, m) (the reference's search, recode.cpp:1285) without its cost on a
 // miss.  A payload P holding a 00 00 0y trigram (y <= 3) at offset j -- an unescaped payload whose
-// NAL had emulation-prevention bytes -- can only occur at q with a trigram of the file at q + j, so
-// the index's trigrams with the same y, in ascending order, are the only candidates and the first
-// that matches is memmem's answer.  Such payloads are exactly the ones that usually occur nowhere,
-// where memmem would scan to the end of the file for each of them (O(misses x file): minutes for a
-// 10-minute 4K stream).  A payload without one is found in its own NAL (its bytes are verbatim
-// there), so memmem stops at most one NAL past `from`.
+// NAL had emulation-prevention bytes -- can only occur at q with a trigram of the file at q + j
+// followed by the same four bytes as in P (when P has them), so the index's entries with that key
+// from position from + j on, in ascending order, are the only candidates and the first that matches
+// is memmem's answer.  Such payloads are exactly the ones that usually occur nowhere, where memmem
+// would scan to the end of the file for each of them (O(misses x file): minutes for a 10-minute 4K
+// stream); with the key a miss costs a binary search.  A payload without one is found in its own
+// NAL (its bytes are verbatim there), so memmem stops at most one NAL past `from`.
 const uint8_t* find_payload(const uint8_t* in, size_t n, size_t from, const uint8_t* P, size_t m, TrigramIndex* ix) {
   size_t j = 0;
   bool anchor = false;
@@ -586,14 +616,61 @@ const uint8_t* find_payload(const uint8_t* in, size_t n, size_t from, const uint
     q++;
   }
   if (!anchor) return (const uint8_t*)memmem(in + from, n - from, P, m);
-  if (!ix->built) ix->build(in, n);
-  const std::vector<uint64_t>& v = ix->pos[P[j + 2]];
-  for (auto it = std::lower_bound(v.begin(), v.end(), (uint64_t)(from + j)); it != v.end(); ++it) {
-    const size_t q = (size_t)*it - j;
-    if (q + m > n) break;
-    if (memcmp(in + q, P, m) == 0) return in + q;
+  if (!ix->built) {
+    const double tb = now_s();
+    ix->build(in, n);
+    if (getenv("AVR_ASM_TIMING")) fprintf(stderr, "index build %.3f s, %zu entries\n", now_s() - tb, ix->e.size());
+  }
+  using E = TrigramIndex::Entry;
+  const bool keyed = j + 7 <= m;   // P holds the four bytes after its trigram
+  const uint64_t key = keyed ? TrigramIndex::key_at(P, m, j) : (uint64_t)P[j + 2] << 32;
+  const uint64_t key_end = keyed ? key : key + ((uint64_t)1 << 32) - 1;
+  for (auto it = std::lower_bound(ix->e.begin(), ix->e.end(), E{key, (uint64_t)(from + j)}); it != ix->e.end(); ++it) {
+    if (it->key > key_end) break;
+    if (!keyed && it->pos < from + j) continue;   // entries of another next-four-bytes key, earlier positions
+    const size_t q = (size_t)it->pos - j;
+    if (q + m > n) {
+      if (keyed) break;
+      continue;
+    }
+    if (memcmp(in + q, P, m) == 0) {
+      if (keyed) return in + q;
+      // the y-only range is sorted by key, not position: keep the smallest match
+      const uint8_t* best = in + q;
+      for (++it; it != ix->e.end() && it->key <= key_end; ++it) {
+        const size_t q2 = (size_t)it->pos - j;
+        if (it->pos >= from + j && q2 + m <= n && in + q2 < best && memcmp(in + q2, P, m) == 0) best = in + q2;
+      }
+      return best;
+    }
   }
   return nullptr;
+}
+
+// memmem(in + from, n - from, P, m) for a payload the parse found verbatim at `own` >= from: memmem's
+// answer is the first occurrence at or after `from` and `own` is one, so only [from, own) -- the
+// literal gap before the slice: start code or length, NAL and slice header, skipped NAL units --
+// needs a search.  Candidates are the gap's bytes equal to P[0] (memchr), each checked on its first
+// 64 bytes and, if those agree, in full; a gap with more than a few such deep candidates (only a
+// degenerate payload has them) goes to memmem over [from, own + m - 1).  O(gap) per slice instead
+// of memmem's O(m) needle preparation plus its scan: the segmentation of a 4 GB stream no longer
+// reads the stream once more.
+const uint8_t* find_before(const uint8_t* in, size_t from, size_t own, const uint8_t* P, size_t m) {
+  const size_t head = std::min<size_t>(m, 64);
+  int deep = 0;
+  for (size_t q = from; q < own;) {
+    const uint8_t* h = (const uint8_t*)memchr(in + q, P[0], own - q);
+    if (!h) break;
+    if (memcmp(h, P, head) == 0) {
+      if (++deep > 4) {
+        const uint8_t* r = (const uint8_t*)memmem(in + from, own - from + m - 1, P, m);
+        return r ? r : in + own;
+      }
+      if (memcmp(h + head, P + head, m - head) == 0) return h;
+    }
+    q = (size_t)(h - in) + 1;
+  }
+  return in + own;
 }
 
 // find_next_coded_block_and_emit_literal (recode.cpp:1275-1297): slice i becomes a cabac block when
@@ -606,7 +683,10 @@ std::vector<const uint8_t*> segment(const uint8_t* in, size_t n, const std::vect
   size_t prev_end = 0;
   for (size_t i = 0; i < sv.size(); i++) {
     if (!ok[i] || sv[i].size < (size_t)avr::kSurrogateMarkerBytes) continue;
-    const uint8_t* f = find_payload(in, n, prev_end, sv[i].payload, sv[i].size, &ix);
+    const uint64_t own = sv[i].file_pos;
+    const uint8_t* f = own != ~(uint64_t)0 && own >= prev_end && own + sv[i].size <= n
+                           ? find_before(in, prev_end, (size_t)own, sv[i].payload, sv[i].size)
+                           : find_payload(in, n, prev_end, sv[i].payload, sv[i].size, &ix);
     if (f) {
       found[i] = f;
       prev_end = (size_t)(f - in) + sv[i].size;
@@ -618,13 +698,55 @@ std::vector<const uint8_t*> segment(const uint8_t* in, size_t n, const ParsedFil
   return segment(in, n, views_of(pf), ok);
 }
 
-// compressor::run's block stream (recode.cpp:1115-1125, 1275-1297) as a Recoded protobuf.
+// A large host output buffer handed to the caller (freed by avr_free = free): 2 MiB aligned and
+// advised to transparent huge pages, so its first touch costs one fault per 2 MiB instead of per
+// 4 KiB page (a 4.4 GB container or payload arena: ~1 s of page faults otherwise).
+uint8_t* host_alloc(size_t n) {
+  constexpr size_t kHuge = (size_t)2 << 20;
+  if (n < 16 * kHuge) return (uint8_t*)malloc(n ? n : 1);
+  void* p = nullptr;
+  if (posix_memalign(&p, kHuge, n)) return nullptr;
+  (void)madvise(p, n & ~(kHuge - 1), MADV_HUGEPAGE);
+  return (uint8_t*)p;
+}
+
+// Byte copies of a container's literals and re-coded blocks, spread over host threads when they are
+// large (a 10-minute 4K stream's container is 4.4 GB).
+void parallel_copies(const std::vector<avr::PbCopy>& jobs, uint8_t* base) {
+  uint64_t total = 0;
+  for (const auto& j : jobs) total += j.len;
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const unsigned T = total < ((uint64_t)64 << 20) ? 1u : hw;
+  if (T == 1) {
+    for (const auto& j : jobs) memcpy(base + j.dst, j.src, j.len);
+    return;
+  }
+  // thread t copies the bytes [t total / T, (t + 1) total / T) of the concatenated jobs
+  auto work = [&](unsigned t) {
+    const uint64_t lo = total * t / T, hi = total * (t + 1) / T;
+    uint64_t at = 0;
+    for (const auto& j : jobs) {
+      const uint64_t a = std::max(at, lo), b = std::min(at + j.len, hi);
+      if (a < b) memcpy(base + j.dst + (a - at), j.src + (a - at), (size_t)(b - a));
+      at += j.len;
+      if (at >= hi) break;
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+}
+
+// compressor::run's block stream (recode.cpp:1115-1125, 1275-1297) as a Recoded protobuf, written
+// once: the blocks' headers in order, their bytes by parallel_copies, into the caller's buffer dst
+// (cap bytes; too small: AVR_ERR_INVALID_ARGUMENT with *out_len = the size needed) or, without one,
+// into one exactly sized buffer allocated here (*out).
 int emit_container(const uint8_t* in, size_t n, const std::vector<SliceView>& sv, const std::vector<const uint8_t*>& found,
                    const std::vector<std::pair<const uint8_t*, size_t>>& recoded, int model, uint8_t** out,
-                   size_t* out_len) {
-  std::vector<uint8_t> o;
-  o.reserve(n + n / 8 + 1024);
-  if (const char* tag = avr::version_of_model(model)) avr::pb_put_metadata_version(&o, tag);
+                   size_t* out_len, uint8_t* dst = nullptr, size_t cap = 0) {
+  std::vector<avr::PbBlock> blocks;
+  blocks.reserve(2 * sv.size() + 1);
   size_t prev_end = 0;
   for (size_t i = 0; i < sv.size(); i++) {
     const SliceView& s = sv[i];
@@ -634,7 +756,7 @@ int emit_container(const uint8_t* in, size_t n, const std::vector<SliceView>& sv
       lit.has_literal = true;
       lit.literal = in + prev_end;
       lit.literal_len = (size_t)(found[i] - (in + prev_end));
-      avr::pb_put_block(&o, lit);
+      blocks.push_back(lit);
       prev_end = (size_t)(found[i] - in) + s.size;
       b.has_size = true;
       b.size = (int64_t)s.size;
@@ -650,17 +772,35 @@ int emit_container(const uint8_t* in, size_t n, const std::vector<SliceView>& sv
       b.has_size = true;
       b.size = (int64_t)s.size;
     }
-    avr::pb_put_block(&o, b);
+    blocks.push_back(std::move(b));
   }
   avr::PbBlock lit;
   lit.has_literal = true;
   lit.literal = in + prev_end;
   lit.literal_len = n - prev_end;
-  avr::pb_put_block(&o, lit);
-  *out = (uint8_t*)malloc(o.size() ? o.size() : 1);
-  if (!*out) return AVR_ERR_OUT_OF_MEMORY;
-  memcpy(*out, o.data(), o.size());
-  *out_len = o.size();
+  blocks.push_back(lit);
+  std::vector<uint8_t> md;
+  if (const char* tag = avr::version_of_model(model)) avr::pb_put_metadata_version(&md, tag);
+  size_t total = md.size();
+  for (const auto& b : blocks) total += avr::pb_block_size(b);
+  if (dst && total > cap) {
+    *out_len = total;
+    return AVR_ERR_INVALID_ARGUMENT;
+  }
+  uint8_t* o = dst ? dst : host_alloc(total);
+  if (!o) return AVR_ERR_OUT_OF_MEMORY;
+  if (!md.empty()) memcpy(o, md.data(), md.size());
+  size_t at = md.size();
+  std::vector<avr::PbCopy> copies;
+  copies.reserve(2 * blocks.size());
+  for (const auto& b : blocks) at = avr::pb_write_block(o, at, b, &copies);
+  if (at != total) {
+    if (!dst) free(o);
+    return fail(nullptr, AVR_ERR_DEVICE, "internal error: container size");
+  }
+  parallel_copies(copies, o);
+  if (out) *out = dst ? nullptr : o;
+  *out_len = total;
   return AVR_OK;
 }
 
@@ -1177,7 +1317,7 @@ namespace {
 // Rank 0's container from gathered per-slice outputs (both avr_assemble_container entry points).
 int assemble(const uint8_t* file, size_t n, int model, const std::vector<SliceView>& sv, const int32_t* status,
              const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets, const uint32_t* lens, uint8_t** out,
-             size_t* out_len) {
+             size_t* out_len, uint8_t* dst = nullptr, size_t cap = 0) {
   std::vector<char> ok(sv.size(), 0);
   std::vector<std::pair<const uint8_t*, size_t>> blobs(sv.size(), {nullptr, 0});
   for (size_t i = 0; i < sv.size(); i++) {
@@ -1187,7 +1327,12 @@ int assemble(const uint8_t* file, size_t n, int model, const std::vector<SliceVi
       blobs[i] = {recoded + offsets[i], lens[i]};
     }
   }
-  return emit_container(file, n, sv, segment(file, n, sv, ok), blobs, model, out, out_len);
+  const double t0 = now_s();
+  const std::vector<const uint8_t*> found = segment(file, n, sv, ok);
+  const double t1 = now_s();
+  const int r = emit_container(file, n, sv, found, blobs, model, out, out_len, dst, cap);
+  if (getenv("AVR_ASM_TIMING")) fprintf(stderr, "assemble: segment %.3f s, emit %.3f s\n", t1 - t0, now_s() - t1);
+  return r;
 }
 }  // namespace
 
@@ -1205,11 +1350,12 @@ int avr_assemble_container(const uint8_t* file, size_t n, int model, int n_slice
   });
 }
 
-int avr_assemble_container_parsed(const uint8_t* file, size_t n, int model, const avr_slice_desc* descs, int n_slices,
-                                  const uint8_t* arena, size_t arena_len, const int32_t* status,
-                                  const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets,
-                                  const uint32_t* lens, uint8_t** out, size_t* out_len) {
-  if (!file || !out || !out_len || n_slices < 0 || (n_slices && (!descs || !arena || !status || !offsets || !lens)) ||
+namespace {
+int assemble_parsed(const uint8_t* file, size_t n, int model, const avr_slice_desc* descs, int n_slices,
+                    const uint8_t* arena, size_t arena_len, const int32_t* status, const uint8_t* recoded,
+                    size_t recoded_len, const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len,
+                    uint8_t* dst, size_t cap) {
+  if (!file || !out_len || n_slices < 0 || (n_slices && (!descs || !arena || !status || !offsets || !lens)) ||
       !parallel_model(model))
     return AVR_ERR_INVALID_ARGUMENT;
   return guarded(nullptr, [&]() -> int {
@@ -1217,10 +1363,43 @@ int avr_assemble_container_parsed(const uint8_t* file, size_t n, int model, cons
     for (int i = 0; i < n_slices; i++) {
       const avr_slice_desc& d = descs[i];
       if (d.payload_offset > arena_len || d.payload_size > arena_len - d.payload_offset) return AVR_ERR_INVALID_ARGUMENT;
-      sv[i] = {arena + d.payload_offset, d.payload_size, d.coded != 0};
+      // only avr_parse_stream's own descriptors of this file: a coded slice is one recodable_candidate
+      // accepted (a surrogate marker long, its LDS ring within a workgroup), and a payload the parse
+      // found verbatim stands at file_offset (its first and last bytes checked: O(1) per slice)
+      if (d.coded && (d.payload_size < (uint32_t)avr::kSurrogateMarkerBytes ||
+                      avr::shared_bytes(ring_cols(d)) > kLdsBudget))
+        return AVR_ERR_INVALID_ARGUMENT;
+      const uint8_t* P = arena + d.payload_offset;
+      const size_t m = d.payload_size;
+      if (d.file_offset != ~(uint64_t)0) {
+        const size_t k = std::min<size_t>(m, 16);
+        if (d.file_offset > n || m > n - d.file_offset || memcmp(file + d.file_offset, P, k) != 0 ||
+            memcmp(file + d.file_offset + m - k, P + m - k, k) != 0)
+          return AVR_ERR_INVALID_ARGUMENT;
+      }
+      sv[i] = {P, m, d.coded != 0, d.file_offset};
     }
-    return assemble(file, n, model, sv, status, recoded, recoded_len, offsets, lens, out, out_len);
+    return assemble(file, n, model, sv, status, recoded, recoded_len, offsets, lens, out, out_len, dst, cap);
   });
+}
+}  // namespace
+
+int avr_assemble_container_parsed(const uint8_t* file, size_t n, int model, const avr_slice_desc* descs, int n_slices,
+                                  const uint8_t* arena, size_t arena_len, const int32_t* status,
+                                  const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets,
+                                  const uint32_t* lens, uint8_t** out, size_t* out_len) {
+  if (!out) return AVR_ERR_INVALID_ARGUMENT;
+  return assemble_parsed(file, n, model, descs, n_slices, arena, arena_len, status, recoded, recoded_len, offsets, lens,
+                         out, out_len, nullptr, 0);
+}
+
+int avr_assemble_container_into(const uint8_t* file, size_t n, int model, const avr_slice_desc* descs, int n_slices,
+                                const uint8_t* arena, size_t arena_len, const int32_t* status, const uint8_t* recoded,
+                                size_t recoded_len, const uint64_t* offsets, const uint32_t* lens, uint8_t* out,
+                                size_t out_cap, size_t* out_len) {
+  if (!out) return AVR_ERR_INVALID_ARGUMENT;
+  return assemble_parsed(file, n, model, descs, n_slices, arena, arena_len, status, recoded, recoded_len, offsets, lens,
+                         nullptr, out_len, out, out_cap);
 }
 
 int avr_container_model(const uint8_t* avrc, size_t n, int* model) {
@@ -1435,15 +1614,10 @@ static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int 
                                   avr::SeqFiles(), avr::kFlagFields));
     return AVR_OK;
   }
-  const int chunk = std::max(1, std::min(n, kMaxSlicesPerLaunch));
-  HIP_TRY(c, c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * chunk, true));
-  HIP_TRY(c, c->order.reserve(sizeof(int) * (size_t)chunk));
-  for (int s0 = 0; s0 < n; s0 += chunk) {
-    const int m = std::min(chunk, n - s0);
-    HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), d_desc + s0, m, max_w, d_in, d_out,
-                                  d_res + s0, c->est.as<uint16_t>(), nullptr, nullptr, c->order_or_null(), s,
-                                  avr::SeqFiles(), avr::kFlagFields | coder_flag(model)));
-  }
+  HIP_TRY(c, reserve_parallel(c, n, max_w));
+  HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), d_desc, n, max_w, d_in, d_out, d_res,
+                                c->est.as<uint16_t>(), nullptr, nullptr, c->order_or_null(), s, avr::SeqFiles(),
+                                avr::kFlagFields | coder_flag(model), c->queue.p));
   return AVR_OK;
 }
 
@@ -1493,43 +1667,60 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
     return AVR_ERR_INVALID_ARGUMENT;
   *descs = nullptr;
   *arena = nullptr;
-  ParsedFile pf;
-  if (int r = parse_file(nullptr, file, n, &pf)) return r;
-  Plan plan;
-  uint64_t work = 0;
-  int mh = 1;
-  for (const avr::SliceInfo& s : pf.slices) {
-    avr_slice_desc d = desc_from_header(s);
-    append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
-    d.payload_size = (uint32_t)s.size;
-    d.read_limit = (uint32_t)s.read_limit;
-    d.coded = recodable_candidate(s);
-    d.out_offset = work;
-    d.out_capacity = (uint32_t)(s.size * 2 + 256);
-    work += ((uint64_t)d.out_capacity + 15) & ~15ull;
-    if (d.coded) plan.max_w = std::max(plan.max_w, ring_cols(d));   // uncoded slices are never walked
-    mh = std::max(mh, d.mb_height);
-    plan.descs.push_back(d);
-  }
-  plan.arena.resize(plan.arena.size() + 16, 0);
-  const size_t dn = sizeof(avr_slice_desc) * plan.descs.size();
-  *descs = (avr_slice_desc*)malloc(dn ? dn : 1);
-  *arena = (uint8_t*)malloc(plan.arena.size());
-  if (!*descs || !*arena) {
-    free(*descs);
-    free(*arena);
-    *descs = nullptr;
-    *arena = nullptr;
-    return AVR_ERR_OUT_OF_MEMORY;
-  }
-  if (dn) memcpy(*descs, plan.descs.data(), dn);
-  memcpy(*arena, plan.arena.data(), plan.arena.size());
-  *n_slices = (int)plan.descs.size();
-  *arena_len = plan.arena.size();
-  *work_len = work;
-  *max_w = plan.max_w;
-  *max_h = mh;
-  return AVR_OK;
+  return guarded(nullptr, [&]() -> int {
+    ParsedFile pf;
+    if (int r = parse_file(nullptr, file, n, &pf)) return r;
+    // the arena's layout first (append_aligned's: 16-byte aligned payloads, each followed by >= 16
+    // zero bytes), then one zeroed allocation and the payload copies on host threads
+    const size_t ns = pf.slices.size();
+    std::vector<avr_slice_desc> dv(ns);
+    std::vector<avr::PbCopy> copies(ns);
+    uint64_t work = 0, at = 0;
+    int mw = 1, mh = 1;
+    for (size_t i = 0; i < ns; i++) {
+      const avr::SliceInfo& s = pf.slices[i];
+      avr_slice_desc& d = dv[i];
+      d = desc_from_header(s);
+      d.payload_offset = (at + 15) & ~(uint64_t)15;
+      at = d.payload_offset + s.read_limit + 16;
+      copies[i] = {(size_t)d.payload_offset, s.payload(), s.read_limit};
+      d.payload_size = (uint32_t)s.size;
+      d.read_limit = (uint32_t)s.read_limit;
+      d.coded = recodable_candidate(s);
+      d.file_offset = s.file_payload_offset();
+      d.out_offset = work;
+      d.out_capacity = (uint32_t)(s.size * 2 + 256);
+      work += ((uint64_t)d.out_capacity + 15) & ~15ull;
+      if (d.coded) mw = std::max(mw, ring_cols(d));   // uncoded slices are never walked
+      mh = std::max(mh, d.mb_height);
+    }
+    const size_t alen = at + 16;
+    const size_t dn = sizeof(avr_slice_desc) * ns;
+    *descs = (avr_slice_desc*)malloc(dn ? dn : 1);
+    *arena = host_alloc(alen);
+    if (!*descs || !*arena) {
+      free(*descs);
+      free(*arena);
+      *descs = nullptr;
+      *arena = nullptr;
+      return AVR_ERR_OUT_OF_MEMORY;
+    }
+    if (dn) memcpy(*descs, dv.data(), dn);
+    parallel_copies(copies, *arena);
+    // the zero bytes between and after the payloads
+    uint64_t z = 0;
+    for (const auto& cp : copies) {
+      memset(*arena + z, 0, cp.dst - z);
+      z = cp.dst + cp.len;
+    }
+    memset(*arena + z, 0, alen - z);
+    *n_slices = (int)ns;
+    *arena_len = alen;
+    *work_len = work;
+    *max_w = mw;
+    *max_h = mh;
+    return AVR_OK;
+  });
 }
 
 int avr_pack_outputs(avr_ctx* c, const avr_slice_desc* d_desc, const avr_slice_result* d_res, int n,

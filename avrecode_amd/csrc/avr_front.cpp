@@ -77,18 +77,31 @@ void skip_scaling_list(Bits& b, int size) {
   }
 }
 
+// Emulation prevention removed (7.4.1): every 00 00 03 drops its 03, scanning left to right (the
+// byte after a dropped 03 starts the next match).  The 03 bytes are found by memchr and the runs
+// between them copied whole: a multi-GB stream unescapes at memory speed, not byte by byte.
 std::vector<uint8_t> unescape(const uint8_t* src, size_t n) {
-  std::vector<uint8_t> out;
-  out.reserve(n);
-  for (size_t i = 0; i < n;) {
-    if (i + 2 < n && src[i] == 0 && src[i + 1] == 0 && src[i + 2] == 3) {
-      out.push_back(0);
-      out.push_back(0);
-      i += 3;
-    } else {
-      out.push_back(src[i++]);
+  std::vector<uint8_t> out(n);
+  size_t i = 0, o = 0;
+  while (i < n) {
+    // the first 00 00 03 at or after i: a 03 at p >= i + 2 with two zeros before it
+    size_t j = n;
+    for (size_t k = i + 2; k < n;) {
+      const uint8_t* p = (const uint8_t*)memchr(src + k, 3, n - k);
+      if (!p) break;
+      const size_t q = (size_t)(p - src);
+      if (src[q - 1] == 0 && src[q - 2] == 0) {
+        j = q - 2;
+        break;
+      }
+      k = q + 1;
     }
+    const size_t run = (j < n ? j + 2 : n) - i;   // the bytes before the 03 (both zeros included)
+    memcpy(out.data() + o, src + i, run);
+    o += run;
+    i = j < n ? j + 3 : n;
   }
+  out.resize(o);
   return out;
 }
 
@@ -473,18 +486,27 @@ bool demux_mp4(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
   return true;
 }
 
+// The first j >= k with f[j] = f[j + 1] = 0 and f[j + 2] = 1 (or 0 too, with zero3), j + 3 <= n; n
+// when there is none.  memchr finds the zeros: start codes are found at memory speed.
+size_t scan_start(const uint8_t* f, size_t n, size_t k, bool zero3) {
+  while (k + 3 <= n) {
+    const uint8_t* p = (const uint8_t*)memchr(f + k, 0, n - 2 - k);
+    if (!p) return n;
+    const size_t j = (size_t)(p - f);
+    if (f[j + 1] == 0 && (f[j + 2] == 1 || (zero3 && f[j + 2] == 0))) return j;
+    k = j + 1;
+  }
+  return n;
+}
+
 void demux_annexb(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
-  auto is_sc = [&](size_t j) { return j + 3 <= n && f[j] == 0 && f[j + 1] == 0 && f[j + 2] == 1; };
-  size_t i = 0;
-  while (i + 3 <= n && !is_sc(i)) i++;
+  size_t i = scan_start(f, n, 0, false);
   while (i + 3 <= n) {
-    size_t start = i + 3, j = start;
-    while (j + 3 <= n && !(f[j] == 0 && f[j + 1] == 0 && (f[j + 2] == 1 || f[j + 2] == 0))) j++;
+    const size_t start = i + 3, j = scan_start(f, n, start, true);
     size_t end = j + 3 <= n ? j : n;
     while (end > start && f[end - 1] == 0) end--;
     if (end > start) nals->push_back({start, end - start});
-    i = j;
-    while (i + 3 <= n && !is_sc(i)) i++;
+    i = scan_start(f, n, j, false);
   }
 }
 
@@ -545,6 +567,7 @@ bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s) {
   const size_t end = (bits + 7) / 8;
   s->size = end > h.cabac_start ? end - h.cabac_start : 0;
   s->read_limit = rbsp.size() > h.cabac_start + s->size ? s->size + 1 : s->size;
+  s->verbatim = rbsp.size() == n - 1;
   s->rbsp = std::move(rbsp);
   return true;
 }
@@ -594,6 +617,55 @@ void pb_put_block(std::vector<uint8_t>* o, const PbBlock& b) {
   if (b.has_parity) varint(&m, 5 << 3), varint(&m, b.length_parity ? 1 : 0);
   if (b.has_last_byte) bytes_field(&m, 6, (const uint8_t*)b.last_byte.data(), b.last_byte.size());
   bytes_field(o, 2, m.data(), m.size());
+}
+
+namespace {
+size_t varint_size(uint64_t v) {
+  size_t k = 1;
+  while (v >= 0x80) v >>= 7, k++;
+  return k;
+}
+size_t bytes_field_size(int field, size_t n) { return varint_size((uint64_t)field << 3 | 2) + varint_size(n) + n; }
+size_t block_inner_size(const PbBlock& b) {
+  size_t m = 0;
+  if (b.has_size) m += varint_size(1 << 3) + varint_size((uint64_t)b.size);
+  if (b.has_literal) m += bytes_field_size(2, b.literal_len);
+  if (b.has_skip) m += varint_size(3 << 3) + 1;
+  if (b.has_cabac) m += bytes_field_size(4, b.cabac_len);
+  if (b.has_parity) m += varint_size(5 << 3) + 1;
+  if (b.has_last_byte) m += bytes_field_size(6, b.last_byte.size());
+  return m;
+}
+size_t put_varint(uint8_t* o, size_t at, uint64_t v) {
+  while (v >= 0x80) {
+    o[at++] = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  o[at++] = (uint8_t)v;
+  return at;
+}
+size_t put_bytes(uint8_t* o, size_t at, int field, const uint8_t* p, size_t n, std::vector<PbCopy>* copies) {
+  at = put_varint(o, at, (uint64_t)field << 3 | 2);
+  at = put_varint(o, at, n);
+  if (copies && n) copies->push_back({at, p, n});
+  else if (n) memcpy(o + at, p, n);
+  return at + n;
+}
+}  // namespace
+
+size_t pb_block_size(const PbBlock& b) { return bytes_field_size(2, block_inner_size(b)); }
+
+// pb_put_block's bytes, field for field
+size_t pb_write_block(uint8_t* o, size_t at, const PbBlock& b, std::vector<PbCopy>* copies) {
+  at = put_varint(o, at, 2 << 3 | 2);
+  at = put_varint(o, at, block_inner_size(b));
+  if (b.has_size) at = put_varint(o, at, 1 << 3), at = put_varint(o, at, (uint64_t)b.size);
+  if (b.has_literal) at = put_bytes(o, at, 2, b.literal, b.literal_len, copies);
+  if (b.has_skip) at = put_varint(o, at, 3 << 3), at = put_varint(o, at, b.skip_coded ? 1 : 0);
+  if (b.has_cabac) at = put_bytes(o, at, 4, b.cabac, b.cabac_len, copies);
+  if (b.has_parity) at = put_varint(o, at, 5 << 3), at = put_varint(o, at, b.length_parity ? 1 : 0);
+  if (b.has_last_byte) at = put_bytes(o, at, 6, (const uint8_t*)b.last_byte.data(), b.last_byte.size(), nullptr);
+  return at;
 }
 
 void pb_put_metadata_version(std::vector<uint8_t>* o, const std::string& version) {

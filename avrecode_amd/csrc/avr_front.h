@@ -39,7 +39,10 @@ struct SliceInfo {
   std::vector<uint8_t> rbsp;             // unescaped NAL payload after the header byte
   size_t size = 0;                       // init_decoder size
   size_t read_limit = 0;                 // bytes a decoder may read from the payload start
+  bool verbatim = false;                 // the NAL has no emulation-prevention bytes: the payload
+                                         //   is the file's bytes at file_payload_offset()
   const uint8_t* payload() const { return rbsp.data() + h.cabac_start; }
+  uint64_t file_payload_offset() const { return verbatim ? nal_offset + 1 + h.cabac_start : ~(uint64_t)0; }
 };
 
 struct NalRef {
@@ -90,6 +93,16 @@ struct PbBlock {
   std::string last_byte;
 };
 void pb_put_block(std::vector<uint8_t>* o, const PbBlock& b);
+// The same bytes written into a buffer sized beforehand: pb_block_size(b) bytes at o + at (returns
+// at + that).  The literal and cabac fields' bytes are left to the caller as copy jobs (dst offset
+// in o, source, length) when copies is given, else copied here.
+struct PbCopy {
+  size_t dst;
+  const uint8_t* src;
+  size_t len;
+};
+size_t pb_block_size(const PbBlock& b);
+size_t pb_write_block(uint8_t* o, size_t at, const PbBlock& b, std::vector<PbCopy>* copies);
 void pb_put_metadata_version(std::vector<uint8_t>* o, const std::string& version);
 bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version,
               bool* has_metadata = nullptr);

@@ -47,20 +47,32 @@ struct SeqFiles {
 hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
                          int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                          uint8_t* frames, int* frame_meta, int* order, hipStream_t stream,
-                         const SeqFiles& files = SeqFiles(), uint32_t flags = 0);
+                         const SeqFiles& files = SeqFiles(), uint32_t flags = 0, void* qscratch = nullptr);
+// Parallel compress / decompress batches larger than the chip holds at once (more than
+// resident_slices) run as one persistent launch over a largest-first queue when launch_slices gets
+// a queue scratch of queue_scratch_bytes(n) (device); est then needs est_slots(n, max_mb_width)
+// estimator scratches of kEstGlobal u16 (one per resident workgroup), else n.
+size_t queue_scratch_bytes(int n);
+int slots_per_cu(size_t lds);
+int resident_slices(size_t lds);
+int est_slots(int n, int max_mb_width);
 // one per kernel translation unit (avr_k_*.hip); lds = shared_bytes(max_mb_width)
 hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                    const int* order, uint32_t flags, hipStream_t stream);
+                                    const int* order, uint32_t flags, hipStream_t stream,
+                                    uint32_t* qhead = nullptr, int qgrid = 0);
 hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                      const int* order, uint32_t flags, hipStream_t stream);
+                                      const int* order, uint32_t flags, hipStream_t stream,
+                                    uint32_t* qhead = nullptr, int qgrid = 0);
 hipError_t launch_parallel_compress32(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                      const int* order, uint32_t flags, hipStream_t stream);
+                                      const int* order, uint32_t flags, hipStream_t stream,
+                                    uint32_t* qhead = nullptr, int qgrid = 0);
 hipError_t launch_parallel_decompress32(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                         const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                        const int* order, uint32_t flags, hipStream_t stream);
+                                        const int* order, uint32_t flags, hipStream_t stream,
+                                    uint32_t* qhead = nullptr, int qgrid = 0);
 hipError_t launch_parallel_generate(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                     const int* order, uint32_t flags, hipStream_t stream);

@@ -157,6 +157,7 @@ struct Shared {
   int32_t p_status, p_stop_ok, c_err;  // slice results of the two waves
   uint32_t elog_n;           // entries appended to the HBM table's write log by this model
   uint32_t prio;             // the slice's current wave priority (walker -> modeler / coder)
+  uint32_t qnext;            // persistent launches: the queue entry this workgroup drew
   uint32_t c_len, c_last;
   uint32_t bill[6];          // the coder's h264_model billing by CodingType (kFlagBill launches)
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
@@ -292,6 +293,7 @@ static inline hipError_t reset_cu_board(hipStream_t stream) {
   if (e == hipSuccess) e = hipMemsetAsync(rem, 0, sizeof(avr_cu_rem), stream);
   return e;
 }
+constexpr uint32_t kNoCell = 0xffffffffu;   // Walker::prio_cell not assigned yet
 AVR_FI void cu_post(uint32_t cell, uint32_t rem) {
   if (__lane_id() == 0) __hip_atomic_store(&avr_cu_rem[cell], rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -2179,7 +2181,7 @@ AVR_FI void begin_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, 
   if (MODE == MODE_DECOMPRESS) w.byp_e = w.sh->est[1024];
   w.mc_load();
   if (!RM && (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS)) {
-    w.prio_cell = cu_cell();
+    if (w.prio_cell == kNoCell) w.prio_cell = cu_cell();
     w.prio_cur = 0xffffffffu;   // set on the first macroblock
   }
   if (MODE == MODE_COMPRESS || MODE == MODE_TRACE) {
@@ -2710,22 +2712,17 @@ constexpr int slice_threads() {
   return MODE == MODE_GENERATE || MODE == MODE_TRACE ? 64 : MODE == MODE_COMPRESS ? 192 : 128;
 }
 
-// FLD = false: the progressive frames of the batch; FLD = true: its field pictures and MBAFF frames
-// (a second launch over the same batch: each kernel leaves the other's slices alone)
-template <int MODE, bool FLD, bool P32 = false>
-__global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
-                                                                const uint8_t* in, uint8_t* out, avr_slice_result* res,
-                                                                uint16_t* est_scratch, const int* order,
-                                                                uint32_t flags) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  if ((int)blockIdx.x >= n) return;
-  const int s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
+// One slice of a parallel launch on this workgroup (every thread): the hot tables are in LDS
+// already; est_g is the slice's estimator scratch; cell = the walker's CU-board cell (kNoCell:
+// register one).
+template <int MODE, bool FLD, bool P32>
+AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice_desc* descs, int s, const uint8_t* in,
+                           uint8_t* out, avr_slice_result* res, uint16_t* est_g, uint32_t flags, uint32_t cell) {
   const avr_slice_desc* d = &descs[s];
-  if ((d->structure != AVR_STRUCT_FRAME) != FLD) return;
   Walker<MODE, false, FLD, P32> w;
   w.sh = (Shared*)smem;
   w.ring = (EdgeRec*)(smem + sizeof(Shared));
-  load_hot_tables(w.sh, G);
+  w.prio_cell = cell;
   w.T = &w.sh->tab;
   w.G = G;
   w.frames = nullptr;
@@ -2734,7 +2731,7 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   w.gmode = false;
   w.gsink = nullptr;
   w.gcount = 0;
-  w.est_g = est_scratch + (size_t)s * kEstGlobal;
+  w.est_g = est_g;
   w.ring_cols = flags >> kFlagRingShift;
   if (!d->coded) {
     if (threadIdx.x == 0) {
@@ -2769,23 +2766,79 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
 }
 
+// FLD = false: the progressive frames of the batch; FLD = true: its field pictures and MBAFF frames
+// (a second launch over the same batch: each kernel leaves the other's slices alone).
+//
+// Two ways to run a batch:
+//  - qhead == nullptr: workgroup b runs slice order[b] (the CU grouping of schedule_kernel) or b,
+//    with the estimator scratch of that slice -- a batch that is resident all at once;
+//  - qhead != nullptr (a batch larger than the chip holds at once): a persistent grid of about one
+//    workgroup per resident slot; each workgroup takes the next entry of the queue `order` (the
+//    slices sorted largest first, queue_order_kernel) by an atomic on *qhead until the queue is
+//    empty, with one estimator scratch per workgroup (est_table_reset undoes the previous slice's
+//    stores).  Every workgroup leaves when it draws past the end, so the grid always drains.
+//    Largest first is LPT: the batch ends on small slices instead of on a large one started late,
+//    and there are no launch boundaries inside the batch to wait at.
+template <int MODE, bool FLD, bool P32 = false>
+__global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+                                                                const uint8_t* in, uint8_t* out, avr_slice_result* res,
+                                                                uint16_t* est_scratch, const int* order,
+                                                                uint32_t* qhead, uint32_t flags) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  Shared* sh = (Shared*)smem;
+  // one call site of the slice body for both ways (the walker is inlined once per kernel)
+  uint16_t* est_g = est_scratch + (size_t)blockIdx.x * kEstGlobal;
+  uint32_t cell = kNoCell;   // the walker wave's cell on the CU board, for every slice of a persistent workgroup
+  bool loaded = false, done = false;
+  for (;;) {
+    int s;
+    if (qhead) {
+      if (threadIdx.x == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext = atomicAdd(qhead, 1u);
+      __syncthreads();
+      const uint32_t k = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext);
+      __syncthreads();   // every thread has its entry before thread 0 draws again
+      if (k >= (uint32_t)n) break;
+      s = order[k];
+    } else {
+      if (done || (int)blockIdx.x >= n) break;
+      done = true;
+      s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
+      est_g = est_scratch + (size_t)s * kEstGlobal;
+    }
+    if ((descs[s].structure != AVR_STRUCT_FRAME) != FLD) continue;
+    if (!loaded) {
+      load_hot_tables(sh, G);
+      loaded = true;
+      if (qhead && (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x < 64) cell = cu_cell();
+    }
+    parallel_slice<MODE, FLD, P32>(smem, G, descs, s, in, out, res, est_g, flags, cell);
+  }
+}
+
 // Host side of the parallel launches (instantiated in each kernel TU, avr_k_*.hip, with that TU's
 // own CU board): the progressive kernel over the batch, then -- when the batch may hold field
 // pictures / MBAFF frames -- the field-capable kernel over the same batch (its workgroups for
 // progressive slices return at once).  The board starts empty on every launch (cu_cell's slot
-// counter must not carry a previous launch's residue).
+// counter must not carry a previous launch's residue).  q.head: the persistent queue launch
+// (slices_parallel_kernel) over q.grid workgroups, q.head[0] for the progressive kernel and
+// q.head[1] for the field one (both zero on entry).
+struct QueueLaunch {
+  uint32_t* head = nullptr;
+  int grid = 0;
+};
 template <int MODE, bool P32>
 inline hipError_t launch_parallel(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                   const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
-                                  const int* order, uint32_t flags, hipStream_t stream) {
+                                  const int* order, uint32_t flags, hipStream_t stream, QueueLaunch q = QueueLaunch()) {
+  const int grid = q.head ? q.grid : n;
   if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
-  hipLaunchKernelGGL((slices_parallel_kernel<MODE, false, P32>), dim3(n), dim3(slice_threads<MODE>()), lds, stream,
-                     T, descs, n, in, out, res, est, order, flags);
+  hipLaunchKernelGGL((slices_parallel_kernel<MODE, false, P32>), dim3(grid), dim3(slice_threads<MODE>()), lds, stream,
+                     T, descs, n, in, out, res, est, order, q.head, flags);
   if (flags & kFlagFields) {
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
-    hipLaunchKernelGGL((slices_parallel_kernel<MODE, true, P32>), dim3(n), dim3(slice_threads<MODE>()), lds, stream,
-                       T, descs, n, in, out, res, est, order, flags);
+    hipLaunchKernelGGL((slices_parallel_kernel<MODE, true, P32>), dim3(grid), dim3(slice_threads<MODE>()), lds, stream,
+                       T, descs, n, in, out, res, est, order, q.head ? q.head + 1 : nullptr, flags);
   }
   return hipGetLastError();
 }

@@ -153,6 +153,10 @@ typedef struct {
   int32_t coded;             /* 0: skip_coded slice (reference mode only calls frame_spec) */
   int32_t structure;         /* AVR_STRUCT_*: frame, top / bottom field picture (PAFF), MBAFF frame;
                               * mb_height is the FRAME height in macroblocks in every case */
+  uint64_t file_offset;      /* host only (avr_parse_stream): where the payload's bytes stand verbatim in
+                              * the parsed file (its NAL has no emulation-prevention bytes), else
+                              * UINT64_MAX; the container assembly's segmentation starts there
+                              * (recode.cpp:1275-1297).  The kernels ignore it. */
 } avr_slice_desc;
 enum { AVR_STRUCT_FRAME = 0, AVR_STRUCT_TOP_FIELD = 1, AVR_STRUCT_BOTTOM_FIELD = 2, AVR_STRUCT_MBAFF = 3 };
 
@@ -243,7 +247,11 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
  * + lens[k]), inside recoded_len (AVR_ERR_INVALID_ARGUMENT otherwise).  The result is
  * byte-identical to avr_compress_file(..., model).  avr_assemble_container parses `file` again;
  * avr_assemble_container_parsed takes avr_parse_stream's descs and arena for it instead (the parse
- * a sharded caller already holds: no second pass over a multi-GB stream). */
+ * a sharded caller already holds: no second pass over a multi-GB stream).  Only that call's output,
+ * unmodified, for this file is accepted: a coded desc must be a recodable candidate and a verbatim
+ * payload must stand at its file_offset (checked on its first and last bytes; otherwise
+ * AVR_ERR_INVALID_ARGUMENT).  The segmentation searches only each slice's literal gap when the parse
+ * found its payload verbatim, and the container is written once, its bytes copied by host threads. */
 int avr_assemble_container(const uint8_t* file, size_t n, int model, int n_slices, const int32_t* status,
                            const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets, const uint32_t* lens,
                            uint8_t** out, size_t* out_len);
@@ -251,6 +259,14 @@ int avr_assemble_container_parsed(const uint8_t* file, size_t n, int model, cons
                                   const uint8_t* arena, size_t arena_len, const int32_t* status,
                                   const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets,
                                   const uint32_t* lens, uint8_t** out, size_t* out_len);
+/* avr_assemble_container_parsed into the caller's buffer out (out_cap bytes): a step that assembles
+ * every time reuses one buffer, already mapped, instead of a fresh multi-GB allocation.  *out_len =
+ * the container's size; when it exceeds out_cap nothing is written and AVR_ERR_INVALID_ARGUMENT is
+ * returned with *out_len set.  A bound: n + sum(lens of coded slices) + 64 (n_slices + 2). */
+int avr_assemble_container_into(const uint8_t* file, size_t n, int model, const avr_slice_desc* descs, int n_slices,
+                                const uint8_t* arena, size_t arena_len, const int32_t* status, const uint8_t* recoded,
+                                size_t recoded_len, const uint64_t* offsets, const uint32_t* lens, uint8_t* out,
+                                size_t out_cap, size_t* out_len);
 /* The model mode a Recoded container was written with (its Metadata.version): AVR_MODEL_*.
  * AVR_ERR_FORMAT for bytes that are not a Recoded message or name another avrecode-amd format. */
 int avr_container_model(const uint8_t* avrc, size_t n, int* model);

@@ -118,4 +118,7 @@ def test_widened_sps_keeps_the_other_fields():
     data = (FIX / "mbaff_ib.264").read_bytes()
     base, same = avr.parse_stream(data), avr.parse_stream(_wide(data, int(avr.parse_stream(data).descs["mb_width"][0])))
     assert same.arena.tobytes() == base.arena.tobytes()
-    assert same.descs.tobytes() == base.descs.tobytes()
+    # every field but the payloads' file positions (the rewritten SPS may change its length)
+    fields = [f for f in base.descs.dtype.names if f != "file_offset"]
+    for f in fields:
+        assert (same.descs[f] == base.descs[f]).all(), f
