@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "avr_create", "avr_destroy", "avr_last_error", "avr_free", "avr_compress_file", "avr_decompress_file",
     "avr_roundtrip_file", "avr_compress_slices", "avr_decompress_slices", "avr_pack_outputs",
     "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream",
-    "avr_assemble_container", "avr_assemble_container_parsed", "avr_assemble_container_into", "avr_container_model", "avr_synthesize_stream",
+    "avr_assemble_container", "avr_assemble_container_parsed", "avr_assemble_container_into", "avr_dec_plan_new", "avr_dec_plan_free", "avr_dec_plan_load", "avr_dec_plan_descs", "avr_dec_plan_arena", "avr_dec_plan_splice", "avr_container_model", "avr_synthesize_stream",
     "avr_container_describe", "avr_compress_files", "avr_decompress_files",
     "avr_hooks_compress_begin", "avr_hooks_compress_stream_begin", "avr_hooks_feed",
     "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
@@ -179,6 +179,13 @@ def lib() -> ctypes.CDLL:
     L.avr_assemble_container.argtypes = [vp, sz, i32, i32, vp, vp, sz, vp, vp, pp, psz]
     L.avr_assemble_container_parsed.argtypes = [vp, sz, i32, vp, i32, vp, sz, vp, vp, sz, vp, vp, pp, psz]
     L.avr_assemble_container_into.argtypes = [vp, sz, i32, vp, i32, vp, sz, vp, vp, sz, vp, vp, vp, sz, psz]
+    L.avr_dec_plan_new.argtypes = [pp]
+    L.avr_dec_plan_free.argtypes = [vp]
+    L.avr_dec_plan_free.restype = None
+    L.avr_dec_plan_load.argtypes = [vp, vp, sz, pi, psz, psz, pi, pi]
+    L.avr_dec_plan_descs.argtypes = [vp, vp]
+    L.avr_dec_plan_arena.argtypes = [vp, vp, sz]
+    L.avr_dec_plan_splice.argtypes = [vp, vp, vp, sz, vp, vp, vp, sz, psz]
     L.avr_container_model.argtypes = [vp, sz, pi]
     L.avr_synthesize_stream.argtypes = [vp, ctypes.POINTER(_SynthParams), i32, pp, psz]
     L.avr_container_describe.argtypes = [vp, sz, pp, pp, psz]
@@ -293,6 +300,79 @@ def plan_decompress(avrc) -> ParsedStream:
     d = _take_array(descs, ns.value * SLICE_DESC.itemsize).view(SLICE_DESC)
     a = _take_array(arena, alen.value)
     return ParsedStream(d, a, int(wlen.value), int(mw.value), int(mh.value))
+
+
+class DecompressPlan:
+    """The sharded decompress's host halves on one parse of a PARALLEL-model container
+    (avr_dec_plan_*): load(avrc) plans it (no bytes copied), parsed(arena_out) gives the decompress
+    batch (descs + the re-coded streams' arena, written into arena_out when given), splice(...) the
+    file from the regenerated slices (into out when given: the view holding the file is returned).
+    The handle keeps its scratch across loads; the container passed to load must stay alive and
+    unchanged until the next load.  Host only."""
+
+    def __init__(self):
+        self._h = ctypes.c_void_p()
+        r = lib().avr_dec_plan_new(ctypes.byref(self._h))
+        if r != AVR_OK:
+            raise AvrError(r, "avr_dec_plan_new failed")
+        self._keep = None
+
+    def load(self, avrc) -> "DecompressPlan":
+        p, n, keep = _buf(avrc)
+        ns, mw, mh = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        al, wl = ctypes.c_size_t(), ctypes.c_size_t()
+        r = lib().avr_dec_plan_load(self._h, p, n, ctypes.byref(ns), ctypes.byref(al), ctypes.byref(wl),
+                                    ctypes.byref(mw), ctypes.byref(mh))
+        if r != AVR_OK:
+            self._keep = None
+            raise AvrError(r, "avr_dec_plan_load failed")
+        self._keep = (avrc, keep)
+        self.n_slices, self.arena_len, self.work_len = ns.value, al.value, wl.value
+        self.max_mb_width, self.max_mb_height = mw.value, mh.value
+        d = np.zeros(self.n_slices, dtype=SLICE_DESC)
+        if self.n_slices:
+            lib().avr_dec_plan_descs(self._h, d.ctypes.data)
+        self.descs = d
+        return self
+
+    def parsed(self, arena_out: "np.ndarray | None" = None) -> ParsedStream:
+        a = np.empty(self.arena_len, dtype=np.uint8) if arena_out is None else arena_out[:self.arena_len]
+        if a.nbytes < self.arena_len:
+            raise ValueError("DecompressPlan.parsed: arena_out too small")
+        r = lib().avr_dec_plan_arena(self._h, a.ctypes.data, a.nbytes)
+        if r != AVR_OK:
+            raise AvrError(r, "avr_dec_plan_arena failed")
+        return ParsedStream(self.descs.copy(), a, self.work_len, self.max_mb_width, self.max_mb_height)
+
+    def splice(self, status, regen, offsets, lens, out: "np.ndarray | None" = None):
+        st = np.ascontiguousarray(status, dtype=np.int32)
+        of = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        if len(st) != self.n_slices or len(of) != len(st) or len(ln) != len(st):
+            raise ValueError("DecompressPlan.splice: one status / offset / length per planned slice")
+        rp, rn, keep = _buf(regen)
+        olen = ctypes.c_size_t()
+        L = lib()
+        if out is None:
+            L.avr_dec_plan_splice(self._h, st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data, None, 0,
+                                  ctypes.byref(olen))
+            out = np.empty(olen.value, dtype=np.uint8)
+        r = L.avr_dec_plan_splice(self._h, st.ctypes.data, rp, rn, of.ctypes.data, ln.ctypes.data, out.ctypes.data,
+                                  out.nbytes, ctypes.byref(olen))
+        if r != AVR_OK:
+            raise AvrError(r, f"avr_dec_plan_splice failed (file {olen.value} B, buffer {out.nbytes} B)")
+        return out[:olen.value]
+
+    def close(self):
+        if self._h:
+            lib().avr_dec_plan_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def container_model(avrc) -> int:

@@ -107,3 +107,64 @@ class DeviceBatch:
     def payloads(self) -> list[bytes]:
         return [self.ps.arena[int(d["payload_offset"]):int(d["payload_offset"]) + int(d["payload_size"])].tobytes()
                 for d in self.ps.descs]
+
+
+class DecompressRange:
+    """One rank's decompress batch of a sharded container decompress, in device buffers that grow
+    as needed and are reused from step to step: the planned slices' descriptors and re-coded
+    streams (d_desc, d_in), the regenerated bytes (d_work), the results (d_res), and their packed
+    copy (d_packed, d_offsets) for the gather to rank 0.  upload() takes a host ParsedStream
+    (DecompressPlan.parsed / shard.subset) or device tensors received from rank 0."""
+
+    def __init__(self, ctx: Context, device=None):
+        self.ctx = ctx
+        self.device = torch.device("cuda", ctx.device) if device is None else device
+        self.n = 0
+        self._cap = {}
+
+    def _buf(self, name: str, nbytes: int, dtype=torch.uint8) -> torch.Tensor:
+        itemsize = torch.empty(0, dtype=dtype).element_size()
+        count = max(1, (nbytes + itemsize - 1) // itemsize)
+        t = self._cap.get(name)
+        if t is None or t.numel() < count:
+            t = torch.empty(count + count // 16, dtype=dtype, device=self.device)
+            self._cap[name] = t
+        return t
+
+    def upload(self, descs, arena, n: int, work_len: int, max_mb_width: int, max_mb_height: int, stream=None):
+        """descs / arena: numpy (host) or uint8 torch tensors (device)."""
+        self.n, self.work_len = n, work_len
+        self.max_mb_width, self.max_mb_height = max_mb_width, max_mb_height
+        nd = n * SLICE_DESC.itemsize
+        self.d_desc = self._buf("desc", nd)
+        self.d_in = self._buf("in", (arena.nbytes if isinstance(arena, np.ndarray) else arena.numel()) + 16)
+        with torch.cuda.stream(stream) if stream is not None else _null():
+            for dst, src, k in ((self.d_desc, descs, nd), (self.d_in, arena, None)):
+                if isinstance(src, np.ndarray):
+                    src = torch.from_numpy(np.ascontiguousarray(src).view(np.uint8).reshape(-1))
+                k = src.numel() if k is None else k
+                if k:
+                    dst[:k].copy_(src[:k], non_blocking=False)
+        self.d_work = self._buf("work", work_len + 16)
+        self.d_res = self._buf("res", max(1, n) * SLICE_RESULT.itemsize)
+
+    def run(self, model: int = MODEL_PARALLEL, stream=None):
+        self.ctx.decompress_slices(self.d_desc, self.n, self.max_mb_width, self.max_mb_height, self.d_in, self.d_work,
+                                   self.d_res, model, stream)
+
+    def pack(self, stream=None):
+        d_packed = self._buf("packed", self.work_len + 16)
+        d_offsets = self._buf("offsets", 8 * (self.n + 1), torch.int64)
+        self.ctx.pack_outputs(self.d_desc, self.d_res, self.n, self.d_work, d_packed, d_offsets, stream)
+        return d_packed, d_offsets
+
+    def results(self) -> np.ndarray:
+        return self.d_res[:max(1, self.n) * SLICE_RESULT.itemsize].cpu().numpy().view(SLICE_RESULT)[: self.n]
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -243,9 +243,36 @@ bool check_reciprocals(const avr::EngineTables& t) {
   return true;
 }
 
+// A byte vector whose resize() leaves new bytes uninitialised (multi-GB buffers that are written
+// right after: no memset pass first).
+template <class T>
+struct DefaultInit : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = DefaultInit<U>;
+  };
+  DefaultInit() = default;
+  template <class U>
+  DefaultInit(const DefaultInit<U>&) {}
+  template <class U>
+  void construct(U* p) {
+    ::new ((void*)p) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+};
+typedef std::vector<uint8_t, DefaultInit<uint8_t>> Bytes;
+
 struct Plan {
   std::vector<avr_slice_desc> descs;
-  std::vector<uint8_t> arena;   // payloads (compress) or recoded streams (decompress)
+  Bytes arena;   // payloads (compress) or recoded streams (decompress)
+  // decompress_setup with layout_only: the arena is not built; its byte copies are listed in
+  // arena_copies (dst in the arena, source in the container) and its length in arena_end
+  bool layout_only = false;
+  std::vector<avr::PbCopy> arena_copies;
+  uint64_t arena_end = 0;
   int max_w = 1;
   // sequential (reference-model) plans over several files: file f is descs[file_first[f] ..
   // file_first[f + 1]); empty = one file
@@ -261,7 +288,8 @@ struct Plan {
   }
 };
 
-void append_aligned(std::vector<uint8_t>* arena, const uint8_t* p, size_t n, size_t extra, uint64_t* off) {
+template <class V>
+void append_aligned(V* arena, const uint8_t* p, size_t n, size_t extra, uint64_t* off) {
   size_t o = (arena->size() + 15) & ~(size_t)15;
   arena->resize(o + n + extra, 0);
   if (n) memcpy(arena->data() + o, p, n);
@@ -514,13 +542,15 @@ struct ParsedFile {
   std::vector<avr::SliceInfo> slices;
 };
 
-int parse_file(avr_ctx* c, const uint8_t* in, size_t n, ParsedFile* pf) {
+// views: slices without emulation-prevention bytes point into `in` instead of holding a copy (the
+// caller keeps `in` alive while it uses pf)
+int parse_file(avr_ctx* c, const uint8_t* in, size_t n, ParsedFile* pf, bool views = false) {
   std::vector<avr::NalRef> nals;
   if (!avr::demux(in, n, &nals)) return fail(c, AVR_ERR_FORMAT, "not an MP4/avcC or Annex-B H.264 stream");
   avr::StreamParser sp;
   for (auto& nr : nals) {
     avr::SliceInfo s;
-    if (sp.next(in + nr.offset, nr.size, &s)) {
+    if (sp.next(in + nr.offset, nr.size, &s, views)) {
       s.nal_offset = nr.offset;
       s.nal_size = nr.size;
       pf->slices.push_back(std::move(s));
@@ -711,14 +741,19 @@ uint8_t* host_alloc(size_t n) {
 }
 
 // Byte copies of a container's literals and re-coded blocks, spread over host threads when they are
-// large (a 10-minute 4K stream's container is 4.4 GB).
-void parallel_copies(const std::vector<avr::PbCopy>& jobs, uint8_t* base) {
+// large (a 10-minute 4K stream's container is 4.4 GB).  A job without a source fills its bytes
+// with `fill` (the decompressor's surrogate blocks).
+void copy_part(uint8_t* dst, const uint8_t* src, size_t len, uint8_t fill) {
+  if (src) memcpy(dst, src, len);
+  else memset(dst, fill, len);
+}
+void parallel_copies(const std::vector<avr::PbCopy>& jobs, uint8_t* base, uint8_t fill = 0) {
   uint64_t total = 0;
   for (const auto& j : jobs) total += j.len;
   const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   const unsigned T = total < ((uint64_t)64 << 20) ? 1u : hw;
   if (T == 1) {
-    for (const auto& j : jobs) memcpy(base + j.dst, j.src, j.len);
+    for (const auto& j : jobs) copy_part(base + j.dst, j.src, j.len, fill);
     return;
   }
   // thread t copies the bytes [t total / T, (t + 1) total / T) of the concatenated jobs
@@ -727,7 +762,7 @@ void parallel_copies(const std::vector<avr::PbCopy>& jobs, uint8_t* base) {
     uint64_t at = 0;
     for (const auto& j : jobs) {
       const uint64_t a = std::max(at, lo), b = std::min(at + j.len, hi);
-      if (a < b) memcpy(base + j.dst + (a - at), j.src + (a - at), (size_t)(b - a));
+      if (a < b) copy_part(base + j.dst + (a - at), j.src ? j.src + (a - at) : nullptr, (size_t)(b - a), fill);
       at += j.len;
       if (at >= hi) break;
     }
@@ -851,7 +886,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   for (int f = 0; f < nf; f++) {
     out[f] = nullptr;
     out_len[f] = 0;
-    st[f] = parse_file(c, in[f], in_len[f], &pf[f]);
+    st[f] = parse_file(c, in[f], in_len[f], &pf[f], /*views=*/true);
   }
   // 1) parallel model: every candidate slice of every file through the parallel kernel -- per-slice
   //    parse, restore check, device roundtrip and the model's output.  Reference model: nothing
@@ -984,13 +1019,15 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
 // sequential launch.
 struct DecJob {
   std::vector<avr::PbBlock> blocks;
-  std::vector<uint8_t> stream;       // read_packet's stream: literals + surrogate blocks
+  Bytes stream;                      // read_packet's stream: literals + surrogate blocks
   bool parallel = false;
   int model = AVR_MODEL_REFERENCE;   // from Recoded.Metadata.version
   std::vector<int> desc_of_block;    // plan index per coded block (-1: none)
 };
 
 int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* plan) {
+  const bool tm = getenv("AVR_ASM_TIMING") != nullptr;
+  double t0 = now_s();
   std::string version;
   if (!avr::pb_parse(in, n, &j->blocks, &version)) return fail(c, AVR_ERR_FORMAT, "not a Recoded protobuf");
   j->model = avr::model_of_version(version);
@@ -1000,27 +1037,45 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
     return fail(c, AVR_ERR_FORMAT, "unsupported container version " + version + " (expected " + avr::kParallelModelTag +
                                        " or " + avr::kParallel32ModelTag + ")");
   j->parallel = parallel_model(j->model);
-  // read_packet (recode.cpp:1359-1409): literals and surrogate blocks form the stream
+  // read_packet (recode.cpp:1359-1409): literals and surrogate blocks form the stream -- its layout
+  // first, then one allocation, the markers, and the literal copies and 'X' fills on host threads
   uint64_t seq = 1;
+  size_t total = 0;
   for (auto& b : j->blocks) {
     if ((int)b.has_literal + (int)b.has_cabac + (int)b.has_skip != 1)
       return fail(c, AVR_ERR_FORMAT, "Invalid input block: must have exactly one type");
     if (b.has_literal) {
-      j->stream.insert(j->stream.end(), b.literal, b.literal + b.literal_len);
+      total += b.literal_len;
     } else if (b.has_cabac) {
       if (!b.has_size) return fail(c, AVR_ERR_FORMAT, "CABAC block requires size field.");
       if (b.size < avr::kSurrogateMarkerBytes || b.size > ((int64_t)1 << 31))
         return fail(c, AVR_ERR_FORMAT, "Invalid coded block size for surrogate: " + std::to_string(b.size));
-      uint8_t mk[8];
-      avr::surrogate_marker(seq++, mk);
-      j->stream.insert(j->stream.end(), mk, mk + 8);
-      j->stream.insert(j->stream.end(), (size_t)b.size - 8, (uint8_t)'X');
+      total += (size_t)b.size;
     } else if (!b.skip_coded) {
       return fail(c, AVR_ERR_FORMAT, "Unknown input block type");
     }
   }
+  j->stream.resize(total);
+  {
+    std::vector<avr::PbCopy> fills;
+    fills.reserve(j->blocks.size());
+    size_t at = 0;
+    for (auto& b : j->blocks) {
+      if (b.has_literal) {
+        if (b.literal_len) fills.push_back({at, b.literal, b.literal_len});
+        at += b.literal_len;
+      } else if (b.has_cabac) {
+        avr::surrogate_marker(seq++, j->stream.data() + at);
+        fills.push_back({at + 8, nullptr, (size_t)b.size - 8});
+        at += (size_t)b.size;
+      }
+    }
+    parallel_copies(fills, j->stream.data(), (uint8_t)'X');
+  }
+  if (tm) fprintf(stderr, "setup: pb+stream %.3f s\n", now_s() - t0), t0 = now_s();
   ParsedFile pf;
-  if (int r = parse_file(c, j->stream.data(), j->stream.size(), &pf)) return r;
+  if (int r = parse_file(c, j->stream.data(), j->stream.size(), &pf, /*views=*/true)) return r;
+  if (tm) fprintf(stderr, "setup: parse %.3f s\n", now_s() - t0), t0 = now_s();
   // recognize_coded_block (recode.cpp:1546-1573): slices claim coded blocks in order
   j->desc_of_block.assign(j->blocks.size(), -1);
   size_t next_coded = 0;
@@ -1054,17 +1109,50 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
     descs.push_back(d);
     next_coded++;
   }
-  // all checks passed: append to the shared plan
+  // all checks passed: append to the shared plan (append_aligned's layout: 16-byte aligned streams,
+  // each followed by >= 16 zero bytes), the re-coded streams copied on host threads
+  if (!plan) {
+    for (size_t k = 0; k < descs.size(); k++) j->desc_of_block[block_of[k]] = (int)k;
+    return AVR_OK;
+  }
+  std::vector<avr::PbCopy> copies;
+  copies.reserve(descs.size());
+  uint64_t at = plan->layout_only ? plan->arena_end : plan->arena.size();
   for (size_t k = 0; k < descs.size(); k++) {
-    avr_slice_desc d = descs[k];
+    avr_slice_desc& d = descs[k];
     const avr::PbBlock& b = j->blocks[block_of[k]];
     if (d.coded) {
-      append_aligned(&plan->arena, b.cabac, b.cabac_len, 16, &d.payload_offset);
+      d.payload_offset = (at + 15) & ~(uint64_t)15;
+      copies.push_back({(size_t)d.payload_offset, b.cabac, b.cabac_len});
+      at = d.payload_offset + b.cabac_len + 16;
       plan->max_w = std::max(plan->max_w, ring_cols(d));
     }
-    j->desc_of_block[block_of[k]] = (int)plan->descs.size();
-    plan->descs.push_back(d);
   }
+  if (plan->layout_only) {
+    plan->arena_copies.insert(plan->arena_copies.end(), copies.begin(), copies.end());
+    plan->arena_end = at;
+    for (size_t k = 0; k < descs.size(); k++) {
+      j->desc_of_block[block_of[k]] = (int)plan->descs.size();
+      plan->descs.push_back(descs[k]);
+    }
+    return AVR_OK;
+  }
+  const size_t a0 = plan->arena.size();
+  plan->arena.resize(at);
+  {
+    uint64_t z = a0;   // the zero bytes between the streams
+    for (const auto& cp : copies) {
+      memset(plan->arena.data() + z, 0, cp.dst - z);
+      z = cp.dst + cp.len;
+    }
+    memset(plan->arena.data() + z, 0, at - z);
+  }
+  parallel_copies(copies, plan->arena.data());
+  for (size_t k = 0; k < descs.size(); k++) {
+    j->desc_of_block[block_of[k]] = (int)plan->descs.size();
+    plan->descs.push_back(descs[k]);
+  }
+  if (tm) fprintf(stderr, "setup: match+arena %.3f s\n", now_s() - t0);
   return AVR_OK;
 }
 
@@ -1095,14 +1183,6 @@ int splice_job(avr_ctx* c, const DecJob& j, Slice&& slice, std::vector<uint8_t>*
       else if (n) o->back() = (uint8_t)b.last_byte[0];
     }
   }
-  return AVR_OK;
-}
-
-int malloc_copy(const std::vector<uint8_t>& v, uint8_t** out, size_t* out_len) {
-  *out = (uint8_t*)malloc(v.size() ? v.size() : 1);
-  if (!*out) return AVR_ERR_OUT_OF_MEMORY;
-  if (!v.empty()) memcpy(*out, v.data(), v.size());
-  *out_len = v.size();
   return AVR_OK;
 }
 
@@ -1212,25 +1292,164 @@ const char* avr_last_error(const avr_ctx* c) { return c ? c->err.c_str() : "no c
 
 void avr_free(void* p) { free(p); }
 
-int avr_plan_decompress(const uint8_t* avrc, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
-                        size_t* arena_len, size_t* work_len, int* max_mb_width, int* max_mb_height) {
-  if (!avrc || !descs || !n_slices || !arena || !arena_len || !work_len || !max_mb_width || !max_mb_height)
+// ------------------------------------------------------------------ sharded decompress plans
+// decompressor::run (recode.cpp:1338-1409) cut in two around the device work: load = read_packet's
+// surrogate stream parsed and matched to the container's coded blocks (decompress_setup in layout
+// mode: descs and the arena layout, no bytes copied), then the arena written where the caller wants
+// it, and the splice of the regenerated slices with the literals and the last-byte patch
+// (recode.cpp:1345-1356).  A handle keeps its scratch (the surrogate stream) for the next load.
+}  // extern "C"
+struct avr_dec_plan {
+  DecJob job;
+  Plan plan;
+  uint64_t work = 0;
+  int max_h = 1;
+  const uint8_t* avrc = nullptr;   // the caller's container (the blocks point into it)
+  size_t n = 0;
+};
+extern "C" {
+
+int avr_dec_plan_new(avr_dec_plan** out) {
+  if (!out) return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(nullptr, [&]() -> int {
+    *out = new avr_dec_plan();
+    return AVR_OK;
+  });
+}
+
+void avr_dec_plan_free(avr_dec_plan* h) { delete h; }
+
+int avr_dec_plan_load(avr_dec_plan* h, const uint8_t* avrc, size_t n, int* n_slices, size_t* arena_len,
+                      size_t* work_len, int* max_mb_width, int* max_mb_height) {
+  if (!h || !avrc || !n_slices || !arena_len || !work_len || !max_mb_width || !max_mb_height)
     return AVR_ERR_INVALID_ARGUMENT;
   return guarded(nullptr, [&]() -> int {
-    DecJob j;
-    Plan plan;
-    if (int r = decompress_setup(nullptr, avrc, n, &j, &plan)) return r;
-    if (!j.parallel) return AVR_ERR_UNSUPPORTED;   // the reference model's slices chain: no split
+    h->avrc = nullptr;
+    h->job.blocks.clear();
+    h->job.desc_of_block.clear();
+    h->job.stream.clear();   // keeps its capacity: the next stream is written over mapped pages
+    h->plan.descs.clear();
+    h->plan.arena_copies.clear();
+    h->plan.arena_end = 0;
+    h->plan.max_w = 1;
+    h->plan.layout_only = true;
+    if (int r = decompress_setup(nullptr, avrc, n, &h->job, &h->plan)) return r;
+    if (!h->job.parallel) return AVR_ERR_UNSUPPORTED;   // the reference model's slices chain: no split
     uint64_t w = 0;
     int mh = 1;
-    for (auto& d : plan.descs) {
+    for (auto& d : h->plan.descs) {
       d.out_offset = w;
       w += ((uint64_t)d.out_capacity + 15) & ~15ull;
       mh = std::max(mh, d.mb_height);
     }
-    plan.arena.resize(plan.arena.size() + 16, 0);
-    *descs = (avr_slice_desc*)malloc(sizeof(avr_slice_desc) * std::max<size_t>(1, plan.descs.size()));
-    *arena = (uint8_t*)malloc(plan.arena.size());
+    h->avrc = avrc;
+    h->n = n;
+    h->work = w;
+    h->max_h = mh;
+    *n_slices = (int)h->plan.descs.size();
+    *arena_len = h->plan.arena_end + 16;
+    *work_len = w;
+    *max_mb_width = h->plan.max_w;
+    *max_mb_height = mh;
+    return AVR_OK;
+  });
+}
+
+int avr_dec_plan_descs(const avr_dec_plan* h, avr_slice_desc* out) {
+  if (!h || !h->avrc || (!out && !h->plan.descs.empty())) return AVR_ERR_INVALID_ARGUMENT;
+  if (!h->plan.descs.empty()) memcpy(out, h->plan.descs.data(), sizeof(avr_slice_desc) * h->plan.descs.size());
+  return AVR_OK;
+}
+
+int avr_dec_plan_arena(const avr_dec_plan* h, uint8_t* out, size_t cap) {
+  if (!h || !h->avrc || !out || cap < h->plan.arena_end + 16) return AVR_ERR_INVALID_ARGUMENT;
+  return guarded(nullptr, [&]() -> int {
+    const auto& cp = h->plan.arena_copies;
+    const uint64_t end = h->plan.arena_end + 16;
+    uint64_t z = 0;   // the zero bytes between and after the streams
+    for (const auto& c : cp) {
+      memset(out + z, 0, c.dst - z);
+      z = c.dst + c.len;
+    }
+    memset(out + z, 0, end - z);
+    parallel_copies(cp, out);
+    return AVR_OK;
+  });
+}
+
+}  // extern "C"
+namespace {
+// splice_job's output laid out: the literal and regenerated-slice copies, the last-byte patches
+// (position, byte) and the total length.
+int splice_layout(const avr_dec_plan* h, const int32_t* status, const uint8_t* regen, size_t regen_len,
+                  const uint64_t* offsets, const uint32_t* lens, std::vector<avr::PbCopy>* copies,
+                  std::vector<std::pair<size_t, uint8_t>>* patches, size_t* total) {
+  const DecJob& j = h->job;
+  const int ns = (int)h->plan.descs.size();
+  // every slice's regenerated bytes inside regen and within its own output capacity
+  for (int k = 0; k < ns; k++)
+    if (status[k] == 0 && (offsets[k] > regen_len || lens[k] > regen_len - offsets[k] ||
+                           lens[k] > h->plan.descs[k].out_capacity))
+      return AVR_ERR_INVALID_ARGUMENT;
+  copies->reserve(j.blocks.size());
+  size_t at = 0;
+  for (size_t i = 0; i < j.blocks.size(); i++) {
+    const avr::PbBlock& b = j.blocks[i];
+    if (b.has_literal) {
+      if (b.literal_len) copies->push_back({at, b.literal, b.literal_len});
+      at += b.literal_len;
+      continue;
+    }
+    if (!b.has_cabac) continue;
+    const int k = j.desc_of_block[i];
+    if (k < 0) return AVR_ERR_FORMAT;          // "Not all blocks were decoded." (recode.cpp:1354)
+    if (status[k]) return AVR_ERR_FORMAT;      // the slice failed to decode
+    const size_t len = lens[k];
+    if (len) copies->push_back({at, regen + offsets[k], len});
+    size_t m = len;
+    if (b.has_parity && b.has_last_byte && !b.last_byte.empty()) {   // recode.cpp:1345-1356
+      if ((int)b.length_parity != (int)(m & 1)) patches->push_back({at + m, (uint8_t)b.last_byte[0]}), m++;
+      else if (m) patches->push_back({at + m - 1, (uint8_t)b.last_byte[0]});
+    }
+    at += m;
+  }
+  *total = at;
+  return AVR_OK;
+}
+}  // namespace
+extern "C" {
+
+int avr_dec_plan_splice(const avr_dec_plan* h, const int32_t* status, const uint8_t* regen, size_t regen_len,
+                        const uint64_t* offsets, const uint32_t* lens, uint8_t* out, size_t out_cap, size_t* out_len) {
+  const int ns = h ? (int)h->plan.descs.size() : 0;
+  if (!h || !h->avrc || !out_len || (ns && (!status || !regen || !offsets || !lens))) return AVR_ERR_INVALID_ARGUMENT;
+  *out_len = 0;
+  return guarded(nullptr, [&]() -> int {
+    std::vector<avr::PbCopy> copies;
+    std::vector<std::pair<size_t, uint8_t>> patches;
+    size_t total = 0;
+    if (int r = splice_layout(h, status, regen, regen_len, offsets, lens, &copies, &patches, &total)) return r;
+    *out_len = total;
+    if (total > out_cap || (total && !out)) return AVR_ERR_INVALID_ARGUMENT;
+    parallel_copies(copies, out);
+    for (const auto& pt : patches) out[pt.first] = pt.second;
+    return AVR_OK;
+  });
+}
+
+int avr_plan_decompress(const uint8_t* avrc, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
+                        size_t* arena_len, size_t* work_len, int* max_mb_width, int* max_mb_height) {
+  if (!avrc || !descs || !n_slices || !arena || !arena_len || !work_len || !max_mb_width || !max_mb_height)
+    return AVR_ERR_INVALID_ARGUMENT;
+  *descs = nullptr;
+  *arena = nullptr;
+  return guarded(nullptr, [&]() -> int {
+    avr_dec_plan h;
+    int ns = 0;
+    size_t al = 0;
+    if (int r = avr_dec_plan_load(&h, avrc, n, &ns, &al, work_len, max_mb_width, max_mb_height)) return r;
+    *descs = (avr_slice_desc*)malloc(sizeof(avr_slice_desc) * std::max(1, ns));
+    *arena = host_alloc(al);
     if (!*descs || !*arena) {
       free(*descs);
       free(*arena);
@@ -1238,13 +1457,10 @@ int avr_plan_decompress(const uint8_t* avrc, size_t n, avr_slice_desc** descs, i
       *arena = nullptr;
       return AVR_ERR_OUT_OF_MEMORY;
     }
-    if (!plan.descs.empty()) memcpy(*descs, plan.descs.data(), sizeof(avr_slice_desc) * plan.descs.size());
-    memcpy(*arena, plan.arena.data(), plan.arena.size());
-    *n_slices = (int)plan.descs.size();
-    *arena_len = plan.arena.size();
-    *work_len = w;
-    *max_mb_width = plan.max_w;
-    *max_mb_height = mh;
+    avr_dec_plan_descs(&h, *descs);
+    if (int r = avr_dec_plan_arena(&h, *arena, al)) return r;
+    *n_slices = ns;
+    *arena_len = al;
     return AVR_OK;
   });
 }
@@ -1254,25 +1470,24 @@ int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int3
                          size_t* out_len) {
   if (!avrc || n_slices < 0 || (n_slices && (!status || !regen || !offsets || !lens)) || !out || !out_len)
     return AVR_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
   return guarded(nullptr, [&]() -> int {
-    DecJob j;
-    Plan plan;
-    if (int r = decompress_setup(nullptr, avrc, n, &j, &plan)) return r;
-    if (!j.parallel) return AVR_ERR_UNSUPPORTED;
-    if ((int)plan.descs.size() != n_slices) return AVR_ERR_INVALID_ARGUMENT;
-    // every slice's regenerated bytes inside regen and within its own output capacity
-    for (int k = 0; k < n_slices; k++)
-      if (status[k] == 0 && (offsets[k] > regen_len || lens[k] > regen_len - offsets[k] ||
-                             lens[k] > plan.descs[k].out_capacity))
-        return AVR_ERR_INVALID_ARGUMENT;
-    std::vector<uint8_t> o;
-    if (int r = splice_job(nullptr, j, [&](int k, const uint8_t** p, size_t* len) {
-          *p = regen + offsets[k];
-          *len = lens[k];
-          return (int)status[k];
-        }, &o))
-      return r;
-    return malloc_copy(o, out, out_len);
+    avr_dec_plan h;
+    int ns = 0, mw = 0, mh = 0;
+    size_t al = 0, wl = 0;
+    if (int r = avr_dec_plan_load(&h, avrc, n, &ns, &al, &wl, &mw, &mh)) return r;
+    if (ns != n_slices) return AVR_ERR_INVALID_ARGUMENT;
+    std::vector<avr::PbCopy> copies;
+    std::vector<std::pair<size_t, uint8_t>> patches;
+    size_t total = 0;
+    if (int r = splice_layout(&h, status, regen, regen_len, offsets, lens, &copies, &patches, &total)) return r;
+    uint8_t* o = host_alloc(total);
+    if (!o) return AVR_ERR_OUT_OF_MEMORY;
+    parallel_copies(copies, o);
+    for (const auto& pt : patches) o[pt.first] = pt.second;
+    *out = o;
+    *out_len = total;
+    return AVR_OK;
   });
 }
 
@@ -1344,7 +1559,7 @@ int avr_assemble_container(const uint8_t* file, size_t n, int model, int n_slice
     return AVR_ERR_INVALID_ARGUMENT;
   return guarded(nullptr, [&]() -> int {
     ParsedFile pf;
-    if (int r = parse_file(nullptr, file, n, &pf)) return r;
+    if (int r = parse_file(nullptr, file, n, &pf, /*views=*/true)) return r;
     if ((size_t)n_slices != pf.slices.size()) return AVR_ERR_INVALID_ARGUMENT;
     return assemble(file, n, model, views_of(pf), status, recoded, recoded_len, offsets, lens, out, out_len);
   });
@@ -1669,7 +1884,7 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
   *arena = nullptr;
   return guarded(nullptr, [&]() -> int {
     ParsedFile pf;
-    if (int r = parse_file(nullptr, file, n, &pf)) return r;
+    if (int r = parse_file(nullptr, file, n, &pf, /*views=*/true)) return r;
     // the arena's layout first (append_aligned's: 16-byte aligned payloads, each followed by >= 16
     // zero bytes), then one zeroed allocation and the payload copies on host threads
     const size_t ns = pf.slices.size();
@@ -2248,6 +2463,7 @@ int lazy_device_work(avr_hooks_session* hs, size_t i, bool trace, size_t batch =
     // the regenerated payload in place of the surrogate one; the NAL's bytes after the payload
     // (from the literal that follows the block) stay, as does the parse's read limit
     avr::SliceInfo& s = hs->pf.slices[k];
+    s.own();
     if (g.size() != s.size || s.rbsp.size() < s.h.cabac_start + s.size)
       return fail(hs->c, AVR_ERR_FORMAT, "slice " + std::to_string(k) + " regenerated " + std::to_string(g.size()) +
                                              " bytes for a " + std::to_string(s.size) + "-byte payload");
@@ -2365,7 +2581,7 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
             hs->model = m;
             hs->original.assign(avrc, avrc + n);   // the container (the job's blocks point into it)
             if (int e = decompress_setup(c, hs->original.data(), hs->original.size(), &hs->job, &hs->dplan)) return e;
-            hs->stream = hs->job.stream;
+            hs->stream.assign(hs->job.stream.begin(), hs->job.stream.end());
             if (int e = parse_file(c, hs->stream.data(), hs->stream.size(), &hs->pf)) return e;
             if (!coded_from_container(hs->job.blocks, hs->pf.slices.size(), &hs->coded))
               return fail(c, AVR_ERR_FORMAT, "hooks: container blocks do not match the file's slices");

@@ -105,6 +105,18 @@ std::vector<uint8_t> unescape(const uint8_t* src, size_t n) {
   return out;
 }
 
+// Does unescape() remove anything: is there a 00 00 03 in the n bytes at src?
+bool has_epb(const uint8_t* src, size_t n) {
+  for (size_t k = 2; k < n;) {
+    const uint8_t* p = (const uint8_t*)memchr(src + k, 3, n - k);
+    if (!p) return false;
+    const size_t q = (size_t)(p - src);
+    if (src[q - 1] == 0 && src[q - 2] == 0) return true;
+    k = q + 1;
+  }
+  return false;
+}
+
 // FFmpeg 2.8 decode_nal_units: trailing zero bytes dropped, stop bit excluded.
 size_t rbsp_bit_length(const uint8_t* rbsp, size_t n) {
   while (n > 0 && rbsp[n - 1] == 0) n--;
@@ -524,11 +536,15 @@ bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals) {
   return !nals->empty();   // nothing H.264 in it: av_decoder::run throws (recode.cpp:92-93)
 }
 
-bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s) {
+bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s, bool views) {
   if (n < 2) return false;
   const int type = nal[0] & 0x1f, ref_idc = (nal[0] >> 5) & 3;
   if (type != 1 && type != 5 && type != 6 && type != 7 && type != 8) return false;
-  std::vector<uint8_t> rbsp = unescape(nal + 1, n - 1);
+  // a slice NAL without emulation-prevention bytes is its own RBSP: no copy when views are allowed
+  const bool view = views && (type == 1 || type == 5) && !has_epb(nal + 1, n - 1);
+  std::vector<uint8_t> rbsp = view ? std::vector<uint8_t>() : unescape(nal + 1, n - 1);
+  const uint8_t* rd = view ? nal + 1 : rbsp.data();
+  const size_t rn = view ? n - 1 : rbsp.size();
   if (type == 6) {
     int b = parse_x264_build(rbsp.data(), rbsp.size());
     if (b > 0) x264_build_ = b;
@@ -543,7 +559,7 @@ bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s) {
     return false;
   }
   SliceHeader h;
-  if (!parse_slice_header(sps_, pps_, rbsp.data(), rbsp.size(), type, ref_idc, &h) || !h.entropy_coding_mode)
+  if (!parse_slice_header(sps_, pps_, rd, rn, type, ref_idc, &h) || !h.entropy_coding_mode)
     return false;
   h.x264_build = x264_build_;
   const SliceHeader& p = prev_;
@@ -563,12 +579,17 @@ bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s) {
   have_prev_ = true;
   s->h = h;
   s->picture_id = picture_id_;
-  const size_t bits = rbsp_bit_length(rbsp.data(), rbsp.size());
+  const size_t bits = rbsp_bit_length(rd, rn);
   const size_t end = (bits + 7) / 8;
   s->size = end > h.cabac_start ? end - h.cabac_start : 0;
-  s->read_limit = rbsp.size() > h.cabac_start + s->size ? s->size + 1 : s->size;
-  s->verbatim = rbsp.size() == n - 1;
-  s->rbsp = std::move(rbsp);
+  s->read_limit = rn > h.cabac_start + s->size ? s->size + 1 : s->size;
+  s->verbatim = rn == n - 1;
+  if (view) {
+    s->view = rd;
+    s->view_len = rn;
+  } else {
+    s->rbsp = std::move(rbsp);
+  }
   return true;
 }
 

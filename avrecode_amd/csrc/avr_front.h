@@ -36,12 +36,19 @@ struct SliceInfo {
   SliceHeader h;
   int picture_id = 0;
   size_t nal_offset = 0, nal_size = 0;   // escaped NAL in the file
-  std::vector<uint8_t> rbsp;             // unescaped NAL payload after the header byte
+  std::vector<uint8_t> rbsp;             // unescaped NAL payload after the header byte (owned), or
+  const uint8_t* view = nullptr;         //   these view_len bytes of the parsed buffer when the NAL
+  size_t view_len = 0;                   //   has no emulation-prevention bytes (StreamParser views)
   size_t size = 0;                       // init_decoder size
   size_t read_limit = 0;                 // bytes a decoder may read from the payload start
   bool verbatim = false;                 // the NAL has no emulation-prevention bytes: the payload
                                          //   is the file's bytes at file_payload_offset()
-  const uint8_t* payload() const { return rbsp.data() + h.cabac_start; }
+  const uint8_t* rbsp_data() const { return view ? view : rbsp.data(); }
+  size_t rbsp_size() const { return view ? view_len : rbsp.size(); }
+  const uint8_t* payload() const { return rbsp_data() + h.cabac_start; }
+  void own() {   // copy a view (before writing to rbsp)
+    if (view) rbsp.assign(view, view + view_len), view = nullptr, view_len = 0;
+  }
   uint64_t file_payload_offset() const { return verbatim ? nal_offset + 1 + h.cabac_start : ~(uint64_t)0; }
 };
 
@@ -67,8 +74,10 @@ void mp4_sample_nals(const uint8_t* file, const NalRef& sample, int len_size, st
 // Stateful walk over a NAL sequence (parameter sets, x264 SEI, picture boundaries).
 class StreamParser {
  public:
-  // Returns true and fills *s when the NAL is a CABAC slice FFmpeg would decode.
-  bool next(const uint8_t* nal, size_t n, SliceInfo* s);
+  // Returns true and fills *s when the NAL is a CABAC slice FFmpeg would decode.  views: a slice
+  // NAL without emulation-prevention bytes is not copied (SliceInfo::view points into nal, which
+  // must outlive *s).
+  bool next(const uint8_t* nal, size_t n, SliceInfo* s, bool views = false);
 
  private:
   Sps sps_[32];

@@ -221,6 +221,47 @@ def sharded_decompress(ctx, avrc: bytes, device=None, run_range=None) -> bytes |
     return splice_container(avrc, st, blob, offs, lens)
 
 
+def scatter_parsed(ps: "ParsedStream | None", ranges, device, src: int = 0):
+    """Rank src's decompress batch (ps, e.g. DecompressPlan.parsed of the container it assembled) cut
+    into the contiguous slice ranges `ranges` (one [lo, hi) per rank): each rank receives its own as
+    (descs, arena, n, work_len, max_mb_width, max_mb_height) -- host arrays on src, the arena as a
+    device tensor elsewhere (point-to-point over RCCL / xGMI: one header, the descriptors and the
+    re-coded streams per rank; gloo moves host tensors).  Offsets are rebased as in subset()."""
+    import torch
+    import torch.distributed as dist
+
+    from . import SLICE_DESC
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if rank == src:
+        mine = None
+        for r in range(world):
+            lo, hi = ranges[r]
+            sub = ps if (lo, hi) == (0, len(ps.descs)) else subset(ps, lo, hi)
+            if r == rank:
+                mine = sub
+                continue
+            hdr = torch.tensor([hi - lo, sub.arena.nbytes, sub.work_len, sub.max_mb_width, sub.max_mb_height],
+                               dtype=torch.int64, device=device)
+            dist.send(hdr, r)
+            if hi > lo:
+                dist.send(torch.from_numpy(np.ascontiguousarray(sub.descs).view(np.uint8).reshape(-1)).to(device), r)
+                dist.send(torch.from_numpy(sub.arena).to(device), r)
+        return (mine.descs, mine.arena, len(mine.descs), mine.work_len, mine.max_mb_width, mine.max_mb_height)
+    hdr = torch.zeros(5, dtype=torch.int64, device=device)
+    dist.recv(hdr, src)
+    n, alen, wlen, mw, mh = (int(x) for x in hdr.cpu())
+    descs = np.zeros(0, dtype=SLICE_DESC)
+    arena = torch.zeros(16, dtype=torch.uint8, device=device)
+    if n:
+        d = torch.empty(n * SLICE_DESC.itemsize, dtype=torch.uint8, device=device)
+        dist.recv(d, src)
+        descs = d.cpu().numpy().view(SLICE_DESC)
+        arena = torch.empty(alen, dtype=torch.uint8, device=device)
+        dist.recv(arena, src)
+    return descs, arena, n, wlen, mw, mh
+
+
 def deal_files(sizes, world: int) -> list[list[int]]:
     """Files to ranks, whole: longest-processing-time-first by bytes (the largest file goes to the
     least-loaded rank).  Returns each rank's file indices in ascending order."""

@@ -378,9 +378,17 @@ def rmode_files_section(ctx, args):
 def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     """BASELINE configs[3]: ONE 4K stream (1 slice per frame, a 1-s GOP I + 29 P tiled to
     `seconds` with rewritten frame numbers) cut by NAL unit into contiguous slice ranges balanced
-    by bytes (shard.partition), one range per GPU.  Timed: every rank's device roundtrip of its
-    range (compress + decompress + verify), the device pack of its re-coded blocks, the RCCL gather
-    to rank 0 (shard.gather_flat) and rank 0's Recoded container assembly.  value = stream bytes /
+    by bytes (shard.partition), one range per GPU.  One timed step is the reference's `roundtrip`
+    (recode.cpp:1594-1624) of the whole stream, sharded:
+      compress    every rank's device compress of its range, the device pack of its re-coded
+                  blocks, the gather to rank 0 (shard.gather_flat over RCCL) and rank 0's Recoded
+                  container assembly (avr_assemble_container_into, into one reused buffer);
+      decompress  rank 0's plan of that container (decompressor::run's read_packet parse,
+                  avr_dec_plan_load: no bytes copied) and the re-coded streams' arena, the scatter of
+                  each rank's range of it (shard.scatter_parsed over RCCL), every rank's device
+                  decompress + pack, the gather of the regenerated slices to rank 0 and its splice
+                  with the container's literals and the last-byte patch (avr_dec_plan_splice).
+    The spliced file is compared with the stream outside the timed region.  value = stream bytes /
     max-over-ranks time (strong scaling: the stream is the same at every N).  Returns rank 0's
     record (None elsewhere)."""
     import numpy as np
@@ -389,7 +397,7 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
 
     import avrecode_amd as avr
     from avrecode_amd import shard, workloads
-    from avrecode_amd.batch import DeviceBatch
+    from avrecode_amd.batch import DecompressRange, DeviceBatch
 
     model = avr.MODEL_PARALLEL
     progress(f"rank {rank}: generating the {seconds}-s stream")
@@ -406,44 +414,76 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     setup["subset_s"] = time.perf_counter() - t
     t = time.perf_counter()
     batch = DeviceBatch(ctx, part)
+    drange = DecompressRange(ctx, dev)
     torch.cuda.synchronize()
     setup["h2d_s"] = time.perf_counter() - t
     progress(f"rank {rank}: slices [{lo}, {hi}) resident on the GPU ({setup['h2d_s']:.1f} s)")
     stream = torch.cuda.Stream(dev)
     mk = lambda: [torch.cuda.Event(enable_timing=True) for _ in range(4)]  # noqa: E731
     gdev = _coll(dev)
-    PH = ("kernels_s", "results_d2h_s", "gather_s", "assemble_s")
+    n_mine = hi - lo
+    dplan = avr.DecompressPlan() if rank == 0 else None
+    bufs = {}   # rank 0's container, arena and file buffers: allocated at the first step, then reused
 
-    cbuf = [None]   # rank 0's container buffer: allocated at the first step, reused (already mapped)
+    def buf(name, need):
+        b = bufs.get(name)
+        if b is None or b.nbytes < need:
+            b = bufs[name] = np.empty(need + need // 64 + 4096, dtype=np.uint8)
+        return b
 
     def step(ev, ph):
-        # wall-clock phases of one step: device roundtrip + pack; per-slice results to the host;
-        # the gather to rank 0 (RCCL send/recv, device to device, then one D2H into one array);
-        # rank 0's container assembly from its own parse (no second parse of the stream), written
-        # into one reused buffer
-        t0 = time.perf_counter()
-        batch.roundtrip_timed(ev, model, stream)
+        marks = [time.perf_counter()]
+
+        def mark(name):
+            marks.append(time.perf_counter())
+            ph[name] = ph.get(name, 0.0) + marks[-1] - marks[-2]
+
+        # compress: device compress + pack, results to the host, gather, assembly
+        ev[0].record(stream)
+        batch.compress(model, stream)
+        ev[1].record(stream)
         flat, d_off = batch.pack(stream)
         stream.synchronize()
-        t1 = time.perf_counter()
-        v = batch.verdicts()
+        mark("compress_s")
         res = batch.results("c")
-        offs = d_off.cpu().numpy()[: hi - lo].astype(np.int64)
-        lens = np.where(res["status"] == 0, res["out_len"], 0).astype(np.int64)
-        st = np.where(v == 1, 0, -1).astype(np.int64)
-        t2 = time.perf_counter()
+        offs = d_off[:n_mine].cpu().numpy().astype(np.int64)
+        ok_c = res["status"] == 0
+        lens = np.where(ok_c, res["out_len"], 0).astype(np.int64)
+        st = np.where(ok_c, 0, -1).astype(np.int64)
+        mark("results_d2h_s")
         g = shard.gather_flat(flat, st, offs, lens, dst=0, device=gdev)
-        t3 = time.perf_counter()
-        avrc = None
+        mark("gather_s")
+        avrc = pp = dranges = None
         if g is not None:
             need = avr.container_bound(len(data), len(g[0]), int(np.asarray(g[3], dtype=np.int64).sum()))
-            if cbuf[0] is None or cbuf[0].nbytes < need:
-                cbuf[0] = np.empty(need + need // 64, dtype=np.uint8)
-            avrc = avr.assemble_container(data, *g, model=model, ps=ps, out=cbuf[0])
-        t4 = time.perf_counter()
-        for k, dt in zip(PH, (t1 - t0, t2 - t1, t3 - t2, t4 - t3)):
-            ph[k] = ph.get(k, 0.0) + dt
-        return avrc, bool((v == 1).all())
+            avrc = avr.assemble_container(data, *g, model=model, ps=ps, out=buf("container", need))
+        mark("assemble_s")
+        # decompress: rank 0 plans the container, every rank regenerates its range
+        if rank == 0:
+            dplan.load(avrc)
+            pp = dplan.parsed(buf("arena", dplan.arena_len))
+            dranges = shard.partition(pp.descs["payload_size"], world)
+        mark("plan_s")
+        descs, arena, nd, wl, mw, mh = shard.scatter_parsed(pp, dranges, gdev)
+        drange.upload(descs, arena, nd, wl, mw, mh, stream)
+        torch.cuda.synchronize()
+        mark("scatter_h2d_s")
+        ev[2].record(stream)
+        drange.run(model, stream)
+        ev[3].record(stream)
+        dflat, dd_off = drange.pack(stream)
+        stream.synchronize()
+        mark("decompress_s")
+        dres = drange.results()
+        dlens = np.where(dres["status"] == 0, dres["out_len"], 0).astype(np.int64)
+        doffs = dd_off[:nd].cpu().numpy().astype(np.int64)
+        gd = shard.gather_flat(dflat, dres["status"].astype(np.int64), doffs, dlens, dst=0, device=gdev)
+        mark("gather_d_s")
+        out = None
+        if gd is not None:
+            out = dplan.splice(*gd, out=buf("file", len(data)))
+        mark("splice_s")
+        return avrc, out, int(lens.sum())
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
@@ -454,38 +494,38 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ok = True
         phases = {}
         for k in range(args.stream_steps):
-            avrc, good = step(evs[k], phases)
-            ok = ok and good
+            avrc, out, C = step(evs[k], phases)
             progress(f"rank {rank}: step {k} done")
         torch.cuda.synchronize()
         dist.barrier()
         elapsed = time.perf_counter() - t0
+    # the last step's spliced file must be the stream (checked outside the timed region)
+    good = True
+    if rank == 0:
+        good = out is not None and len(out) == len(data) and np.array_equal(out, np.frombuffer(data, dtype=np.uint8))
     mx = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
-    bad = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=gdev)
+    bad = torch.tensor([0.0 if good else 1.0], dtype=torch.float64, device=gdev)
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     dist.all_reduce(bad, op=dist.ReduceOp.SUM)
     t = torch.cat([mx, bad])
     if rank != 0:
         return None
-    # the container must decompress to the stream (checked outside the timed region)
-    exact = bool(t[1] == 0) and ctx.decompress(avrc) == data
+    exact = bool(t[1] == 0)
     t_comp = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
     t_dec = sum(e[2].elapsed_time(e[3]) for e in evs) / len(evs) / 1e3
-    v = batch.verdicts()
     S = int(part.descs["payload_size"].sum())
-    C = int(batch.results("c")["out_len"][v == 1].sum())
     dominant, t_dom = ("compress", t_comp) if t_comp >= t_dec else ("decompress", t_dec)
     kernel_name = KERNEL_NAMES[dominant]
     rec = {
         "metric": METRIC, "value": len(data) * args.stream_steps / float(t[0]) / 1e6, "unit": "MB/s",
         "n_gpus": world, "steps": args.stream_steps, "warmup": args.warmup,
         "ms_per_step": float(t[0]) / args.stream_steps * 1e3, "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "u64", "data": "synthetic (device generator, seeded; one GOP tiled)",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (device generator, seeded; one GOP tiled)",
         "bit_exact": exact,
-        "config": {"workload": "one 4K stream sharded by NAL unit, RCCL gather reassembly (BASELINE configs[3])"
+        "config": {"workload": "one 4K stream sharded by NAL unit: compress, RCCL gather, container assembly, "
+                               "container plan, RCCL scatter, decompress, RCCL gather, splice (BASELINE configs[3])"
                                + ("" if seconds == 600 else f"; REDUCED stream: {seconds} s of the config's 600 s"),
                    "seconds": seconds, "fps": 30, "mb": list(args.stream_mb), "slices": len(ps.descs),
                    "stream_bytes": len(data), "container_bytes": len(avrc), "model": "parallel",
@@ -788,7 +828,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u64",
+            "dtype": "u8",
             "data": "synthetic (device generator, seeded)",
             "bit_exact": bit_exact and bad == 0,
             "config": {

@@ -289,6 +289,27 @@ int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int3
                          size_t regen_len, const uint64_t* offsets, const uint32_t* lens, uint8_t** out,
                          size_t* out_len);
 
+/* The sharded decompress's host halves on one parse (decompressor::run, recode.cpp:1338-1409):
+ * a plan handle loads a PARALLEL-model container -- read_packet's surrogate stream parsed and
+ * matched to the coded blocks, as avr_plan_decompress, but without copying any bytes yet -- then
+ * writes the descriptors and the re-coded streams' arena where the caller wants them (the arena
+ * with host threads), and splices the regenerated slices with the literals and the last-byte patch
+ * (recode.cpp:1345-1356) into the caller's buffer, as avr_splice_container.  The container must stay
+ * alive and unchanged from avr_dec_plan_load to the last call on it; a handle keeps its scratch
+ * (the surrogate stream's buffer) for the next load.  arena_len / work_len / max_mb_* as
+ * avr_plan_decompress.  avr_dec_plan_splice: *out_len = the file's size; AVR_ERR_INVALID_ARGUMENT
+ * when out_cap is smaller (nothing written) or a slice's bytes lie outside regen or past its
+ * capacity, AVR_ERR_FORMAT when a coded block has no slice or a slice's status is not 0. */
+typedef struct avr_dec_plan avr_dec_plan;
+int avr_dec_plan_new(avr_dec_plan** out);
+void avr_dec_plan_free(avr_dec_plan* plan);
+int avr_dec_plan_load(avr_dec_plan* plan, const uint8_t* avrc, size_t n, int* n_slices, size_t* arena_len,
+                      size_t* work_len, int* max_mb_width, int* max_mb_height);
+int avr_dec_plan_descs(const avr_dec_plan* plan, avr_slice_desc* out);
+int avr_dec_plan_arena(const avr_dec_plan* plan, uint8_t* out, size_t cap);
+int avr_dec_plan_splice(const avr_dec_plan* plan, const int32_t* status, const uint8_t* regen, size_t regen_len,
+                        const uint64_t* offsets, const uint32_t* lens, uint8_t* out, size_t out_cap, size_t* out_len);
+
 /* Container codec check (host only): parse a Recoded protobuf (recode.proto:1-19) with the
  * library's own wire codec -- the one avr_decompress_file uses -- and return (a) its fields as JSON,
  * {"version": null | hex, "blocks": [{"size": int, "literal": hex, "skip_coded": bool, "cabac": hex,

@@ -6,7 +6,8 @@ this box's one GPU, and RCCL will not put two ranks on one device):
 * the default mode: every rank's weak-scaling batch (headline), the max-over-ranks reduction, the
   corpus dealt over the ranks (corpus_sharded);
 * --stream-shard (BASELINE configs[3]): the stream cut over the ranks, the gather to rank 0 and its
-  container assembly.
+  container assembly, rank 0's plan of that container scattered over the ranks, every rank's
+  decompress, the gather of the regenerated slices and rank 0's splice into the stream.
 Each run must print one JSON line with n_gpus 2 and bit_exact true.
 """
 import json
@@ -50,4 +51,6 @@ def test_bench_stream_shard_two_ranks():
                            "--warmup", "1"])
     assert line["n_gpus"] == 2 and line["bit_exact"] is True
     assert line["scaling"] == "strong" and line["config"]["slices"] == 30
-    assert set(line["config"]["step_phases_s_rank0"]) == {"kernels_s", "results_d2h_s", "gather_s", "assemble_s"}
+    assert set(line["config"]["step_phases_s_rank0"]) == {
+        "compress_s", "results_d2h_s", "gather_s", "assemble_s", "plan_s", "scatter_h2d_s", "decompress_s",
+        "gather_d_s", "splice_s"}
