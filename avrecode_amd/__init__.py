@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "avr_create", "avr_destroy", "avr_last_error", "avr_free", "avr_compress_file", "avr_decompress_file",
     "avr_roundtrip_file", "avr_compress_slices", "avr_decompress_slices", "avr_pack_outputs",
     "avr_roundtrip_slices", "avr_derive_decompress_descs", "avr_verify_slices", "avr_parse_stream",
-    "avr_assemble_container", "avr_assemble_container_parsed", "avr_assemble_container_into", "avr_dec_plan_new", "avr_dec_plan_free", "avr_dec_plan_load", "avr_dec_plan_descs", "avr_dec_plan_arena", "avr_dec_plan_splice", "avr_container_model", "avr_synthesize_stream",
+    "avr_assemble_container", "avr_assemble_container_parsed", "avr_assemble_container_into", "avr_parse_stream_range", "avr_slice_payload_sizes", "avr_dec_plan_new", "avr_dec_plan_free", "avr_dec_plan_load", "avr_dec_plan_descs", "avr_dec_plan_arena", "avr_dec_plan_splice", "avr_container_model", "avr_synthesize_stream",
     "avr_container_describe", "avr_compress_files", "avr_decompress_files",
     "avr_hooks_compress_begin", "avr_hooks_compress_stream_begin", "avr_hooks_feed",
     "avr_hooks_decompress_begin", "avr_hook_init_decoder", "avr_hook_get",
@@ -176,6 +176,8 @@ def lib() -> ctypes.CDLL:
     L.avr_verify_slices.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
     L.avr_pack_outputs.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
     L.avr_parse_stream.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
+    L.avr_parse_stream_range.argtypes = [vp, sz, i32, i32, pp, pi, pp, psz, psz, pi, pi]
+    L.avr_slice_payload_sizes.argtypes = [vp, sz, pp, pi]
     L.avr_assemble_container.argtypes = [vp, sz, i32, i32, vp, vp, sz, vp, vp, pp, psz]
     L.avr_assemble_container_parsed.argtypes = [vp, sz, i32, vp, i32, vp, sz, vp, vp, sz, vp, vp, pp, psz]
     L.avr_assemble_container_into.argtypes = [vp, sz, i32, vp, i32, vp, sz, vp, vp, sz, vp, vp, vp, sz, psz]
@@ -267,21 +269,38 @@ class ParsedStream:
         return int(self.descs["payload_size"].sum())
 
 
-def parse_stream(data) -> ParsedStream:
-    """Host-side slice extraction (avr_parse_stream).  Needs no GPU."""
+def parse_stream(data, lo: int = 0, hi: "int | None" = None) -> ParsedStream:
+    """Host-side slice extraction (avr_parse_stream; with a slice range [lo, hi),
+    avr_parse_stream_range: that range only, rebased as shard.subset would).  Needs no GPU."""
     L = lib()
     p, n, keep = _buf(data)
     descs, arena = ctypes.c_void_p(), ctypes.c_void_p()
     ns, mw, mh = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     alen, wlen = ctypes.c_size_t(), ctypes.c_size_t()
-    r = L.avr_parse_stream(p, n, ctypes.byref(descs), ctypes.byref(ns), ctypes.byref(arena), ctypes.byref(alen),
-                           ctypes.byref(wlen), ctypes.byref(mw), ctypes.byref(mh))
+    if lo == 0 and hi is None:
+        r = L.avr_parse_stream(p, n, ctypes.byref(descs), ctypes.byref(ns), ctypes.byref(arena), ctypes.byref(alen),
+                               ctypes.byref(wlen), ctypes.byref(mw), ctypes.byref(mh))
+    else:
+        r = L.avr_parse_stream_range(p, n, int(lo), -1 if hi is None else int(hi), ctypes.byref(descs),
+                                     ctypes.byref(ns), ctypes.byref(arena), ctypes.byref(alen), ctypes.byref(wlen),
+                                     ctypes.byref(mw), ctypes.byref(mh))
     del keep
     if r != AVR_OK:
         raise AvrError(r, "avr_parse_stream failed")
     d = _take_array(descs, ns.value * SLICE_DESC.itemsize).view(SLICE_DESC)
     a = _take_array(arena, alen.value)
     return ParsedStream(d, a, int(wlen.value), int(mw.value), int(mh.value))
+
+
+def slice_payload_sizes(data) -> np.ndarray:
+    """Every CABAC slice's payload_size (avr_slice_payload_sizes): a sharded run's partition input,
+    without copying the payloads.  Host only."""
+    p, n, keep = _buf(data)
+    out, ns = ctypes.c_void_p(), ctypes.c_int()
+    r = lib().avr_slice_payload_sizes(p, n, ctypes.byref(out), ctypes.byref(ns))
+    if r != AVR_OK:
+        raise AvrError(r, "avr_slice_payload_sizes failed")
+    return _take_array(out, 4 * ns.value).view(np.uint32)
 
 
 def plan_decompress(avrc) -> ParsedStream:

@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -1810,7 +1811,17 @@ int avr_roundtrip_files(avr_ctx* c, int n_files, const uint8_t* const* in, const
     return AVR_ERR_INVALID_ARGUMENT;
   for (int f = 0; f < n_files; f++)
     if (!in[f]) return AVR_ERR_INVALID_ARGUMENT;
-  return guarded(c, [&] { return roundtrip_files(c, n_files, in, in_len, model, out, out_len, status, times); });
+  const int r = guarded(c, [&] { return roundtrip_files(c, n_files, in, in_len, model, out, out_len, status, times); });
+  if (r != AVR_OK) {
+    // a batch that failed as a whole leaves no partial outputs: every file gets the error
+    for (int f = 0; f < n_files; f++) {
+      free(out[f]);
+      out[f] = nullptr;
+      out_len[f] = 0;
+      status[f] = r;
+    }
+  }
+  return r;
 }
 
 static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int max_w, int max_h,
@@ -1876,24 +1887,26 @@ int avr_verify_slices(avr_ctx* c, const avr_slice_desc* d_desc, const avr_slice_
   return AVR_OK;
 }
 
-int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
-                     size_t* arena_len, size_t* work_len, int* max_w, int* max_h) {
-  if (!file || !descs || !n_slices || !arena || !arena_len || !work_len || !max_w || !max_h)
+int avr_parse_stream_range(const uint8_t* file, size_t n, int lo, int hi, avr_slice_desc** descs, int* n_slices,
+                           uint8_t** arena, size_t* arena_len, size_t* work_len, int* max_w, int* max_h) {
+  if (!file || !descs || !n_slices || !arena || !arena_len || !work_len || !max_w || !max_h || lo < 0)
     return AVR_ERR_INVALID_ARGUMENT;
   *descs = nullptr;
   *arena = nullptr;
   return guarded(nullptr, [&]() -> int {
     ParsedFile pf;
     if (int r = parse_file(nullptr, file, n, &pf, /*views=*/true)) return r;
+    const int total = (int)pf.slices.size();
+    const int b = std::min(lo, total), e = hi < 0 ? total : std::max(b, std::min(hi, total));
     // the arena's layout first (append_aligned's: 16-byte aligned payloads, each followed by >= 16
-    // zero bytes), then one zeroed allocation and the payload copies on host threads
-    const size_t ns = pf.slices.size();
+    // zero bytes), then one allocation and the payload copies on host threads
+    const size_t ns = (size_t)(e - b);
     std::vector<avr_slice_desc> dv(ns);
     std::vector<avr::PbCopy> copies(ns);
     uint64_t work = 0, at = 0;
     int mw = 1, mh = 1;
     for (size_t i = 0; i < ns; i++) {
-      const avr::SliceInfo& s = pf.slices[i];
+      const avr::SliceInfo& s = pf.slices[b + i];
       avr_slice_desc& d = dv[i];
       d = desc_from_header(s);
       d.payload_offset = (at + 15) & ~(uint64_t)15;
@@ -1934,6 +1947,25 @@ int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int*
     *work_len = work;
     *max_w = mw;
     *max_h = mh;
+    return AVR_OK;
+  });
+}
+
+int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
+                     size_t* arena_len, size_t* work_len, int* max_w, int* max_h) {
+  return avr_parse_stream_range(file, n, 0, -1, descs, n_slices, arena, arena_len, work_len, max_w, max_h);
+}
+
+int avr_slice_payload_sizes(const uint8_t* file, size_t n, uint32_t** sizes, int* n_slices) {
+  if (!file || !sizes || !n_slices) return AVR_ERR_INVALID_ARGUMENT;
+  *sizes = nullptr;
+  return guarded(nullptr, [&]() -> int {
+    ParsedFile pf;
+    if (int r = parse_file(nullptr, file, n, &pf, /*views=*/true)) return r;
+    *sizes = (uint32_t*)malloc(sizeof(uint32_t) * std::max<size_t>(1, pf.slices.size()));
+    if (!*sizes) return AVR_ERR_OUT_OF_MEMORY;
+    for (size_t i = 0; i < pf.slices.size(); i++) (*sizes)[i] = (uint32_t)pf.slices[i].size;
+    *n_slices = (int)pf.slices.size();
     return AVR_OK;
   });
 }
@@ -2567,13 +2599,20 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
                                const uint8_t** stream, size_t* stream_len) {
   if (!c || !avrc || !out) return AVR_ERR_INVALID_ARGUMENT;
   *out = nullptr;
-  std::unique_ptr<avr_hooks_session> hs(new avr_hooks_session);
+  std::unique_ptr<avr_hooks_session> hs(new (std::nothrow) avr_hooks_session);
+  if (!hs) return fail(c, AVR_ERR_OUT_OF_MEMORY, "host allocation failed");
   hs->c = c;
   hs->decompress = true;
   {
-    std::vector<avr::PbBlock> probe;
-    std::string version;
-    const int m = avr::pb_parse(avrc, n, &probe, &version) ? avr::model_of_version(version) : 0;
+    // the container's model from its Metadata.version alone (no block list), inside guarded(): no
+    // exception crosses the C ABI
+    int m = 0;
+    if (int r = guarded(c, [&]() -> int {
+          std::string version;
+          m = avr::pb_read_version(avrc, n, &version) ? avr::model_of_version(version) : 0;
+          return AVR_OK;
+        }))
+      return r;
     if (parallel_model(m) && !getenv("AVR_HOOKS_EAGER")) {
       // the parallel model's slices are independent: plan the container now, regenerate on demand
       if (int r = guarded(c, [&]() -> int {

@@ -695,6 +695,34 @@ void pb_put_metadata_version(std::vector<uint8_t>* o, const std::string& version
   bytes_field(o, 1, m.data(), m.size());
 }
 
+bool pb_read_version(const uint8_t* in, size_t n, std::string* version) {
+  version->clear();
+  const uint8_t *p = in, *e = in + n;
+  while (p < e) {
+    uint64_t tag, len;
+    if (!rd_varint(&p, e, &tag)) return false;
+    if ((tag & 7) != 2 || (tag >> 3) != 1) {
+      if (!skip_field(&p, e, (int)(tag & 7))) return false;
+      continue;
+    }
+    if (!rd_varint(&p, e, &len) || (uint64_t)(e - p) < len) return false;
+    const uint8_t *q = p, *qe = p + len;
+    p += len;
+    while (q < qe) {
+      uint64_t t2, l2;
+      if (!rd_varint(&q, qe, &t2)) return false;
+      if ((t2 & 7) != 2) {
+        if (!skip_field(&q, qe, (int)(t2 & 7))) return false;
+        continue;
+      }
+      if (!rd_varint(&q, qe, &l2) || (uint64_t)(qe - q) < l2) return false;
+      if ((t2 >> 3) == 1) version->assign((const char*)q, l2);
+      q += l2;
+    }
+  }
+  return true;
+}
+
 bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version, bool* has_metadata) {
   blocks->clear();
   version->clear();

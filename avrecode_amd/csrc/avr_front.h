@@ -115,6 +115,9 @@ size_t pb_write_block(uint8_t* o, size_t at, const PbBlock& b, std::vector<PbCop
 void pb_put_metadata_version(std::vector<uint8_t>* o, const std::string& version);
 bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::string* version,
               bool* has_metadata = nullptr);
+// Recoded.Metadata.version only (empty without Metadata); false for bytes that are not a Recoded
+// message at the top level.  No block list is built.
+bool pb_read_version(const uint8_t* in, size_t n, std::string* version);
 
 // Recoded.Metadata.version of the parallel model's containers (the reference model writes none, as
 // the reference does): its decisions through the reference's arithmetic_code<uint64_t, uint8_t>, or

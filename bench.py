@@ -405,12 +405,15 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     progress(f"rank {rank}: {len(data)} bytes; parsing")
     setup = {}
     t = time.perf_counter()
-    ps = avr.parse_stream(data)
+    # rank 0 parses the whole stream (its assembly reads every slice); the other ranks only the
+    # payload sizes (the partition) and then their own range
+    ps = avr.parse_stream(data) if rank == 0 else None
+    sizes = ps.descs["payload_size"] if rank == 0 else avr.slice_payload_sizes(data)
     setup["parse_s"] = time.perf_counter() - t
-    progress(f"rank {rank}: parsed {len(ps.descs)} slices in {setup['parse_s']:.1f} s")
+    progress(f"rank {rank}: parsed {len(sizes)} slices in {setup['parse_s']:.1f} s")
     t = time.perf_counter()
-    lo, hi = shard.partition(ps.descs["payload_size"], world)[rank]
-    part = shard.subset(ps, lo, hi)
+    lo, hi = shard.partition(sizes, world)[rank]
+    part = shard.subset(ps, lo, hi) if rank == 0 else avr.parse_stream(data, lo, hi)
     setup["subset_s"] = time.perf_counter() - t
     t = time.perf_counter()
     batch = DeviceBatch(ctx, part)

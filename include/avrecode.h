@@ -238,6 +238,15 @@ int avr_verify_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, const avr_slic
  * take (unsupported syntax, or shorter than a surrogate marker, recode.cpp:1285). */
 int avr_parse_stream(const uint8_t* file, size_t n, avr_slice_desc** descs, int* n_slices, uint8_t** arena,
                      size_t* arena_len, size_t* work_len, int* max_mb_width, int* max_mb_height);
+/* avr_parse_stream for the slices [lo, hi) only (hi < 0: to the end), descs and arena rebased to
+ * them: a rank of a sharded compress takes its own range of a stream without copying the rest
+ * (the whole stream's headers are still parsed: slice indices and picture ids are the file's). */
+int avr_parse_stream_range(const uint8_t* file, size_t n, int lo, int hi, avr_slice_desc** descs, int* n_slices,
+                           uint8_t** arena, size_t* arena_len, size_t* work_len, int* max_mb_width,
+                           int* max_mb_height);
+/* The payload_size of every CABAC slice of a file (what avr_parse_stream reports), without copying a
+ * payload: the input of a sharded run's partition on every rank.  *sizes malloc'd (avr_free). */
+int avr_slice_payload_sizes(const uint8_t* file, size_t n, uint32_t** sizes, int* n_slices);
 
 /* Rank 0 of a sharded PARALLEL-model compress: build the Recoded container from per-slice outputs
  * gathered from every rank (compressor::run + find_next_coded_block_and_emit_literal,

@@ -157,8 +157,10 @@ def _gloo_worker(rank, world, port, name, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["realshort.mp4", "cockatoo.mp4"])
-def test_gloo_world2_sharded_assembly(name):
+@pytest.mark.parametrize("name,world", [("realshort.mp4", 2), ("cockatoo.mp4", 2), ("realshort.mp4", 8)])
+def test_gloo_world2_sharded_assembly(name, world):
+    """The gather's message sequence (size all_gather, then per rank one metadata and one byte
+    send/recv in rank order) at world 2 and at the node's 8 ranks."""
     import socket
 
     import torch.multiprocessing as mp
@@ -166,7 +168,7 @@ def test_gloo_world2_sharded_assembly(name):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(_gloo_worker, args=(2, port, name, td), nprocs=2, join=True)
+        mp.spawn(_gloo_worker, args=(world, port, name, td), nprocs=world, join=True)
         c = open(os.path.join(td, "out.avrc"), "rb").read()
     assert hashlib.sha256(c).hexdigest() == GOLD[(name, "P")]["avrc_sha256"]
 
@@ -261,7 +263,7 @@ def _gloo_decompress_worker(rank, world, port, name, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_sharded_decompress_reassembles(world):
     import socket
 

@@ -135,6 +135,9 @@ def test_segmentation_equals_reference_search():
 
 
 def test_assembly_scales_linearly():
+    """A 4x longer stream (the same slices, with their filler NAL units, tiled four times) takes
+    about 4x the time: no per-slice search that grows with the file.  Best of three runs each, with
+    slack for timer and scheduler noise on a shared host."""
     def best_time(data, ps):
         t = []
         for _ in range(3):
@@ -142,11 +145,13 @@ def test_assembly_scales_linearly():
             _assemble(data, ps, parsed=True)
             t.append(time.perf_counter() - t0)
         return min(t)
-    small = _stream(300, seed=2)
-    # the same slices tiled four times (a long stream of one repeated GOP, as configs[3] is made)
-    head, sl = _nals(small)
-    big = head + b"".join(sl) * 4
-    ps_s, ps_b = avr.parse_stream(small), avr.parse_stream(big)
+    small = _stream(900, seed=2)
+    # the parameter sets once, then everything after them (slices and filler NAL units in their
+    # order) four times: a long stream of one repeated GOP, as configs[3] is made
+    ps_s = avr.parse_stream(small)
+    body_at = small.index(b"\x00\x00\x00\x01", small.index(b"\x00\x00\x00\x01\x68") + 4)
+    big = small[:body_at] + small[body_at:] * 4
+    ps_b = avr.parse_stream(big)
     assert len(ps_b.descs) == 4 * len(ps_s.descs)
     ts, tb = best_time(small, ps_s), best_time(big, ps_b)
-    assert tb <= 4.5 * ts + 0.02, (ts, tb)
+    assert tb <= 6 * ts + 0.05, (ts, tb)

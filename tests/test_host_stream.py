@@ -126,7 +126,7 @@ def _scatter_worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_scatter_parsed(world):
     import socket
 
@@ -203,3 +203,20 @@ def test_assembly_rate_at_stream_scale():
     print(f"assembly: {len(data) / 1e9:.2f} GB in {dt:.3f} s = {rate:.2f} GB/s")
     assert len(c) > len(data) * 0.98
     assert rate > 0.3
+
+
+@pytest.mark.parametrize("name", ["realshort.mp4", "cockatoo.mp4", "paff_ipp.264"])
+def test_parse_range_equals_subset(name):
+    """A rank's own range of a stream (avr_parse_stream_range) is shard.subset of the whole parse,
+    and avr_slice_payload_sizes the whole parse's payload sizes: the other ranks of a sharded run
+    need neither the whole arena nor a copy of every payload."""
+    data = (FIX / name).read_bytes()
+    ps = avr.parse_stream(data)
+    n = len(ps.descs)
+    assert (avr.slice_payload_sizes(data) == ps.descs["payload_size"]).all()
+    for lo, hi in ((0, n), (0, n // 2), (n // 3, n), (n // 2, n // 2), (1, 2)):
+        a, b = avr.parse_stream(data, lo, hi), shard.subset(ps, lo, hi)
+        assert a.descs.tobytes() == b.descs.tobytes(), (lo, hi)
+        if hi > lo:
+            assert a.arena.tobytes()[:len(b.arena)] == b.arena.tobytes()
+        assert a.work_len == b.work_len
