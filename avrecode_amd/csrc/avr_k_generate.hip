@@ -5,12 +5,12 @@ namespace avr {
 
 hipError_t launch_parallel_generate(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds, const uint8_t* in,
                     uint8_t* out, avr_slice_result* res, uint16_t* est, const int* order, uint32_t flags, hipStream_t stream) {
-  hipLaunchKernelGGL((slices_parallel_kernel<MODE_GENERATE, false>), dim3(n), dim3(slice_threads<MODE_GENERATE>()), lds, stream, T, descs, n, in, out, res, est, order, nullptr, flags);
+  hipLaunchKernelGGL((slices_parallel_kernel<MODE_GENERATE, false>), dim3(n), dim3(slice_threads<MODE_GENERATE>()), lds, stream, T, descs, n, in, out, res, est, order, flags);
   // field pictures / MBAFF frames: a second launch over the batch (its workgroups for progressive
   // slices return at once)
   if (flags & kFlagFields) {
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-    hipLaunchKernelGGL((slices_parallel_kernel<MODE_GENERATE, true>), dim3(n), dim3(slice_threads<MODE_GENERATE>()), lds, stream, T, descs, n, in, out, res, est, order, nullptr, flags);
+    hipLaunchKernelGGL((slices_parallel_kernel<MODE_GENERATE, true>), dim3(n), dim3(slice_threads<MODE_GENERATE>()), lds, stream, T, descs, n, in, out, res, est, order, flags);
   }
   return hipGetLastError();
 }

@@ -18,7 +18,11 @@ constexpr int kEstLogN = kEstTable;
 constexpr int kEstLog = kEstTable + 2;
 constexpr int kEstLogCap = 8191;
 constexpr uint32_t kEstLogOverflow = 0xffffffffu;
-constexpr int kEstGlobal = kEstLog + 2 * kEstLogCap;
+// then, for the progressive parallel kernels of wide launches (kFlagMringGlobal), the upper row's
+// model bytes (Walker::mring: 52 B per macroblock column, up to kMringCols columns)
+constexpr int kEstMring = kEstLog + 2 * kEstLogCap;
+constexpr int kMringCols = 288;
+constexpr int kEstGlobal = kEstMring + kMringCols * 26;
 static_assert(kEstGlobal % 8 == 0 && kEstTable % 8 == 0, "16-byte clears");
 
 constexpr uint32_t kFlagBill = 1;   // launch flag: the coders bill per CodingType (avr_slice_result.bill)
@@ -31,7 +35,16 @@ constexpr uint32_t kFlagFields = 2;
 // launch flag: parallel model with the P32 container coder (avr_k_*32.hip) instead of the reference's
 // arithmetic_code<uint64_t, uint8_t>
 constexpr uint32_t kFlagP32 = 4;
+// launch flag (set by launch_slices): the progressive parallel kernels keep the upper row's model
+// bytes in global scratch instead of LDS, so that four workgroups of a wide picture fit a CU
+constexpr uint32_t kFlagMringGlobal = 8;
+// LDS of one slice workgroup: the field / reference-model walkers' layout (full EdgeRecs), and the
+// progressive parallel kernels' (EdgeCore ring, plus the model row in LDS unless mring_global)
 size_t shared_bytes(int max_mb_width);
+size_t shared_bytes_progressive(int max_mb_width, bool mring_global);
+// the progressive parallel kernels of a launch of this width keep the model row in global memory:
+// it fits one more workgroup per CU (and the row fits the scratch)
+bool mring_global_for(int max_mb_width);
 // does workgroup b of a 4G-workgroup launch land on CU group b mod G (schedule_kernel's assumption)?
 hipError_t probe_round_robin(size_t lds, bool* ok);
 // mode: 0 compress, 1 decompress, 2 generate, 3 trace (decode-only bin trace).  sequential = reference model (single wavefront).
@@ -60,19 +73,23 @@ int est_slots(int n, int max_mb_width);
 hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                     const int* order, uint32_t flags, hipStream_t stream,
-                                    uint32_t* qhead = nullptr, int qgrid = 0);
+                                    uint32_t* qhead = nullptr, int qgrid = 0, int qgrid_fld = 0,
+                                    size_t lds_fld = 0);
 hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                       const int* order, uint32_t flags, hipStream_t stream,
-                                    uint32_t* qhead = nullptr, int qgrid = 0);
+                                    uint32_t* qhead = nullptr, int qgrid = 0, int qgrid_fld = 0,
+                                    size_t lds_fld = 0);
 hipError_t launch_parallel_compress32(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                       const int* order, uint32_t flags, hipStream_t stream,
-                                    uint32_t* qhead = nullptr, int qgrid = 0);
+                                    uint32_t* qhead = nullptr, int qgrid = 0, int qgrid_fld = 0,
+                                    size_t lds_fld = 0);
 hipError_t launch_parallel_decompress32(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                         const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                         const int* order, uint32_t flags, hipStream_t stream,
-                                    uint32_t* qhead = nullptr, int qgrid = 0);
+                                    uint32_t* qhead = nullptr, int qgrid = 0, int qgrid_fld = 0,
+                                    size_t lds_fld = 0);
 hipError_t launch_parallel_generate(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                     const int* order, uint32_t flags, hipStream_t stream);

@@ -123,6 +123,21 @@ struct EdgeRec {
   uint8_t mnnz[52];
 };
 static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
+// The progressive walkers' ring holds EdgeRec's first ten dwords only (the parse's neighbour
+// fields); the 52 model bytes of each column (EdgeRec::mnnz, read by the NZ-tree keys of the
+// parallel model) live in a row of their own, `mring` (13 dwords per column): in LDS after the
+// ring, or -- when that is what lets four wide workgroups share a CU's LDS (4K: 240 columns x 92 B
+// would leave room for three) -- in the workgroup's global scratch (kFlagMringGlobal).
+struct EdgeCore {
+  uint8_t flags, pad;
+  uint16_t cbp;
+  uint8_t nnz[3][4];
+  uint8_t mvd[2][4][2];
+  int8_t ref[2][2];
+  uint8_t direct8[2], pad2[2];
+};
+static_assert(sizeof(EdgeCore) == 40 && offsetof(EdgeRec, mnnz) == 40, "EdgeCore = EdgeRec's first ten dwords");
+constexpr int kMringDwords = 13;   // per column: EdgeRec::mnnz
 static_assert(sizeof(MbRec) == 180, "MbRec layout (dword map in Walker::edge_src)");
 
 // LDS layout (per workgroup = one slice); the ring is sized by mb_width at launch.
@@ -158,6 +173,7 @@ struct Shared {
   uint32_t elog_n;           // entries appended to the HBM table's write log by this model
   uint32_t prio;             // the slice's current wave priority (walker -> modeler / coder)
   uint32_t qnext;            // persistent launches: the queue entry this workgroup drew
+  uint32_t qcell;            //   and its walker wave's cell on the CU board
   uint32_t c_len, c_last;
   uint32_t bill[6];          // the coder's h264_model billing by CodingType (kFlagBill launches)
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
@@ -536,7 +552,12 @@ struct Walker {
   const EngineTables* G;  // global (init-only tables)
   const avr_slice_desc* d;
   Shared* sh;
-  EdgeRec* ring;
+  // the upper row's edge records: full EdgeRecs for the field walkers (their MBAFF views and pair
+  // records), EdgeCore plus the separate model row (mring) for the progressive ones
+  typedef typename std::conditional<FLD, EdgeRec, EdgeCore>::type ERec;
+  ERec* ring;
+  uint32_t* mring;        // progressive, parallel model: 13 dwords per column (LDS or global)
+  bool mring_global;
   uint16_t* est_g;        // SIG + NZ estimators (global)
   uint8_t* frames;        // RM: 2 frames of W*H*52 model bytes
   int64_t cur_off, prev_off;   // RM: byte offsets of the current / previous frame's model bytes (prev < 0: zeros)
@@ -926,7 +947,7 @@ struct Walker {
   int avr_limit;
 
   // ------------------------------------------------------------------ neighbours (parser)
-  AVR_FI const EdgeRec& top() const { return ring[mb_x]; }
+  AVR_FI const ERec& top() const { return ring[mb_x]; }
   AVR_FI uint16_t nb_cbp_left() const {
     return left_ok ? (lf >> 16) : ((cf & F_INTRA) ? 0x7CF : 0x00F);
   }
@@ -970,7 +991,7 @@ struct Walker {
   // the dword 0 of the left pair's top / bottom and of the upper pair's top / bottom edges.
   static constexpr uint32_t F_FLD = 0x100;   // cf: field macroblock
   static constexpr uint32_t PST_FLD = 1, PST_SKIPT = 2, PST_SKIPB = 4, PST_BOT = 8;
-  AVR_FI EdgeRec* pair_edge(int bot) const { return ring + (1 + bot) * W; }
+  AVR_FI ERec* pair_edge(int bot) const { return ring + (1 + bot) * W; }
   AVR_FI MbRec* pair_rec() const { return (MbRec*)(ring + 3 * W); }
   AVR_FI uint32_t* pair_nb() const { return (uint32_t*)(pair_rec() + 3); }
   AVR_FI uint32_t lds_u32(const uint32_t* p) const { return __builtin_amdgcn_readfirstlane(*p); }
@@ -1156,7 +1177,14 @@ struct Walker {
     if (RM) return (FLD && top_pending) ? 0 : frames[cur_off + ((int64_t)(mrow() - 1) * W + mb_x) * 52 + idx];
     // fresh model per slice: in a field picture the model's upper row belongs to the other field
     if (FLD && fld_pic) return 0;
-    return (top_ok | (FLD && mbaff)) ? ring[mb_x].mnnz[idx] : 0;   // MBAFF: the view holds the model's upper macroblock
+    if constexpr (FLD) {
+      return (top_ok | mbaff) ? ring[mb_x].mnnz[idx] : 0;   // MBAFF: the view holds the model's upper macroblock
+    } else {
+      if (!top_ok) return 0;
+      const uint32_t at = (uint32_t)mb_x * (kMringDwords * 4) + (uint32_t)idx;
+      if (mring_global) return ((const __attribute__((address_space(1))) uint8_t*)mring)[at];
+      return ((const __attribute__((address_space(3))) uint8_t*)mring)[at];
+    }
   }
   AVR_FI int mnnz_prev(int idx) const {
     if (RM) return prev_off < 0 ? 0 : frames[prev_off + ((int64_t)mrow() * W + mb_x) * 52 + idx];
@@ -2002,9 +2030,11 @@ AVR_FI void init_slice_state(Walker<MODE, RM, FLD, P32>& w, const EngineTables* 
       for (int i = lane; i < kEtabSize + 64; i += nt) w.sh->etab[i] = 0;
   }
   uint32_t* ring32 = (uint32_t*)w.ring;
-  // MBAFF: the pair edges and records too (walk_slice refuses the slice when they do not fit)
+  // MBAFF: the pair edges and records too (walk_slice refuses the slice when they do not fit).  The
+  // progressive model row needs no clear: a column's model bytes are read only under a decoded
+  // upper macroblock of this slice (top_ok), which wrote them.
   const int cols = (FLD && d->structure == AVR_STRUCT_MBAFF && (int)w.ring_cols >= 3 * w.W + 7) ? 3 * w.W + 7 : w.W;
-  for (int i = lane; i < cols * (int)sizeof(EdgeRec) / 4; i += nt) ring32[i] = 0;
+  for (int i = lane; i < cols * (int)sizeof(typename Walker<MODE, RM, FLD, P32>::ERec) / 4; i += nt) ring32[i] = 0;
   if (lane < 2) {
     w.sh->fifo_head[lane] = 0;
     w.sh->fifo_tail[lane] = 0;
@@ -2100,7 +2130,16 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
         uint32_t* l32 = (uint32_t*)&w.sh->left;
         if (lane < 45) l32[lane] = v;
         uint32_t* e32 = (uint32_t*)&w.ring[w.mb_x];
-        if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
+        if constexpr (FLD) {
+          if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
+        } else {
+          if (lane < 10) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
+          else if (!RM && lane < 10 + kMringDwords) {   // the model row (RM reads the frame instead)
+            const uint32_t at = (uint32_t)w.mb_x * kMringDwords + (lane - 10);
+            if (w.mring_global) ((__attribute__((address_space(1))) uint32_t*)w.mring)[at] = ev;
+            else ((__attribute__((address_space(3))) uint32_t*)w.mring)[at] = ev;
+          }
+        }
         w.lf = w.cf;
       } else {   // the pair edge of this macroblock; the pair's records move left after its bottom
         const int bot = (w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT) != 0;
@@ -2721,7 +2760,10 @@ AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice
   const avr_slice_desc* d = &descs[s];
   Walker<MODE, false, FLD, P32> w;
   w.sh = (Shared*)smem;
-  w.ring = (EdgeRec*)(smem + sizeof(Shared));
+  w.ring = (typename Walker<MODE, false, FLD, P32>::ERec*)(smem + sizeof(Shared));
+  w.mring_global = !FLD && (flags & kFlagMringGlobal);
+  w.mring = w.mring_global ? (uint32_t*)(est_g + kEstMring)
+                           : (uint32_t*)(smem + sizeof(Shared) + (size_t)(flags >> kFlagRingShift) * sizeof(EdgeCore));
   w.prio_cell = cell;
   w.T = &w.sh->tab;
   w.G = G;
@@ -2783,35 +2825,41 @@ template <int MODE, bool FLD, bool P32 = false>
 __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                                 const uint8_t* in, uint8_t* out, avr_slice_result* res,
                                                                 uint16_t* est_scratch, const int* order,
-                                                                uint32_t* qhead, uint32_t flags) {
+                                                                uint32_t flags) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  if ((int)blockIdx.x >= n) return;
+  const int s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
+  if ((descs[s].structure != AVR_STRUCT_FRAME) != FLD) return;
+  load_hot_tables((Shared*)smem, G);
+  parallel_slice<MODE, FLD, P32>(smem, G, descs, s, in, out, res, est_scratch + (size_t)s * kEstGlobal, flags, kNoCell);
+}
+
+// The persistent variant (a kernel of its own: the loop's state would change the resident
+// kernel's register allocation): about one workgroup per resident slot, each taking the next entry
+// of the largest-first queue by an atomic on *qhead until the queue is empty.
+template <int MODE, bool FLD, bool P32 = false>
+__global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+                                                             const uint8_t* in, uint8_t* out, avr_slice_result* res,
+                                                             uint16_t* est_scratch, const int* queue, uint32_t* qhead,
+                                                             uint32_t flags) {
   extern __shared__ __align__(16) uint8_t smem[];
   Shared* sh = (Shared*)smem;
-  // one call site of the slice body for both ways (the walker is inlined once per kernel)
-  uint16_t* est_g = est_scratch + (size_t)blockIdx.x * kEstGlobal;
-  uint32_t cell = kNoCell;   // the walker wave's cell on the CU board, for every slice of a persistent workgroup
-  bool loaded = false, done = false;
+  load_hot_tables(sh, G);
+  if ((MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x < 64) {
+    const uint32_t c = cu_cell();
+    if (__lane_id() == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->qcell = c;
+  }
   for (;;) {
-    int s;
-    if (qhead) {
-      if (threadIdx.x == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext = atomicAdd(qhead, 1u);
-      __syncthreads();
-      const uint32_t k = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext);
-      __syncthreads();   // every thread has its entry before thread 0 draws again
-      if (k >= (uint32_t)n) break;
-      s = order[k];
-    } else {
-      if (done || (int)blockIdx.x >= n) break;
-      done = true;
-      s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
-      est_g = est_scratch + (size_t)s * kEstGlobal;
-    }
+    if (threadIdx.x == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext = atomicAdd(qhead, 1u);
+    __syncthreads();
+    const uint32_t k = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext);
+    __syncthreads();   // every thread has its entry before thread 0 draws again
+    if (k >= (uint32_t)n) break;
+    const int s = queue[k];
     if ((descs[s].structure != AVR_STRUCT_FRAME) != FLD) continue;
-    if (!loaded) {
-      load_hot_tables(sh, G);
-      loaded = true;
-      if (qhead && (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x < 64) cell = cu_cell();
-    }
-    parallel_slice<MODE, FLD, P32>(smem, G, descs, s, in, out, res, est_g, flags, cell);
+    const uint32_t cell = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->qcell);
+    parallel_slice<MODE, FLD, P32>(smem, G, descs, s, in, out, res, est_scratch + (size_t)blockIdx.x * kEstGlobal,
+                                   flags, cell);
   }
 }
 
@@ -2824,21 +2872,30 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
 // q.head[1] for the field one (both zero on entry).
 struct QueueLaunch {
   uint32_t* head = nullptr;
-  int grid = 0;
+  int grid = 0, grid_fld = 0;   // persistent grids of the progressive and the field kernel
+  size_t lds_fld = 0;           // LDS of the field kernel (0: the progressive kernel's)
 };
 template <int MODE, bool P32>
 inline hipError_t launch_parallel(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                   const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                   const int* order, uint32_t flags, hipStream_t stream, QueueLaunch q = QueueLaunch()) {
-  const int grid = q.head ? q.grid : n;
+  const size_t lds_fld = q.lds_fld ? q.lds_fld : lds;
   if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
-  hipLaunchKernelGGL((slices_parallel_kernel<MODE, false, P32>), dim3(grid), dim3(slice_threads<MODE>()), lds, stream,
-                     T, descs, n, in, out, res, est, order, q.head, flags);
+  if (q.head)
+    hipLaunchKernelGGL((slices_queue_kernel<MODE, false, P32>), dim3(q.grid), dim3(slice_threads<MODE>()), lds, stream,
+                       T, descs, n, in, out, res, est, order, q.head, flags);
+  else
+    hipLaunchKernelGGL((slices_parallel_kernel<MODE, false, P32>), dim3(n), dim3(slice_threads<MODE>()), lds, stream,
+                       T, descs, n, in, out, res, est, order, flags);
   if (flags & kFlagFields) {
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
-    hipLaunchKernelGGL((slices_parallel_kernel<MODE, true, P32>), dim3(grid), dim3(slice_threads<MODE>()), lds, stream,
-                       T, descs, n, in, out, res, est, order, q.head ? q.head + 1 : nullptr, flags);
+    if (q.head)
+      hipLaunchKernelGGL((slices_queue_kernel<MODE, true, P32>), dim3(q.grid_fld), dim3(slice_threads<MODE>()), lds_fld,
+                         stream, T, descs, n, in, out, res, est, order, q.head + 1, flags & ~kFlagMringGlobal);
+    else
+      hipLaunchKernelGGL((slices_parallel_kernel<MODE, true, P32>), dim3(n), dim3(slice_threads<MODE>()), lds_fld,
+                         stream, T, descs, n, in, out, res, est, order, flags & ~kFlagMringGlobal);
   }
   return hipGetLastError();
 }
@@ -2867,7 +2924,9 @@ __global__ __launch_bounds__(192) void slices_sequential_kernel(const EngineTabl
   frame_meta += file;
   Walker<MODE, true, FLD> w;
   w.sh = (Shared*)smem;
-  w.ring = (EdgeRec*)(smem + sizeof(Shared));
+  w.ring = (typename Walker<MODE, true, FLD>::ERec*)(smem + sizeof(Shared));
+  w.mring = nullptr;   // the reference model reads its neighbours' model bytes from the frame
+  w.mring_global = false;
   load_hot_tables(w.sh, G);
   w.T = &w.sh->tab;
   w.G = G;
