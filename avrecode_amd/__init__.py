@@ -237,11 +237,13 @@ class _LibBuffer:
 
     def __init__(self, p: int, n: int):
         self._p = p
+        self._free = lib().avr_free   # held: at interpreter exit the module's globals may be gone
+        self._vp = ctypes.c_void_p
         self.__array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (p, False), "version": 3}
 
     def __del__(self):
         if self._p:
-            lib().avr_free(ctypes.c_void_p(self._p))
+            self._free(self._vp(self._p))
             self._p = 0
 
 

@@ -173,7 +173,6 @@ struct Shared {
   uint32_t elog_n;           // entries appended to the HBM table's write log by this model
   uint32_t prio;             // the slice's current wave priority (walker -> modeler / coder)
   uint32_t qnext;            // persistent launches: the queue entry this workgroup drew
-  uint32_t qcell;            //   and its walker wave's cell on the CU board
   uint32_t c_len, c_last;
   uint32_t bill[6];          // the coder's h264_model billing by CodingType (kFlagBill launches)
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
@@ -2844,11 +2843,12 @@ __global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables
                                                              uint32_t flags) {
   extern __shared__ __align__(16) uint8_t smem[];
   Shared* sh = (Shared*)smem;
-  load_hot_tables(sh, G);
-  if ((MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x < 64) {
-    const uint32_t c = cu_cell();
-    if (__lane_id() == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->qcell = c;
-  }
+  // the hot tables and the walker wave's CU-board cell are set up at the first slice this
+  // workgroup takes (a field-kernel workgroup that finds no field slice does neither).  Measured:
+  // setting them up before the first draw instead made the compress kernel hang on the GPU
+  // (r05c/r05e probes), this order does not (r05d).
+  uint32_t cell = kNoCell;
+  bool loaded = false;
   for (;;) {
     if (threadIdx.x == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext = atomicAdd(qhead, 1u);
     __syncthreads();
@@ -2857,7 +2857,11 @@ __global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables
     if (k >= (uint32_t)n) break;
     const int s = queue[k];
     if ((descs[s].structure != AVR_STRUCT_FRAME) != FLD) continue;
-    const uint32_t cell = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->qcell);
+    if (!loaded) {
+      load_hot_tables(sh, G);
+      loaded = true;
+      if ((MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x < 64) cell = cu_cell();
+    }
     parallel_slice<MODE, FLD, P32>(smem, G, descs, s, in, out, res, est_scratch + (size_t)blockIdx.x * kEstGlobal,
                                    flags, cell);
   }
