@@ -2753,14 +2753,16 @@ constexpr int slice_threads() {
 // One slice of a parallel launch on this workgroup (every thread): the hot tables are in LDS
 // already; est_g is the slice's estimator scratch; cell = the walker's CU-board cell (kNoCell:
 // register one).
-template <int MODE, bool FLD, bool P32>
+// MG: the launch may keep the model row in global scratch (the persistent kernel, which every wide
+// launch uses); the resident kernel's row is always in LDS (a constant: no branch at its accesses).
+template <int MODE, bool FLD, bool P32, bool MG>
 AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice_desc* descs, int s, const uint8_t* in,
                            uint8_t* out, avr_slice_result* res, uint16_t* est_g, uint32_t flags, uint32_t cell) {
   const avr_slice_desc* d = &descs[s];
   Walker<MODE, false, FLD, P32> w;
   w.sh = (Shared*)smem;
   w.ring = (typename Walker<MODE, false, FLD, P32>::ERec*)(smem + sizeof(Shared));
-  w.mring_global = !FLD && (flags & kFlagMringGlobal);
+  w.mring_global = MG && !FLD && (flags & kFlagMringGlobal);
   w.mring = w.mring_global ? (uint32_t*)(est_g + kEstMring)
                            : (uint32_t*)(smem + sizeof(Shared) + (size_t)(flags >> kFlagRingShift) * sizeof(EdgeCore));
   w.prio_cell = cell;
@@ -2830,7 +2832,8 @@ __global__ __launch_bounds__(192, 4) void slices_parallel_kernel(const EngineTab
   const int s = order ? order[blockIdx.x] : (int)blockIdx.x;   // CU grouping (schedule_kernel)
   if ((descs[s].structure != AVR_STRUCT_FRAME) != FLD) return;
   load_hot_tables((Shared*)smem, G);
-  parallel_slice<MODE, FLD, P32>(smem, G, descs, s, in, out, res, est_scratch + (size_t)s * kEstGlobal, flags, kNoCell);
+  parallel_slice<MODE, FLD, P32, false>(smem, G, descs, s, in, out, res, est_scratch + (size_t)s * kEstGlobal, flags,
+                                        kNoCell);
 }
 
 // The persistent variant (a kernel of its own: the loop's state would change the resident
@@ -2862,8 +2865,8 @@ __global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables
       loaded = true;
       if ((MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x < 64) cell = cu_cell();
     }
-    parallel_slice<MODE, FLD, P32>(smem, G, descs, s, in, out, res, est_scratch + (size_t)blockIdx.x * kEstGlobal,
-                                   flags, cell);
+    parallel_slice<MODE, FLD, P32, true>(smem, G, descs, s, in, out, res, est_scratch + (size_t)blockIdx.x * kEstGlobal,
+                                         flags, cell);
   }
 }
 
