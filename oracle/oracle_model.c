@@ -129,6 +129,40 @@ void avr_model_free(avr_model_t *m) {
   free(m);
 }
 
+/* Experiment hooks (a per-file prior for the parallel model's per-context
+ * estimators; measured by scripts/prior_experiment.py, not part of any format):
+ *   AVR_ORACLE_STATS=path  count every coded bin of a per-context key (kind < 1026, the
+ *                          model's default keys, recode.cpp:677-683) by context and value; the
+ *                          counts (u64[1026][2]) are written to path at exit
+ *   AVR_ORACLE_PRIOR=path  a new per-context estimator starts from path's (u16[1026][2]: pos,
+ *                          neg) instead of {1, 1} (recode.cpp:1057) */
+static uint64_t g_stats[1026][2];
+static int g_stats_on = -1;
+static uint16_t g_prior[1026][2];
+static int g_prior_on = -1;
+static void stats_write(void) {
+  const char *p = getenv("AVR_ORACLE_STATS");
+  FILE *f = p ? fopen(p, "wb") : NULL;
+  if (f) { fwrite(g_stats, sizeof(g_stats), 1, f); fclose(f); }
+}
+static int stats_on(void) {
+  if (g_stats_on < 0) {
+    g_stats_on = getenv("AVR_ORACLE_STATS") != NULL;
+    if (g_stats_on) atexit(stats_write);
+  }
+  return g_stats_on;
+}
+static int prior_on(void) {
+  if (g_prior_on < 0) {
+    const char *p = getenv("AVR_ORACLE_PRIOR");
+    FILE *f = p ? fopen(p, "rb") : NULL;
+    g_prior_on = f && fread(g_prior, sizeof(g_prior), 1, f) == 1;
+    if (f) fclose(f);
+  }
+  return g_prior_on;
+}
+static inline int default_kind(model_key_t key) { return (key & 0xffffffffffffull) == 0 && (key >> 48) < 1026; }
+
 static inline size_t hash_key(model_key_t k) {
   k ^= k >> 33;
   k *= 0xff51afd7ed558ccdull;
@@ -168,6 +202,10 @@ static estimator_t *estimator(avr_model_t *m, model_key_t key) {
   m->keys[j] = key;
   m->vals[j].pos = 1; /* struct estimator { int pos = 1, neg = 1; } (recode.cpp:1057) */
   m->vals[j].neg = 1;
+  if (prior_on() && default_kind(key) && g_prior[key >> 48][0]) {
+    m->vals[j].pos = g_prior[key >> 48][0];
+    m->vals[j].neg = g_prior[key >> 48][1];
+  }
   m->count++;
   return &m->vals[j];
 }
@@ -374,6 +412,7 @@ void model_update_key(avr_model_t *m, int symbol, model_key_t key) {
     if (symbol != (nnz == m->nonzeros_observed)) abort(); /* assert (1033) */
   }
   estimator_t *e = estimator(m, key);
+  if (stats_on() && default_kind(key)) g_stats[key >> 48][symbol != 0]++;
   if (symbol) e->pos++;
   else e->neg++;
   if ((m->coding_type != PIP_SIGNIFICANCE_MAP && e->pos + e->neg > 0x60) ||

@@ -39,11 +39,14 @@ def _run_two_ranks(extra):
 
 def test_bench_default_mode_two_ranks():
     line = _run_two_ranks(["--steps", "1", "--warmup", "1", "--slices", "8", "--mb-width", "40", "--mb-height", "24",
-                           "--corpus-scale", "0.05"])
+                           "--corpus-scale", "0.05", "--stream-leg-seconds", "1", "--stream-mb", "20", "12"])
     assert line["n_gpus"] == 2 and line["bit_exact"] is True
     assert line["scaling"] == "weak" and line["value"] > 0
     assert line["corpus"]["n_gpus"] == 2
     assert line["corpus"]["R"]["bit_exact"] is True and line["corpus"]["P"]["bit_exact"] is True
+    # the configs[3] leg sharded over both ranks inside the default run
+    st = line["stream_shard"]
+    assert st["n_gpus"] == 2 and st["bit_exact"] is True and st["config"]["slices"] == 30
 
 
 def test_bench_stream_shard_two_ranks():
