@@ -369,12 +369,49 @@ def rmode_files_section(ctx, args):
             break
     k = sorted(range(len(walls)), key=walls.__getitem__)[len(walls) // 2]
     progress(f"R-mode files: {total / walls[k] / 1e6:.2f} MB/s")
-    return {"files": len(files), "kinds": "workloads.mixed_files (configs[4] kinds, per-file seeds and lengths, "
-                                          "fixtures every 16th)",
-            "bytes": total, "file_bytes_min_median_max": [sizes[0], sizes[len(sizes) // 2], sizes[-1]],
-            "model": "reference (R)", "MB_s": total / walls[k] / 1e6, "wall_s": walls[k], "compress_s": tc[k],
-            "decompress_s": td[k], "avrc_bytes": sum(map(len, outs)), "bit_exact": True,
-            "phases": {"compress": _round_phases(phc[k]), "decompress": _round_phases(phd[k])}}
+    rec = {"files": len(files), "kinds": "workloads.mixed_files (configs[4] kinds, per-file seeds and lengths, "
+                                         "fixtures every 16th)",
+           "bytes": total, "file_bytes_min_median_max": [sizes[0], sizes[len(sizes) // 2], sizes[-1]],
+           "model": "reference (R)", "MB_s": total / walls[k] / 1e6, "wall_s": walls[k], "compress_s": tc[k],
+           "decompress_s": td[k], "avrc_bytes": sum(map(len, outs)), "bit_exact": True,
+           "phases": {"compress": _round_phases(phc[k]), "decompress": _round_phases(phd[k])}}
+    if not args.no_cpu_baseline:
+        rec["cpu_baseline"] = rmode_files_cpu(datas)
+    return rec
+
+
+def rmode_files_cpu(datas):
+    """The same files through the CPU oracle's R-mode roundtrip (`recode_oracle roundtrip`, the
+    reference's model on one thread per file, recode.cpp:122), one file per host thread, largest
+    first: the all-cores CPU figure beside the GPU's R-mode files throughput."""
+    import concurrent.futures as cf
+    import subprocess
+    import tempfile
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _oracle
+    _, cli = _oracle.build_oracle()
+    threads = cpu_threads()
+    with tempfile.TemporaryDirectory() as td:
+        paths = []
+        for i, d in enumerate(datas):
+            p = Path(td) / f"f{i}.bin"
+            p.write_bytes(d)
+            paths.append(p)
+        order = sorted(range(len(paths)), key=lambda i: -len(datas[i]))
+
+        def one(i):
+            r = subprocess.run([str(cli), "roundtrip", str(paths[i])], capture_output=True, timeout=900)
+            return r.returncode == 0
+
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+            ok = all(ex.map(one, order))
+        dt = time.perf_counter() - t0
+    total = sum(map(len, datas))
+    progress(f"R-mode files on {threads} host threads (oracle): {total / dt / 1e6:.2f} MB/s")
+    return {"value": total / dt / 1e6, "unit": "MB/s", "cores": threads, "kind": "port", "bit_exact": ok,
+            "sample": f"the same {len(datas)} files, oracle R-mode roundtrip (compress + decompress + compare), one "
+                      f"file per thread, largest first, {dt:.1f} s"}
 
 
 def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
