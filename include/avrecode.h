@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AVRECODE_ABI_VERSION 4
+#define AVRECODE_ABI_VERSION 5  /* 5: avr_slice_desc.file_offset (96 B), dec-plan handle, ranged parse */
 
 typedef enum {
   AVR_OK = 0,
