@@ -326,6 +326,31 @@ avr_slice_desc desc_from_header(const avr::SliceInfo& s) {
 
 constexpr int kRModeFallback = 1;
 
+// Does the parallel reference-model compress beat one workgroup per file on this plan?  Its time is
+// its largest slice's: the scan twice (count, write) and the recoded coder, one after the other;
+// the sequential kernel's is its largest file's, with walker, modeler and coder overlapped on three
+// waves.  Measured per payload byte of the chain (profiles/r05_rmode_files_trace.txt: a 4K 4:4:4
+// slice of 1.38 MB, scan 1.8 s per pass, coder ~1.5 s per MB; the sequential compress of its
+// 2-slice file 1.4 s per MB): the parallel pass pays when the largest file's payload exceeds ~3.7
+// times the largest slice's (cockatoo.mp4: 280 slices; a 1-2-slice-per-picture 4K file does not).
+// AVR_RMODE_PARALLEL=1 forces the parallel pass (tests), AVR_RMODE_SEQUENTIAL=1 the sequential kernel.
+bool rmode_parallel_pays(const Plan& plan) {
+  if (getenv("AVR_RMODE_PARALLEL")) return true;
+  const int nf = plan.n_files(), n = (int)plan.descs.size();
+  uint64_t max_slice = 0, max_file = 0;
+  for (int f = 0; f < nf; f++) {
+    const int e = f + 1 < nf ? plan.file_begin(f + 1) : n;
+    uint64_t fs = 0;
+    for (int k = plan.file_begin(f); k < e; k++) {
+      const uint64_t s = plan.descs[k].coded ? plan.descs[k].payload_size : 0;
+      fs += s;
+      max_slice = std::max(max_slice, s);
+    }
+    max_file = std::max(max_file, fs);
+  }
+  return max_file * 10 > max_slice * 37;
+}
+
 // Reference-model compress of a plan (file order) in parallel over slices (avr_k_rmode.hip).
 // Frame metadata generations mirror update_frame_spec (recode.cpp:824-843) as
 // slices_sequential_kernel implements it; a stream whose frame size changes with a stale other
@@ -399,7 +424,19 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
   std::vector<uint64_t> off(n + 1, 0);
   for (int k = 0; k < n; k++) off[k + 1] = off[k] + counts[k];
   const uint64_t N = off[n];
-  if (N >= (1ull << 30)) return kRModeFallback;
+  if (getenv("AVR_RMODE_STATS")) {
+    uint64_t pay = 0;
+    uint32_t mx = 0;
+    double mxr = 0;
+    for (int k = 0; k < n; k++) {
+      pay += plan.descs[k].payload_size;
+      mx = std::max(mx, counts[k]);
+      if (plan.descs[k].payload_size > 0) mxr = std::max(mxr, (double)counts[k] / plan.descs[k].payload_size);
+    }
+    fprintf(stderr, "rmode: %d slices, %llu ops, %llu payload bytes (%.2f ops/B, max slice %u ops, max %.1f ops/B)\n",
+            n, (unsigned long long)N, (unsigned long long)pay, pay ? (double)N / pay : 0.0, mx, mxr);
+  }
+  if (N >= (1ull << 31) - 1) return kRModeFallback;   // hipCUB's item count is an int
   HIP_TRY(c, hipMemcpyAsync(c->rm_off.p, off.data(), sizeof(uint64_t) * (n + 1), hipMemcpyHostToDevice, c->stream));
   std::vector<uint64_t> fop(nf + 1);
   for (int f = 0; f <= nf; f++) fop[f] = off[f < nf ? plan.file_begin(f) : n];
@@ -407,14 +444,15 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
   HIP_TRY(c, hipMemcpyAsync(c->file_op_off.p, fop.data(), sizeof(uint64_t) * (nf + 1), hipMemcpyHostToDevice,
                             c->stream));
   const size_t tb = avr::rmode_sort_temp_bytes(N, nf);
-  HIP_TRY(c, c->rm_ops.reserve(sizeof(uint32_t) * (N + 1) * 6 + tb + 256));
+  // ops, keys, skeys, rops: 4 B per op; vals, svals: 8 B (op index << 2 | flags)
+  HIP_TRY(c, c->rm_ops.reserve(sizeof(uint32_t) * (N + 1) * 8 + tb + 256));
   uint32_t* ops = c->rm_ops.as<uint32_t>();
   uint32_t* keys = ops + (N + 1);
-  uint32_t* vals = keys + (N + 1);
-  uint32_t* skeys = vals + (N + 1);
-  uint32_t* svals = skeys + (N + 1);
-  uint32_t* rops = svals + (N + 1);
-  void* temp = (void*)(((uintptr_t)(rops + (N + 1)) + 255) & ~(uintptr_t)255);
+  uint32_t* skeys = keys + (N + 1);
+  uint32_t* rops = skeys + (N + 1);
+  uint64_t* vals = (uint64_t*)(rops + (N + 1));
+  uint64_t* svals = vals + (N + 1);
+  void* temp = (void*)(((uintptr_t)(svals + (N + 1)) + 255) & ~(uintptr_t)255);
   // 2) write the ops, 3) estimator chains, 4) per-slice coder
   HIP_TRY(c, avr::launch_rscan(c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n, lds,
                                c->in.as<uint8_t>(), c->frames.as<uint8_t>(), c->rm_goff.as<int64_t>(),
@@ -470,7 +508,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
                             c->stream));
   HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   int rm = kRModeFallback;
-  if (sequential && mode == 0 && !getenv("AVR_RMODE_SEQUENTIAL")) {
+  if (sequential && mode == 0 && !getenv("AVR_RMODE_SEQUENTIAL") && rmode_parallel_pays(plan)) {
     rm = run_rmode_compress(c, plan, out_total, flags);
     if (rm < 0) return rm;
   }

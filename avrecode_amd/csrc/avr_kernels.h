@@ -114,7 +114,7 @@ hipError_t launch_rscan(const EngineTables* T, const avr_slice_desc* descs, int 
 size_t rmode_sort_temp_bytes(uint64_t N, int n_files);
 int rmode_max_files_per_pass();
 hipError_t launch_rmode_estimators(const uint32_t* ops, uint64_t N, const uint64_t* file_op_off, int n_files,
-                                   uint32_t* keys, uint32_t* vals, uint32_t* skeys, uint32_t* svals, void* temp,
+                                   uint32_t* keys, uint64_t* vals, uint32_t* skeys, uint64_t* svals, void* temp,
                                    size_t temp_bytes, uint32_t* rops, hipStream_t stream);
 hipError_t launch_rcode(const EngineTables* T, const avr_slice_desc* descs, int n, const uint32_t* rops,
                         const uint64_t* op_off, const uint32_t* counts, uint8_t* out, avr_slice_result* res,

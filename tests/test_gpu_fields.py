@@ -69,10 +69,11 @@ def test_field_picture_slices_match_oracle(ctx, case):
 
 
 @pytest.mark.parametrize("case", CASES[1:5], ids=lambda c: "x".join(map(str, c)))
-def test_field_picture_files_match_oracle(ctx, case):
+def test_field_picture_files_match_oracle(ctx, case, monkeypatch):
     """Whole files in both model modes: the reference model's frame-row coordinates, shared
     frame per field pair and previous-frame contexts, against the oracle; the parallel
     reference-model compress against the sequential kernel."""
+    monkeypatch.setenv("AVR_RMODE_PARALLEL", "1")   # the parallel R-mode compress, whatever the cost rule picks
     st, cf, t8, l0, l1, gop, spp = case
     data = _paff(ctx, 4, slice_type=st, chroma_format_idc=cf, transform_8x8_mode=t8, num_ref_idx_l0=l0,
                  num_ref_idx_l1=l1, gop_length=gop, slices_per_picture=spp, seed=70 + st + 3 * cf)
@@ -91,12 +92,13 @@ def test_field_picture_files_match_oracle(ctx, case):
     assert seq == ctx.compress(data, avr.MODEL_REFERENCE)
 
 
-def test_bottom_field_first(ctx):
+def test_bottom_field_first(ctx, monkeypatch):
     """Field pictures with the bottom field coded first (generator structure 3): the bottom field
     is the IDR / first field, the top field the second field of the same frame_num, so the two
     still share one picture id; the reference model's first-coded field is the bottom one (its
     parallel compress must see the top rows as not yet written).  Batch, both file models, the
     sequential reference-model compress, against the oracle."""
+    monkeypatch.setenv("AVR_RMODE_PARALLEL", "1")   # the parallel R-mode compress, whatever the cost rule picks
     data = _paff(ctx, 4, structure=3, slice_type=1, gop_length=3, slices_per_picture=2, num_ref_idx_l0=2,
                  transform_8x8_mode=1, seed=91)
     d = avr.parse_stream(data).descs
@@ -189,7 +191,8 @@ def test_mbaff_slices_match_oracle(ctx, case):
 
 
 @pytest.mark.parametrize("case", MBAFF_CASES[2:], ids=lambda c: "x".join(map(str, c)))
-def test_mbaff_files_match_oracle(ctx, case):
+def test_mbaff_files_match_oracle(ctx, case, monkeypatch):
+    monkeypatch.setenv("AVR_RMODE_PARALLEL", "1")   # the parallel R-mode compress, whatever the cost rule picks
     st, cf, t8, l0, l1, gop, spp = case
     data = _mbaff(ctx, 4, slice_type=st, chroma_format_idc=cf, transform_8x8_mode=t8, num_ref_idx_l0=l0,
                   num_ref_idx_l1=l1, gop_length=gop, slices_per_picture=spp, seed=120 + st + 3 * cf)
