@@ -13,12 +13,15 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -483,8 +486,10 @@ hipError_t reserve_parallel(avr_ctx* c, int n, int max_w) {
 // regenerate its payload gets status kStatusNoRoundtrip, so no container ever holds a block that
 // cannot be decompressed.
 constexpr int32_t kStatusNoRoundtrip = AVR_SLICE_NO_ROUNDTRIP;
+// out_host: a std::vector<uint8_t> or a Bytes (not zero-filled first: the download overwrites it)
+template <class HostBuf>
 int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_slice_result>* res,
-             std::vector<uint8_t>* out_host, bool verify = false, uint32_t flags = 0) {
+             HostBuf* out_host, bool verify = false, uint32_t flags = 0) {
   const int n = (int)plan.descs.size();
   if (plan.fields()) flags |= avr::kFlagFields;
   res->assign(n, avr_slice_result{0, 0, 0, 0, {0, 0, 0, 0, 0, 0}});
@@ -493,7 +498,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
     d.out_offset = out_total;
     out_total += ((uint64_t)d.out_capacity + 15) & ~15ull;
   }
-  out_host->assign(out_total, 0);
+  out_host->resize(out_total);
   if (!n) return AVR_OK;
   const double t_wall = now_s();
   HIP_TRY(c, c->in.reserve(plan.arena.size() + 4096));
@@ -812,6 +817,35 @@ void parallel_copies(const std::vector<avr::PbCopy>& jobs, uint8_t* base, uint8_
   for (auto& x : th) x.join();
 }
 
+// fn(f) for f in [0, nf) on up to 16 host threads (independent files: segmentation, containers).
+// An exception in a worker (allocation failure) is rethrown here, on the caller's thread, so that
+// guarded() still turns it into a status.
+template <class F>
+void parallel_files(int nf, F&& fn) {
+  const unsigned T = (unsigned)std::min<int>(nf, (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+  if (T <= 1) {
+    for (int f = 0; f < nf; f++) fn(f);
+    return;
+  }
+  std::atomic<int> next{0};
+  std::exception_ptr err;
+  std::mutex mu;
+  auto work = [&]() {
+    try {
+      for (int f; (f = next.fetch_add(1)) < nf;) fn(f);
+    } catch (...) {
+      std::lock_guard<std::mutex> g(mu);
+      if (!err) err = std::current_exception();
+      next = nf;
+    }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < T; t++) th.emplace_back(work);
+  work();
+  for (auto& x : th) x.join();
+  if (err) std::rethrow_exception(err);
+}
+
 // compressor::run's block stream (recode.cpp:1115-1125, 1275-1297) as a Recoded protobuf, written
 // once: the blocks' headers in order, their bytes by parallel_copies, into the caller's buffer dst
 // (cap bytes; too small: AVR_ERR_INVALID_ARGUMENT with *out_len = the size needed) or, without one,
@@ -951,7 +985,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
     }
   }
   std::vector<avr_slice_result> res;
-  std::vector<uint8_t> outb;
+  Bytes outb;
   pc.mark_demux();
   if (int r = run_plan(c, 0, false, plan, &res, &outb, verify,
                        (bills ? avr::kFlagBill : 0u) | coder_flag(model)))
@@ -964,8 +998,8 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
     for (size_t i = 0; i < pf[f].slices.size(); i++)
       ok[f][i] = model == AVR_MODEL_REFERENCE ? st[f] == AVR_OK && recodable_candidate(pf[f].slices[i])
                                               : cand_of[f][i] >= 0 && res[cand_of[f][i]].status == 0;
-    found[f] = segment(in[f], in_len[f], pf[f], ok[f]);
   }
+  parallel_files(nf, [&](int f) { found[f] = segment(in[f], in_len[f], pf[f], ok[f]); });
   // 3) reference model: the coded slices of every file in file order, estimators per file; a
   //    slice that fails there is demoted to skip_coded and its file's pass repeated
   std::vector<std::vector<std::vector<uint8_t>>> recoded(nf);
@@ -998,7 +1032,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
       if (rp.file_first.empty()) break;
       rp.file_first.push_back((int)rp.descs.size());
       std::vector<avr_slice_result> rr;
-      std::vector<uint8_t> ro;
+      Bytes ro;
       if (int r = run_plan(c, 0, true, rp, &rr, &ro, false, bills ? avr::kFlagBill : 0)) return r;
       std::fill(todo.begin(), todo.end(), 0);
       for (size_t k = 0; k < idx.size(); k++) {
@@ -1039,13 +1073,13 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   }
   // 4) containers (compressor::run, recode.cpp:1115-1125)
   int first_err = AVR_OK;
+  parallel_files(nf, [&](int f) {
+    if (st[f] != AVR_OK) return;
+    std::vector<std::pair<const uint8_t*, size_t>> blobs(pf[f].slices.size(), {nullptr, 0});
+    for (size_t i = 0; i < pf[f].slices.size(); i++) blobs[i] = {recoded[f][i].data(), recoded[f][i].size()};
+    st[f] = emit_container(in[f], in_len[f], views_of(pf[f]), found[f], blobs, model, &out[f], &out_len[f]);
+  });
   for (int f = 0; f < nf; f++) {
-    if (st[f] == AVR_OK) {
-      std::vector<std::pair<const uint8_t*, size_t>> blobs(pf[f].slices.size(), {nullptr, 0});
-      for (size_t i = 0; i < pf[f].slices.size(); i++) blobs[i] = {recoded[f][i].data(), recoded[f][i].size()};
-      st[f] = emit_container(in[f], in_len[f], views_of(pf[f]), found[f], blobs, model, &out[f],
-                             &out_len[f]);
-    }
     if (status) status[f] = st[f];
     if (st[f] && !first_err) first_err = st[f];
   }
