@@ -454,6 +454,10 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     lo, hi = shard.partition(sizes, world)[rank]
     part = shard.subset(ps, lo, hi) if rank == 0 else avr.parse_stream(data, lo, hi)
     setup["subset_s"] = time.perf_counter() - t
+    # what this rank's setup held: slices parsed into descriptors, payload bytes copied (rank 0 the
+    # whole stream, the others their own range only)
+    setup_work = [len(ps.descs) if rank == 0 else hi - lo,
+                  len(ps.arena) if rank == 0 else len(part.arena)]
     t = time.perf_counter()
     batch = DeviceBatch(ctx, part)
     drange = DecompressRange(ctx, dev)
@@ -551,9 +555,16 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     bad = torch.tensor([0.0 if good else 1.0], dtype=torch.float64, device=gdev)
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+    # every rank's setup (times and the work it held), for the record
+    mine = torch.tensor([setup["parse_s"], setup["subset_s"], setup["h2d_s"]] + [float(x) for x in setup_work],
+                        dtype=torch.float64, device=gdev)
+    allsetup = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allsetup, mine)
     t = torch.cat([mx, bad])
     if rank != 0:
         return None
+    setup_by_rank = [{"parse_s": round(float(a[0]), 3), "subset_s": round(float(a[1]), 3), "h2d_s": round(float(a[2]), 3),
+                      "slices_parsed": int(a[3]), "payload_bytes_copied": int(a[4])} for a in allsetup]
     exact = bool(t[1] == 0)
     t_comp = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs) / 1e3
     t_dec = sum(e[2].elapsed_time(e[3]) for e in evs) / len(evs) / 1e3
@@ -575,6 +586,7 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
                    "recoded_bytes_C_rank0": C, "compress_ms": t_comp * 1e3, "decompress_ms": t_dec * 1e3,
                    "coder": "arithmetic_code<uint64_t,uint8_t>",
                    "setup_s_rank0": {k: round(v, 3) for k, v in setup.items()},
+                   "setup_by_rank": setup_by_rank,
                    "step_phases_s_rank0": {k: round(v / args.stream_steps, 3) for k, v in phases.items()}},
         "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": (S + C) / t_dom / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (S + C) / t_dom / 1e9 / HBM_PEAK_GBS, "traffic": None,

@@ -47,6 +47,16 @@ def test_bench_default_mode_two_ranks():
     # the configs[3] leg sharded over both ranks inside the default run
     st = line["stream_shard"]
     assert st["n_gpus"] == 2 and st["bit_exact"] is True and st["config"]["slices"] == 30
+    _check_setup_scales(st)
+
+
+def _check_setup_scales(line):
+    """Rank 0 parses the whole stream (its assembly reads every slice); rank 1 holds only its own
+    range's descriptors and payload bytes (setup work on ranks > 0 ~ 1/N)."""
+    r0, r1 = line["config"]["setup_by_rank"]
+    n = line["config"]["slices"]
+    assert r0["slices_parsed"] == n and 0 < r1["slices_parsed"] < n
+    assert r1["payload_bytes_copied"] < 0.8 * r0["payload_bytes_copied"]
 
 
 def test_bench_stream_shard_two_ranks():
@@ -57,3 +67,4 @@ def test_bench_stream_shard_two_ranks():
     assert set(line["config"]["step_phases_s_rank0"]) == {
         "compress_s", "results_d2h_s", "gather_s", "assemble_s", "plan_s", "scatter_h2d_s", "decompress_s",
         "gather_d_s", "splice_s"}
+    _check_setup_scales(line)
