@@ -20,7 +20,8 @@ from dataclasses import dataclass
 import numpy as np
 
 __all__ = [
-    "AvrError", "Context", "MODEL_REFERENCE", "MODEL_PARALLEL", "MODEL_PARALLEL32", "MODEL_NAMES", "SLICE_DESC",
+    "AvrError", "Context", "MODEL_REFERENCE", "MODEL_PARALLEL", "MODEL_PARALLEL32", "MODEL_CHAINED", "MODEL_NAMES",
+    "SLICE_DESC",
     "SLICE_RESULT", "SynthParams", "lib", "parse_stream", "assemble_container", "neighbor_tables",
     "plan_decompress", "splice_container", "container_model", "source_sha", "library_path", "EXPORTED_SYMBOLS",
 ]
@@ -34,7 +35,9 @@ library_path = os.environ.get("AVR_LIBRARY") or os.path.join(_HERE, "libavrecode
 MODEL_REFERENCE = 0
 MODEL_PARALLEL = 1
 MODEL_PARALLEL32 = 2
-MODEL_NAMES = {MODEL_REFERENCE: "R", MODEL_PARALLEL: "P", MODEL_PARALLEL32: "P32"}
+MODEL_CHAINED = 3   # the reference model in chains of CHAIN_SLICES coded slices ("avrecode-amd:R16")
+CHAIN_SLICES = 16
+MODEL_NAMES = {MODEL_REFERENCE: "R", MODEL_PARALLEL: "P", MODEL_PARALLEL32: "P32", MODEL_CHAINED: "C"}
 
 AVR_OK = 0
 _STATUS = {

@@ -96,8 +96,12 @@ namespace {
 
 // Model modes (include/avrecode.h): the reference model, and the parallel model on the reference's
 // arithmetic_code<uint64_t, uint8_t> (PARALLEL) or on the optional 32-bit P32 coder (PARALLEL32).
-bool valid_model(int m) { return m == AVR_MODEL_REFERENCE || m == AVR_MODEL_PARALLEL || m == AVR_MODEL_PARALLEL32; }
+bool valid_model(int m) {
+  return m == AVR_MODEL_REFERENCE || m == AVR_MODEL_PARALLEL || m == AVR_MODEL_PARALLEL32 || m == AVR_MODEL_CHAINED;
+}
 bool parallel_model(int m) { return m == AVR_MODEL_PARALLEL || m == AVR_MODEL_PARALLEL32; }
+// the reference model over a whole file, or in chains of AVR_CHAIN_SLICES coded slices
+bool reference_model(int m) { return m == AVR_MODEL_REFERENCE || m == AVR_MODEL_CHAINED; }
 uint32_t coder_flag(int m) { return m == AVR_MODEL_PARALLEL32 ? avr::kFlagP32 : 0u; }
 constexpr size_t kLdsBudget = 160 * 1024;   // LDS per workgroup (one slice) on gfx950
 constexpr uint64_t kMaxSynthBytes = (uint64_t)1 << 35;   // avr_synthesize_stream's output cap (32 GiB)
@@ -970,7 +974,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   std::vector<std::vector<int>> cand_of(nf);
   for (int f = 0; f < nf; f++) {
     cand_of[f].assign(pf[f].slices.size(), -1);
-    if (st[f] || model == AVR_MODEL_REFERENCE) continue;
+    if (st[f] || reference_model(model)) continue;
     for (size_t i = 0; i < pf[f].slices.size(); i++) {
       const avr::SliceInfo& s = pf[f].slices[i];
       if (!recodable_candidate(s)) continue;
@@ -996,7 +1000,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   for (int f = 0; f < nf; f++) {
     ok[f].assign(pf[f].slices.size(), 0);
     for (size_t i = 0; i < pf[f].slices.size(); i++)
-      ok[f][i] = model == AVR_MODEL_REFERENCE ? st[f] == AVR_OK && recodable_candidate(pf[f].slices[i])
+      ok[f][i] = reference_model(model) ? st[f] == AVR_OK && recodable_candidate(pf[f].slices[i])
                                               : cand_of[f][i] >= 0 && res[cand_of[f][i]].status == 0;
   }
   parallel_files(nf, [&](int f) { found[f] = segment(in[f], in_len[f], pf[f], ok[f]); });
@@ -1004,7 +1008,7 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   //    slice that fails there is demoted to skip_coded and its file's pass repeated
   std::vector<std::vector<std::vector<uint8_t>>> recoded(nf);
   for (int f = 0; f < nf; f++) recoded[f].resize(pf[f].slices.size());
-  if (model == AVR_MODEL_REFERENCE) {
+  if (reference_model(model)) {
     std::vector<char> todo(nf, 0);
     for (int f = 0; f < nf; f++) todo[f] = st[f] == AVR_OK;
     for (int attempt = 0;; attempt++) {
@@ -1014,10 +1018,16 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
         if (!todo[f]) continue;
         if (bills) (*bills)[f] = Bill{};   // this pass re-codes the whole file
         rp.file_first.push_back((int)rp.descs.size());
+        int coded_n = 0;
         for (size_t i = 0; i < pf[f].slices.size(); i++) {
           const avr::SliceInfo& s = pf[f].slices[i];
           avr_slice_desc d = desc_from_header(s);
           d.coded = found[f][i] != nullptr;
+          // chained model: a fresh model (a new "file" of the pass: estimators, frames) before every
+          // AVR_CHAIN_SLICES-th coded slice; uncoded slices before it still flip the old chain's frames
+          if (d.coded && model == AVR_MODEL_CHAINED && coded_n > 0 && coded_n % AVR_CHAIN_SLICES == 0)
+            rp.file_first.push_back((int)rp.descs.size());
+          coded_n += d.coded;
           if (d.coded) {
             append_aligned(&rp.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
             d.payload_size = (uint32_t)s.size;
@@ -1269,8 +1279,9 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
   std::vector<DecJob> jobs(nf);
   // plans[AVR_MODEL_*]: reference-model files (one workgroup each); parallel-model slices on the
   // u64 coder; on the P32 coder
-  Plan plans[3];
+  Plan plans[3];   // indexed by plan_of(model): the chained model's chains go to the reference plan
   Plan& rp = plans[AVR_MODEL_REFERENCE];
+  auto plan_of = [](int m) { return parallel_model(m) ? m : (int)AVR_MODEL_REFERENCE; };
   for (int f = 0; f < nf; f++) {
     out[f] = nullptr;
     out_len[f] = 0;
@@ -1278,13 +1289,22 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
     std::vector<avr::PbBlock> probe;
     const int m = avr::pb_parse(in[f], in_len[f], &probe, &version) ? std::max(0, avr::model_of_version(version)) : 0;
     const bool parallel = parallel_model(m);
-    Plan* plan = &plans[m];
+    Plan* plan = &plans[plan_of(m)];
     const size_t n0 = plan->descs.size();
     if (!parallel) rp.file_first.push_back((int)n0);
     st[f] = decompress_setup(c, in[f], in_len[f], &jobs[f], plan);
     if (st[f]) {   // drop whatever the failed file left (nothing: setup appends only on success)
       plan->descs.resize(n0);
       if (!parallel) rp.file_first.pop_back();
+    } else if (jobs[f].model == AVR_MODEL_CHAINED) {
+      // one workgroup per chain: a new "file" of the sequential launch before every
+      // AVR_CHAIN_SLICES-th coded slice (the compress side's boundaries)
+      int coded_n = 0;
+      for (size_t k = n0; k < plan->descs.size(); k++) {
+        if (!plan->descs[k].coded) continue;
+        if (coded_n > 0 && coded_n % AVR_CHAIN_SLICES == 0) rp.file_first.push_back((int)k);
+        coded_n++;
+      }
     }
   }
   std::vector<avr_slice_result> res_of[3];
@@ -1300,9 +1320,9 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
   int first_err = AVR_OK;
   for (int f = 0; f < nf; f++) {
     DecJob& j = jobs[f];
-    const Plan& plan = plans[j.model];
-    const std::vector<avr_slice_result>& res = res_of[j.model];
-    const std::vector<uint8_t>& outb = out_of[j.model];
+    const Plan& plan = plans[plan_of(j.model)];
+    const std::vector<avr_slice_result>& res = res_of[plan_of(j.model)];
+    const std::vector<uint8_t>& outb = out_of[plan_of(j.model)];
     std::vector<uint8_t> o;
     if (st[f] == AVR_OK)
       st[f] = splice_job(c, j, [&](int k, const uint8_t** p, size_t* len) {
@@ -1898,7 +1918,8 @@ int avr_roundtrip_files(avr_ctx* c, int n_files, const uint8_t* const* in, const
 
 static int batch(avr_ctx* c, int mode, const avr_slice_desc* d_desc, int n, int max_w, int max_h,
                  const uint8_t* d_in, uint8_t* d_out, avr_slice_result* d_res, int model, void* stream) {
-  if (!c || n < 0 || (n && (!d_desc || !d_in || !d_out || !d_res)) || max_w <= 0 || max_h <= 0 || !valid_model(model))
+  if (!c || n < 0 || (n && (!d_desc || !d_in || !d_out || !d_res)) || max_w <= 0 || max_h <= 0 || !valid_model(model) ||
+      model == AVR_MODEL_CHAINED)   // a slice batch has no file to chain over: whole-file calls only
     return AVR_ERR_INVALID_ARGUMENT;
   if (avr::shared_bytes(max_w) > 160 * 1024) return fail(c, AVR_ERR_UNSUPPORTED, "picture too wide for the LDS ring");
   HIP_TRY(c, hipSetDevice(c->device));
@@ -2752,7 +2773,7 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
 
 int avr_hooks_compress_stream_begin(avr_ctx* c, int model, avr_hooks_session** out) {
   if (!c || !out) return AVR_ERR_INVALID_ARGUMENT;
-  if (!valid_model(model)) return AVR_ERR_INVALID_ARGUMENT;
+  if (!valid_model(model) || model == AVR_MODEL_CHAINED) return AVR_ERR_INVALID_ARGUMENT;   // whole-file sessions only
   *out = nullptr;
   avr_hooks_session* hs = new (std::nothrow) avr_hooks_session;
   if (!hs) return AVR_ERR_OUT_OF_MEMORY;

@@ -10,14 +10,16 @@ namespace avr {
 
 const char* const kParallelModelTag = "avrecode-amd:P64";     // parallel model, arithmetic_code<uint64_t, uint8_t>
 const char* const kParallel32ModelTag = "avrecode-amd:P32";   // parallel model, P32 coder (avr_engine.h)
+const char* const kChainedModelTag = "avrecode-amd:R16";      // reference model in chains of 16 coded slices
 
 int model_of_version(const std::string& v) {
   if (v == kParallelModelTag) return 1;
   if (v == kParallel32ModelTag) return 2;
+  if (v == kChainedModelTag) return 3;
   return v.rfind("avrecode-amd:", 0) == 0 ? -1 : 0;
 }
 const char* version_of_model(int model) {
-  return model == 1 ? kParallelModelTag : model == 2 ? kParallel32ModelTag : nullptr;
+  return model == 1 ? kParallelModelTag : model == 2 ? kParallel32ModelTag : model == 3 ? kChainedModelTag : nullptr;
 }
 
 namespace {

@@ -124,6 +124,7 @@ bool pb_read_version(const uint8_t* in, size_t n, std::string* version);
 // through the optional 32-bit P32 coder
 extern const char* const kParallelModelTag;     // "avrecode-amd:P64"
 extern const char* const kParallel32ModelTag;   // "avrecode-amd:P32"
+extern const char* const kChainedModelTag;      // "avrecode-amd:R16"
 // The model a container's Metadata.version names: 0 reference (no tag, or any foreign one), 1
 // parallel / u64 coder, 2 parallel / P32 coder (AVR_MODEL_*); -1 another avrecode-amd format (the
 // round-2 "avrecode-amd:P", ...), which must be refused rather than read as a reference container.

@@ -1,7 +1,8 @@
-// recode CLI (recode.cpp:1627-1659): recode [compress|decompress|roundtrip] [-p|-p32] <input> [output]
+// recode CLI (recode.cpp:1627-1659): recode [compress|decompress|roundtrip] [-p|-p32|-c] <input> [output]
 //   -p    parallel model (fresh model per slice; slices independent) on the reference's
 //         arithmetic_code<uint64_t, uint8_t>; default = reference model.
 //   -p32  parallel model on the optional 32-bit P32 coder (avrecode-amd:P32 containers).
+//   -c    the reference model in chains of 16 coded slices (avrecode-amd:R16 containers).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -36,13 +37,14 @@ static void print_bill(const char* title, const uint64_t* b) {
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    std::cerr << "Usage: " << argv[0] << " [compress|decompress|roundtrip] [-p|-p32] <input> [output]" << std::endl;
+    std::cerr << "Usage: " << argv[0] << " [compress|decompress|roundtrip] [-p|-p32|-c] <input> [output]" << std::endl;
     return 1;
   }
   std::string cmd = argv[1];
   int a = 2, model = AVR_MODEL_REFERENCE;
   if (!strcmp(argv[a], "-p")) model = AVR_MODEL_PARALLEL, a++;
   else if (!strcmp(argv[a], "-p32")) model = AVR_MODEL_PARALLEL32, a++;
+  else if (!strcmp(argv[a], "-c")) model = AVR_MODEL_CHAINED, a++;
   if (a >= argc) return 1;
   const char* input = argv[a++];
   const char* output = a < argc ? argv[a] : nullptr;

@@ -56,7 +56,15 @@ typedef enum {
  * r1 = floor(range * floor(2^32 / tot) / 2^32) * pos; avr_engine.h PEncoder): fewer instructions per
  * decision, not the reference's arithmetic.  Tagged "avrecode-amd:P32".  Containers of every mode
  * decompress with avr_decompress_file, which reads the tag. */
-typedef enum { AVR_MODEL_REFERENCE = 0, AVR_MODEL_PARALLEL = 1, AVR_MODEL_PARALLEL32 = 2 } avr_model;
+/* AVR_MODEL_CHAINED: the reference model in chains -- a fresh model (estimators and frame metadata,
+ * as at the start of a file) before every AVR_CHAIN_SLICES-th coded slice of a file, tagged
+ * "avrecode-amd:R16".  It compresses like the reference model (the estimators learn across a chain's
+ * 16 slices: realshort.mp4 0.998, cockatoo.mp4 0.994 of the input, against 0.990 / 0.991 for the
+ * reference model and 1.041 / 1.010 for the parallel one), and a file's chains decode on as many
+ * workgroups at once.  Whole-file calls only (avr_compress_file(s), avr_decompress_file(s),
+ * avr_roundtrip_file(s)); the device slice-batch calls and the hooks refuse it. */
+typedef enum { AVR_MODEL_REFERENCE = 0, AVR_MODEL_PARALLEL = 1, AVR_MODEL_PARALLEL32 = 2, AVR_MODEL_CHAINED = 3 } avr_model;
+#define AVR_CHAIN_SLICES 16
 
 typedef struct avr_ctx avr_ctx;
 

@@ -242,7 +242,12 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
 /* R: the reference model.  P: the parallel model (fresh model per slice) on the reference's
  * arithmetic_code<uint64_t, uint8_t> (tag "avrecode-amd:P64").  P32: the parallel model on the P-format
  * coder below (tag "avrecode-amd:P32"). */
-enum { AVR_MODE_R = 0, AVR_MODE_P = 1, AVR_MODE_P32 = 2 };
+enum { AVR_MODE_R = 0, AVR_MODE_P = 1, AVR_MODE_P32 = 2, AVR_MODE_C = 3 };
+/* C: the reference model in chains -- a fresh model (estimators and frames, as a new file) before
+ * every AVR_CHAIN_SLICES-th coded slice (tag "avrecode-amd:R16"): each chain is sequential, the chains
+ * are independent, so a file decodes with (coded slices / 16) walkers at once while the model still
+ * learns across a chain's slices. */
+#define AVR_CHAIN_SLICES 16
 
 typedef struct avr_model avr_model_t;
 avr_model_t *avr_model_new(void);
@@ -295,7 +300,7 @@ typedef struct {
 } avr_pb_block_t;
 void avr_pb_put_block(obuf_t *o, const avr_pb_block_t *b);
 /* model mode recorded in Recoded.metadata.version (R-mode: absent, as the reference writes):
- * AVR_MODE_R / _P / _P32, or -1 for another "avrecode-amd:" format */
+ * AVR_MODE_R / _P / _P32 / _C, or -1 for another "avrecode-amd:" format */
 int avr_pb_mode(const uint8_t *in, size_t n);
 /* parses a Recoded message; returns block count, *blocks malloc'd (pointers into in) */
 int avr_pb_parse(const uint8_t *in, size_t n, avr_pb_block_t **blocks);

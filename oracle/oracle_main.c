@@ -1,13 +1,14 @@
 /*
  * Oracle CLI (mirrors recode.cpp:1627-1659 main).  TEST INFRASTRUCTURE ONLY.
  *
- *   recode_oracle compress   [-p|-p32] <input> [output]
+ *   recode_oracle compress   [-p|-p32|-c] <input> [output]
  *   recode_oracle decompress           <input> [output]
- *   recode_oracle roundtrip  [-p|-p32] <input> [output]
+ *   recode_oracle roundtrip  [-p|-p32|-c] <input> [output]
  *   recode_oracle slices          <input>          per-slice parse / regeneration report
  *
  * -p selects the parallel model (fresh model per slice) on arithmetic_code<uint64_t, uint8_t>, -p32 the
- * parallel model on the P-format coder; default is the reference model.
+ * parallel model on the P-format coder, -c the reference model in chains of 16 coded slices (a
+ * fresh model before every 16th: avrecode-amd:R16); default is the reference model.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -119,12 +120,13 @@ int main(int argc, char **argv) {
   int mode = AVR_MODE_R;
   int a = 1;
   if (argc < 3) {
-    fprintf(stderr, "Usage: %s [compress|decompress|roundtrip|slices] [-p] <input> [output]\n", argv[0]);
+    fprintf(stderr, "Usage: %s [compress|decompress|roundtrip|slices] [-p|-p32|-c] <input> [output]\n", argv[0]);
     return 1;
   }
   const char *cmd = argv[a++];
   if (a < argc && !strcmp(argv[a], "-p")) { mode = AVR_MODE_P; a++; }
   else if (a < argc && !strcmp(argv[a], "-p32")) { mode = AVR_MODE_P32; a++; }
+  else if (a < argc && !strcmp(argv[a], "-c")) { mode = AVR_MODE_C; a++; }
   if (a >= argc) return 1;
   const char *in = argv[a++];
   const char *outp = a < argc ? argv[a] : NULL;

@@ -30,6 +30,7 @@ size_t avr_last_bill[8], avr_last_cabac_bill[8];
 static const int SURROGATE_MARKER_BYTES = 8; /* recode.cpp:27 */
 #define AVR_P_MODE_TAG "avrecode-amd:P64"     /* the parallel model + arithmetic_code<uint64_t, uint8_t> */
 #define AVR_P32_MODE_TAG "avrecode-amd:P32"   /* the parallel model + P-format coder (avr_oracle.h) */
+#define AVR_C_MODE_TAG "avrecode-amd:R16"     /* the reference model in chains of 16 coded slices */
 
 /* ===================================================================== protobuf wire codec */
 static void pb_varint(obuf_t *o, uint64_t v) {
@@ -117,6 +118,7 @@ int avr_pb_mode(const uint8_t *in, size_t n) {
         if ((t2 >> 3) == 1)
           mode = (l2 == strlen(AVR_P_MODE_TAG) && !memcmp(q, AVR_P_MODE_TAG, l2))       ? AVR_MODE_P
                  : (l2 == strlen(AVR_P32_MODE_TAG) && !memcmp(q, AVR_P32_MODE_TAG, l2)) ? AVR_MODE_P32
+                 : (l2 == strlen(AVR_C_MODE_TAG) && !memcmp(q, AVR_C_MODE_TAG, l2))     ? AVR_MODE_C
                  : (l2 >= 13 && !memcmp(q, "avrecode-amd:", 13))                          ? -1
                                                                                         : AVR_MODE_R;
         q += l2;
@@ -621,13 +623,15 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
   if (nn < 0) return -1;
   stream_state_t *st = (stream_state_t *)calloc(1, sizeof(stream_state_t));
   st->x264_build = -1;
-  avr_model_t *model = mode == AVR_MODE_R ? avr_model_new() : NULL;
+  const int ref = mode == AVR_MODE_R || mode == AVR_MODE_C;   /* the reference model (whole file or chains) */
+  avr_model_t *model = ref ? avr_model_new() : NULL;
+  size_t chain_n = 0;   /* coded slices so far (C: a fresh model before every AVR_CHAIN_SLICES-th) */
   obuf_t o;
   ob_init(&o);
   if (mode != AVR_MODE_R) {
-    /* Recoded.Metadata.version (recode.proto:3) tags the parallel model and its coder; R-mode writes
-     * none, exactly like the reference (which never sets metadata). */
-    const char *tag = mode == AVR_MODE_P32 ? AVR_P32_MODE_TAG : AVR_P_MODE_TAG;
+    /* Recoded.Metadata.version (recode.proto:3) tags the parallel model and its coder, or the chained
+     * reference model; R-mode writes none, exactly like the reference (which never sets metadata). */
+    const char *tag = mode == AVR_MODE_P32 ? AVR_P32_MODE_TAG : mode == AVR_MODE_C ? AVR_C_MODE_TAG : AVR_P_MODE_TAG;
     obuf_t md;
     ob_init(&md);
     pb_bytes(&md, 1, (const uint8_t *)tag, strlen(tag));
@@ -653,11 +657,18 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
       lit.literal_len = gap;
       avr_pb_put_block(&o, &lit);
       prev_end += gap + s.size;
-      avr_model_t *m = mode == AVR_MODE_R ? model : model_new_p(mode == AVR_MODE_P32);
+      if (mode == AVR_MODE_C && chain_n > 0 && chain_n % AVR_CHAIN_SLICES == 0) {   /* a new chain */
+        size_t unused[8] = {0};
+        avr_model_bills(model, avr_last_bill, unused);
+        avr_model_free(model);
+        model = avr_model_new();
+      }
+      chain_n++;
+      avr_model_t *m = ref ? model : model_new_p(mode == AVR_MODE_P32);
       obuf_t rc;
       size_t bins = 0;
       int r = compress_slice_with_model(m, &s, &rc, &bins);
-      if (mode != AVR_MODE_R) {
+      if (!ref) {
         size_t unused[8] = {0};
         avr_model_bills(m, avr_last_bill, unused);
         avr_model_free(m);
@@ -751,7 +762,8 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
   st->x264_build = -1;
   avr_model_t *model = avr_model_new();
   const int mode = avr_pb_mode(in, n);
-  int mode_r = mode == AVR_MODE_R;
+  int mode_r = mode == AVR_MODE_R || mode == AVR_MODE_C;   /* the reference model (C: in chains) */
+  size_t chain_n = 0;
   if (mode < 0) ret = -10;   /* another avrecode-amd format */
   size_t unused_bill[8] = {0};
   memset(avr_last_cabac_bill, 0, sizeof(avr_last_cabac_bill));
@@ -765,6 +777,12 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
     avr_pb_block_t *b = &blocks[next_coded];
     if ((size_t)b->size != s.size) { ret = -7; free(s.rbsp); break; }
     if (b->has_cabac) {
+      if (mode == AVR_MODE_C && chain_n > 0 && chain_n % AVR_CHAIN_SLICES == 0) {   /* a new chain */
+        avr_model_bills(model, unused_bill, avr_last_cabac_bill);
+        avr_model_free(model);
+        model = avr_model_new();
+      }
+      chain_n++;
       avr_model_t *m = model;
       avr_model_t *fresh = NULL;
       if (!mode_r) m = fresh = model_new_p(mode == AVR_MODE_P32);

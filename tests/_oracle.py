@@ -71,7 +71,7 @@ def oracle_cli(cmd, path, mode="R", out=None):
     _, cli = build_oracle()
     with tempfile.TemporaryDirectory() as td:
         o = Path(td) / "out.bin"
-        args = [str(cli), cmd] + {"R": [], "P": ["-p"], "P32": ["-p32"]}[mode] + [str(path), str(o)]
+        args = [str(cli), cmd] + {"R": [], "P": ["-p"], "P32": ["-p32"], "C": ["-c"]}[mode] + [str(path), str(o)]
         r = subprocess.run(args, capture_output=True)
         if r.returncode != 0:
             raise RuntimeError(f"recode_oracle {cmd} failed: {r.stderr.decode()}")

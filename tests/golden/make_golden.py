@@ -175,14 +175,14 @@ def main():
     (GOLD / "container.json").write_text(json.dumps(container_golden()))
     fx = []
     for name in ["realshort.mp4", "cockatoo.mp4"]:
-        for mode in ["R", "P", "P32"]:
+        for mode in ["R", "P", "P32", "C"]:
             data = oracle_cli("compress", ROOT / "tests" / "fixtures" / name, mode=mode)
             fx.append({"file": name, "mode": mode, "avrc_len": len(data), "avrc_sha256": hashlib.sha256(data).hexdigest()})
     (GOLD / "fixtures.json").write_text(json.dumps(fx, indent=1))
     # fields.json: the field-coded fixtures' containers (the entries' descriptions are kept)
     fields = json.loads((GOLD / "fields.json").read_text())
     for e in fields["files"]:
-        for mode in ["R", "P", "P32"]:
+        for mode in ["R", "P", "P32", "C"]:
             data = oracle_cli("compress", ROOT / "tests" / "fixtures" / e["file"], mode=mode)
             e[mode] = {"avrc_len": len(data), "avrc_sha256": hashlib.sha256(data).hexdigest()}
     (GOLD / "fields.json").write_text(json.dumps(fields, indent=1) + "\n")

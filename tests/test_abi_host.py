@@ -103,7 +103,8 @@ def test_assemble_container_rejects_bad_arguments():
 
 def test_container_model_of_each_format():
     from _oracle import oracle_cli
-    for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL), ("P32", avr.MODEL_PARALLEL32)):
+    for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL), ("P32", avr.MODEL_PARALLEL32),
+                        ("C", avr.MODEL_CHAINED)):
         assert avr.container_model(oracle_cli("compress", FIX / "realshort.mp4", mode=mode)) == model
     with pytest.raises(avr.AvrError):
         avr.container_model(b"\x0a\x10\x0a\x0eavrecode-amd:P")   # the round-2 format: refused

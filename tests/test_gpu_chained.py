@@ -1,0 +1,98 @@
+"""The chained reference model (AVR_MODEL_CHAINED, "avrecode-amd:R16"): the reference model with a
+fresh model before every 16th coded slice of a file.  Its containers must equal the oracle's
+(tests/test_oracle_fixtures.py pins each chain to the reference model run on that chain alone), on
+every device path the reference model has -- the parallel R-mode compress pass with chains as its
+files, the per-chain sequential kernel, batches of several files -- and its decompress runs one
+workgroup per chain.
+"""
+import time
+
+import pytest
+
+from _oracle import ROOT, oracle_cli
+
+torch = pytest.importorskip("torch")
+import avrecode_amd as avr  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+FIX = ROOT / "tests" / "fixtures"
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = avr.Context(0)
+    yield c
+    c.close()
+
+
+def _tiled(copies=5):
+    import bench
+    head, sl = bench._split_slices((FIX / "paff_ipp.264").read_bytes())
+    return head + b"".join(sl * copies)
+
+
+def _oracle_c(data, tmp_path, name="x.264"):
+    f = tmp_path / name
+    f.write_bytes(data)
+    return oracle_cli("compress", f, mode="C")
+
+
+def test_chained_every_compress_path_matches_oracle(ctx, tmp_path, monkeypatch):
+    """40 field slices (three chains): whichever path the cost rule picks, the parallel R-mode pass
+    with chains as files (AVR_RMODE_PARALLEL) and one sequential workgroup per chain
+    (AVR_RMODE_SEQUENTIAL) give the oracle's container, and it decompresses back."""
+    data = _tiled()
+    ref = _oracle_c(data, tmp_path)
+    assert avr.container_model(ref) == avr.MODEL_CHAINED
+    assert ctx.compress(data, avr.MODEL_CHAINED) == ref
+    monkeypatch.setenv("AVR_RMODE_PARALLEL", "1")
+    assert ctx.compress(data, avr.MODEL_CHAINED) == ref
+    monkeypatch.delenv("AVR_RMODE_PARALLEL")
+    monkeypatch.setenv("AVR_RMODE_SEQUENTIAL", "1")
+    assert ctx.compress(data, avr.MODEL_CHAINED) == ref
+    monkeypatch.delenv("AVR_RMODE_SEQUENTIAL")
+    assert ctx.decompress(ref) == data
+    assert ctx.decompress(oracle_cli("compress", tmp_path / "x.264", mode="R")) == data   # R unchanged
+
+
+def test_chained_file_batch(ctx, tmp_path):
+    """Several files in one batch, chains of each file cut independently: every container equals
+    the oracle's for that file alone, and the batched decompress restores every file."""
+    datas = [_tiled(3), (FIX / "cockatoo.mp4").read_bytes(), (FIX / "realshort.mp4").read_bytes(), _tiled(2)]
+    outs = ctx.compress_files(datas, avr.MODEL_CHAINED)
+    for i, (d, o) in enumerate(zip(datas, outs)):
+        assert o == _oracle_c(d, tmp_path, f"f{i}.bin"), i
+    assert ctx.decompress_files(outs) == datas
+
+
+def test_chained_roundtrip_and_ratio(ctx):
+    """avr_roundtrip_file in the chained model; its container sits between the reference model's
+    and the parallel model's (realshort: R 0.990, C 0.998, P 1.041)."""
+    data = (FIX / "realshort.mp4").read_bytes()
+    c, st = ctx.roundtrip(data, avr.MODEL_CHAINED)
+    r = ctx.compress(data, avr.MODEL_REFERENCE)
+    p = ctx.compress(data, avr.MODEL_PARALLEL)
+    assert len(r) <= len(c) < len(p) and len(c) < len(data)
+
+
+def test_chained_decompress_runs_chains_at_once(ctx):
+    """cockatoo.mp4 (267 coded slices: 17 chains): the chained container decompresses on one
+    workgroup per chain, several times faster than the reference model's one chain (3.6 s)."""
+    data = (FIX / "cockatoo.mp4").read_bytes()
+    r = ctx.compress(data, avr.MODEL_REFERENCE)
+    c = ctx.compress(data, avr.MODEL_CHAINED)
+    ctx.decompress(c)   # warm
+    t0 = time.perf_counter()
+    assert ctx.decompress(r) == data
+    t_r = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    assert ctx.decompress(c) == data
+    t_c = time.perf_counter() - t0
+    print(f"cockatoo decompress: R {t_r:.3f} s, chained {t_c:.3f} s")
+    assert t_c < 0.5 * t_r
+
+
+def test_chained_refused_by_slice_batches_and_streaming_hooks(ctx):
+    z = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(avr.AvrError):
+        ctx.compress_slices(z, 0, 1, 1, z, z, z, model=avr.MODEL_CHAINED)

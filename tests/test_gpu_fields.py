@@ -143,7 +143,7 @@ def test_field_fixture_matches_golden(ctx, name):
     import json
     g = {e["file"]: e for e in json.loads((Path(__file__).parent / "golden" / "fields.json").read_text())["files"]}[name]
     data = (Path(__file__).parent / "fixtures" / name).read_bytes()
-    for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+    for mode, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL), ("C", avr.MODEL_CHAINED)):
         avrc = ctx.compress(data, model)
         assert hashlib.sha256(avrc).hexdigest() == g[mode]["avrc_sha256"], mode
         assert ctx.decompress(avrc) == data

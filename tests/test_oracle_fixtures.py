@@ -21,7 +21,7 @@ def test_every_slice_regenerates(name, nslices):
 
 
 @pytest.mark.parametrize("name", ["realshort.mp4", "cockatoo.mp4"])
-@pytest.mark.parametrize("mode", ["R", "P"])
+@pytest.mark.parametrize("mode", ["R", "P", "C"])
 def test_roundtrip_and_golden(name, mode):
     out = oracle_cli("roundtrip", FIX / name, mode=mode)
     assert b"roundtrip succeeded" in out
@@ -55,8 +55,38 @@ def test_field_fixture_regenerates_and_roundtrips(g):
     f = FIX / g["file"]
     r = subprocess.run([str(cli), "slices", str(f)], capture_output=True, text=True)
     assert r.returncode == 0 and f"slices ok {g['slices']} bad 0" in r.stdout, r.stdout[-2000:]
-    for mode in ("R", "P"):
+    for mode in ("R", "P", "C"):
         assert b"roundtrip succeeded" in oracle_cli("roundtrip", f, mode=mode)
         avrc = oracle_cli("compress", f, mode=mode)
         assert len(avrc) == g[mode]["avrc_len"]
         assert hashlib.sha256(avrc).hexdigest() == g[mode]["avrc_sha256"]
+
+
+def _tiled_paff(copies=5):
+    """The PAFF fixture's slices tiled (every copy restarts at its IDR picture): 8 * copies slices,
+    so the chained model (AVR_CHAIN_SLICES = 16) cuts it into several chains."""
+    import bench
+    head, sl = bench._split_slices((FIX / "paff_ipp.264").read_bytes())
+    return head, sl * copies
+
+
+def test_chained_model_is_the_reference_model_per_chain(tmp_path):
+    """The chained model ("avrecode-amd:R16") is the reference model restarted every 16 coded slices:
+    chain j's re-coded blocks equal the reference model's blocks for a file made of the parameter
+    sets and chain j's slices alone (recode.cpp:1057's fresh estimators and update_frame_spec's fresh
+    frames at that file's start), so the chained format is pinned wherever the reference model is."""
+    import avrecode_amd as avr
+    head, sl = _tiled_paff()
+    data = head + b"".join(sl)
+    f = tmp_path / "tiled.264"
+    f.write_bytes(data)
+    assert b"roundtrip succeeded" in oracle_cli("roundtrip", f, mode="C")
+    blocks = [b["cabac"] for b in avr.describe_container(oracle_cli("compress", f, mode="C"))[0]["blocks"] if "cabac" in b]
+    assert len(blocks) == len(sl) == 40
+    whole_r = [b["cabac"] for b in avr.describe_container(oracle_cli("compress", f, mode="R"))[0]["blocks"] if "cabac" in b]
+    assert blocks[:16] == whole_r[:16] and blocks[16:] != whole_r[16:]
+    for j in range(0, len(sl), 16):
+        g = tmp_path / f"chain{j}.264"
+        g.write_bytes(head + b"".join(sl[j:j + 16]))
+        sub = [b["cabac"] for b in avr.describe_container(oracle_cli("compress", g, mode="R"))[0]["blocks"] if "cabac" in b]
+        assert blocks[j:j + 16] == sub, j
