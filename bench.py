@@ -226,7 +226,8 @@ def _round_phases(ph):
 def file_roundtrips(ctx, args):
     """The north-star command, `recode roundtrip <file>` (recode.cpp:1594-1624), on whole files from
     host memory: avr_roundtrip_file = demux + compress (device) + container + decompress (device) +
-    byte compare, both model modes.  MB/s = file bytes / wall time of one roundtrip call (median of
+    byte compare, in the reference model (R), the parallel model (P) and the chained reference model
+    (C: R restarted every 16 coded slices).  MB/s = file bytes / wall time of one roundtrip call (median of
     the timed reps after one untimed warm-up; PCIe copies and host container work included).  Beside
     each file: the CPU oracle's R-mode roundtrip on one host core."""
     import tempfile
@@ -237,7 +238,7 @@ def file_roundtrips(ctx, args):
     out = {}
     for name, data in files:
         rec = {"bytes": len(data)}
-        for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+        for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL), ("C", avr.MODEL_CHAINED)):
             walls, comps, decs, stats = [], [], [], []
             # the first call warms up (buffer allocation); a call of seconds is its own sample
             for it in range(1 + args.file_reps):
@@ -281,9 +282,9 @@ def corpus_section(ctx, args):
     1/2/4/8/17 slices per frame, IBBP and IP GOPs, 4:2:0/4:2:2/4:4:4, plus the two fixtures) as ONE
     batch through avr_roundtrip_files (batched compress + decompress + byte compare of every file,
     the reference's roundtrip over a corpus; the parallel model's per-slice device check runs only
-    for a file whose first container does not come back), both model modes.
+    for a file whose first container does not come back), in the R, P and chained (C) models.
     MB/s = corpus bytes / (the whole call's wall time, median of reps);
-    compression ratio = container bytes / input bytes, P-mode against R-mode (the reference model).
+    compression ratio = container bytes / input bytes, P and C against R (the reference model).
     CPU beside it: the oracle's R-mode roundtrip of every file, one core."""
     import tempfile
     import avrecode_amd as avr
@@ -293,7 +294,7 @@ def corpus_section(ctx, args):
     total = sum(map(len, datas))
     rec = {"files": len(files), "bytes": total, "names": [n for n, _ in files]}
     sizes = {}
-    for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+    for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL), ("C", avr.MODEL_CHAINED)):
         walls, tc, td = [], [], []
         for it in range(1 + args.file_reps):
             t0 = time.perf_counter()
@@ -313,7 +314,8 @@ def corpus_section(ctx, args):
         rec[tag] = {"MB_s": total / walls[k] / 1e6, "wall_s": walls[k], "compress_s": tc[k], "decompress_s": td[k],
                     "avrc_bytes": sum(sizes[tag]), "ratio": sum(sizes[tag]) / total, "bit_exact": True}
     rec["ratio_P_over_R"] = rec["P"]["avrc_bytes"] / rec["R"]["avrc_bytes"]
-    rec["per_file_ratio"] = {n: {"R": sizes["R"][i] / len(d), "P": sizes["P"][i] / len(d)}
+    rec["ratio_C_over_R"] = rec["C"]["avrc_bytes"] / rec["R"]["avrc_bytes"]
+    rec["per_file_ratio"] = {n: {"R": sizes["R"][i] / len(d), "P": sizes["P"][i] / len(d), "C": sizes["C"][i] / len(d)}
                              for i, (n, d) in enumerate(files)}
     if not args.no_cpu_baseline:
         tot = 0.0
@@ -780,7 +782,7 @@ def corpus_sharded(ctx, args, world, rank, dev):
     datas = [files[i][1] for i in mine]
     rec = {"files": len(files), "bytes": total, "n_gpus": world, "scaling": "strong",
            "files_rank0": [files[i][0] for i in shard.deal_files([len(d) for _, d in files], world)[0]]}
-    for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL)):
+    for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL), ("C", avr.MODEL_CHAINED)):
         for it in range(2):   # one warm-up pass, one timed
             dist.barrier()
             t0 = time.perf_counter()

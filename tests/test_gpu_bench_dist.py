@@ -43,7 +43,7 @@ def test_bench_default_mode_two_ranks():
     assert line["n_gpus"] == 2 and line["bit_exact"] is True
     assert line["scaling"] == "weak" and line["value"] > 0
     assert line["corpus"]["n_gpus"] == 2
-    assert line["corpus"]["R"]["bit_exact"] is True and line["corpus"]["P"]["bit_exact"] is True
+    assert all(line["corpus"][m]["bit_exact"] is True for m in ("R", "P", "C"))
     # the configs[3] leg sharded over both ranks inside the default run
     st = line["stream_shard"]
     assert st["n_gpus"] == 2 and st["bit_exact"] is True and st["config"]["slices"] == 30
