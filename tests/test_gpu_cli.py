@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 FIX = ROOT / "tests" / "fixtures"
 CLI = ROOT / "avrecode_amd" / "recode"
 GOLD = {(g["file"], g["mode"]): g for g in json.loads((ROOT / "tests/golden/fixtures.json").read_text())}
-CASES = [(f, m) for f in ("realshort.mp4", "cockatoo.mp4") for m in ("R", "P")]
+CASES = [(f, m) for f in ("realshort.mp4", "cockatoo.mp4") for m in ("R", "P", "C")]
+FLAGS = {"R": [], "P": ["-p"], "C": ["-c"]}
 
 
 def _run(args, timeout=120):
@@ -33,7 +34,7 @@ def _run(args, timeout=120):
 def test_cli_roundtrip(name, mode):
     with tempfile.TemporaryDirectory() as td:
         out = Path(td) / "x.avrc"
-        args = ["roundtrip"] + (["-p"] if mode == "P" else []) + [FIX / name, out]
+        args = ["roundtrip"] + FLAGS[mode] + [FIX / name, out]
         r = _run(args)
         assert r.returncode == 0, r.stderr.decode()
         text = r.stdout.decode()
@@ -49,12 +50,12 @@ def test_cli_compress_then_decompress(name, mode):
     data = (FIX / name).read_bytes()
     with tempfile.TemporaryDirectory() as td:
         c, d = Path(td) / "c.avrc", Path(td) / "d.mp4"
-        r = _run(["compress"] + (["-p"] if mode == "P" else []) + [FIX / name, c])
+        r = _run(["compress"] + FLAGS[mode] + [FIX / name, c])
         assert r.returncode == 0, r.stderr.decode()
         avrc = c.read_bytes()
         assert hashlib.sha256(avrc).hexdigest() == GOLD[(name, mode)]["avrc_sha256"]
         m = _pb.check_container(avrc, data)
-        assert bool(m.HasField("metadata")) == (mode == "P")
+        assert bool(m.HasField("metadata")) == (mode != "R")
         r = _run(["decompress", c, d])
         assert r.returncode == 0, r.stderr.decode()
         assert d.read_bytes() == data
