@@ -83,14 +83,14 @@ def test_hooks_compress_then_decompress(name, mode, model):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model", [0, 1, 2], ids=["R", "P64", "P32"])
+@pytest.mark.parametrize("model", [0, 1, 2, 3], ids=["R", "P64", "P32", "C"])
 def test_hooks_decompress_on_demand(model):
     """A parallel-model container through the hooks is decoded on demand, as the reference's
     decompressor decodes each slice when FFmpeg reaches it (recode.cpp:1411-1520): nothing is
     regenerated before the first init_decoder, each init_decoder that reaches a slice not yet
     regenerated runs one device batch (that slice and at most 31 coded slices after it), and
-    avr_hooks_end still returns the original file.  A reference-model container is regenerated
-    whole at begin (its estimators chain across slices): the debug count reads -1 there."""
+    avr_hooks_end still returns the original file.  A reference-model container (whole or chained)
+    is regenerated whole at begin (its estimators chain across slices): the debug count reads -1."""
     data = (FIX / "cockatoo.mp4").read_bytes()
     r, avrc, walked = _call("hooks_compress", data, len(data), model)
     assert r == 0, r
@@ -102,7 +102,7 @@ def test_hooks_decompress_on_demand(model):
     n = L.hooks_slice_regen(buf, 4096)
     regen = list(buf[:n])
     assert n == 280   # cockatoo's slices, one init_decoder each
-    if model == 0:
+    if model in (0, 3):   # the reference model, whole or in chains: regenerated at begin
         assert set(regen) == {-1}
         return
     assert 0 < regen[0] <= 32
