@@ -62,7 +62,8 @@ typedef enum {
  * 16 slices: realshort.mp4 0.998, cockatoo.mp4 0.994 of the input, against 0.990 / 0.991 for the
  * reference model and 1.041 / 1.010 for the parallel one), and a file's chains decode on as many
  * workgroups at once.  Whole-file calls only (avr_compress_file(s), avr_decompress_file(s),
- * avr_roundtrip_file(s)); the device slice-batch calls and the hooks refuse it. */
+ * avr_roundtrip_file(s), and the whole-file hooks sessions); the device slice-batch calls and the
+ * streaming hooks session refuse it with AVR_ERR_INVALID_ARGUMENT. */
 typedef enum { AVR_MODEL_REFERENCE = 0, AVR_MODEL_PARALLEL = 1, AVR_MODEL_PARALLEL32 = 2, AVR_MODEL_CHAINED = 3 } avr_model;
 #define AVR_CHAIN_SLICES 16
 
