@@ -25,10 +25,12 @@ def ctx():
     c.close()
 
 
-def _tiled(copies=5):
+def _tiled(copies=5, lead=0):
+    """The PAFF fixture's 8 slices tiled; lead > 0 repeats the first GOP's first `lead` slices before
+    the tiles, so that chain boundaries fall on P fields inside a GOP."""
     import bench
     head, sl = bench._split_slices((FIX / "paff_ipp.264").read_bytes())
-    return head + b"".join(sl * copies)
+    return head + b"".join(sl[:lead] + sl * copies)
 
 
 def _oracle_c(data, tmp_path, name="x.264"):
@@ -37,11 +39,12 @@ def _oracle_c(data, tmp_path, name="x.264"):
     return oracle_cli("compress", f, mode="C")
 
 
-def test_chained_every_compress_path_matches_oracle(ctx, tmp_path, monkeypatch):
-    """40 field slices (three chains): whichever path the cost rule picks, the parallel R-mode pass
-    with chains as files (AVR_RMODE_PARALLEL) and one sequential workgroup per chain
+@pytest.mark.parametrize("lead", [0, 3], ids=["idr_aligned", "mid_gop"])
+def test_chained_every_compress_path_matches_oracle(ctx, tmp_path, monkeypatch, lead):
+    """40 (43) field slices, three chains: whichever path the cost rule picks, the parallel R-mode
+    pass with chains as files (AVR_RMODE_PARALLEL) and one sequential workgroup per chain
     (AVR_RMODE_SEQUENTIAL) give the oracle's container, and it decompresses back."""
-    data = _tiled()
+    data = _tiled(lead=lead)
     ref = _oracle_c(data, tmp_path)
     assert avr.container_model(ref) == avr.MODEL_CHAINED
     assert ctx.compress(data, avr.MODEL_CHAINED) == ref

@@ -70,19 +70,23 @@ def _tiled_paff(copies=5):
     return head, sl * copies
 
 
-def test_chained_model_is_the_reference_model_per_chain(tmp_path):
+@pytest.mark.parametrize("lead", [0, 3], ids=["idr_aligned", "mid_gop"])
+def test_chained_model_is_the_reference_model_per_chain(tmp_path, lead):
     """The chained model ("avrecode-amd:R16") is the reference model restarted every 16 coded slices:
     chain j's re-coded blocks equal the reference model's blocks for a file made of the parameter
     sets and chain j's slices alone (recode.cpp:1057's fresh estimators and update_frame_spec's fresh
     frames at that file's start), so the chained format is pinned wherever the reference model is."""
     import avrecode_amd as avr
     head, sl = _tiled_paff()
+    # lead > 0: the first GOP's first `lead` slices again before the tiles (they are a valid start:
+    # the IDR field pair and a P field), so the chain boundaries fall on P fields inside a GOP
+    sl = sl[:lead] + sl
     data = head + b"".join(sl)
     f = tmp_path / "tiled.264"
     f.write_bytes(data)
     assert b"roundtrip succeeded" in oracle_cli("roundtrip", f, mode="C")
     blocks = [b["cabac"] for b in avr.describe_container(oracle_cli("compress", f, mode="C"))[0]["blocks"] if "cabac" in b]
-    assert len(blocks) == len(sl) == 40
+    assert len(blocks) == len(sl) == 40 + lead
     whole_r = [b["cabac"] for b in avr.describe_container(oracle_cli("compress", f, mode="R"))[0]["blocks"] if "cabac" in b]
     assert blocks[:16] == whole_r[:16] and blocks[16:] != whole_r[16:]
     for j in range(0, len(sl), 16):
