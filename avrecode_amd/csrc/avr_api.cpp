@@ -336,10 +336,11 @@ constexpr int kRModeFallback = 1;
 // Does the parallel reference-model compress beat one workgroup per file on this plan?  Its time is
 // its largest slice's: the scan twice (count, write) and the recoded coder, one after the other;
 // the sequential kernel's is its largest file's, with walker, modeler and coder overlapped on three
-// waves.  Measured per payload byte of the chain (profiles/r05_rmode_files_trace.txt: a 4K 4:4:4
-// slice of 1.38 MB, scan 1.8 s per pass, coder ~1.5 s per MB; the sequential compress of its
-// 2-slice file 1.4 s per MB): the parallel pass pays when the largest file's payload exceeds ~3.7
-// times the largest slice's (cockatoo.mp4: 280 slices; a 1-2-slice-per-picture 4K file does not).
+// waves.  Measured per payload byte of the chain (profiles/r05_rcode_ab.txt and
+// r05m_rmode_files_before.log: a 4K 4:4:4 slice of 1.38 MB, scan 1.3-1.8 s per pass, coder ~1.5 s
+// per MB; the per-file kernel's compress of a 2-slice such file 1.4 s per MB): the parallel pass
+// pays when the largest file's payload exceeds ~3.7 times the largest slice's (cockatoo.mp4: 280
+// slices; a 1-2-slice-per-picture 4K file does not).
 // AVR_RMODE_PARALLEL=1 forces the parallel pass (tests), AVR_RMODE_SEQUENTIAL=1 the sequential kernel.
 bool rmode_parallel_pays(const Plan& plan) {
   if (getenv("AVR_RMODE_PARALLEL")) return true;
