@@ -616,6 +616,14 @@ long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int ch
   return idx;
 }
 
+/* the chained model's chain length: AVR_CHAIN_SLICES; AVR_ORACLE_CHAIN=k overrides it on both sides
+ * (experiment only: scripts/chain_experiment.py; such containers still carry the R16 tag) */
+static size_t chain_slices(void) {
+  const char *e = getenv("AVR_ORACLE_CHAIN");
+  const long k = e ? atol(e) : 0;
+  return k > 0 ? (size_t)k : (size_t)AVR_CHAIN_SLICES;
+}
+
 /* ========================================================================== compress */
 int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t *out_len) {
   avr_nal_t *nals;
@@ -657,7 +665,7 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
       lit.literal_len = gap;
       avr_pb_put_block(&o, &lit);
       prev_end += gap + s.size;
-      if (mode == AVR_MODE_C && chain_n > 0 && chain_n % AVR_CHAIN_SLICES == 0) {   /* a new chain */
+      if (mode == AVR_MODE_C && chain_n > 0 && chain_n % chain_slices() == 0) {   /* a new chain */
         size_t unused[8] = {0};
         avr_model_bills(model, avr_last_bill, unused);
         avr_model_free(model);
@@ -777,7 +785,7 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
     avr_pb_block_t *b = &blocks[next_coded];
     if ((size_t)b->size != s.size) { ret = -7; free(s.rbsp); break; }
     if (b->has_cabac) {
-      if (mode == AVR_MODE_C && chain_n > 0 && chain_n % AVR_CHAIN_SLICES == 0) {   /* a new chain */
+      if (mode == AVR_MODE_C && chain_n > 0 && chain_n % chain_slices() == 0) {   /* a new chain */
         avr_model_bills(model, unused_bill, avr_last_cabac_bill);
         avr_model_free(model);
         model = avr_model_new();

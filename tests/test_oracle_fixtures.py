@@ -94,3 +94,23 @@ def test_chained_model_is_the_reference_model_per_chain(tmp_path, lead):
         g.write_bytes(head + b"".join(sl[j:j + 16]))
         sub = [b["cabac"] for b in avr.describe_container(oracle_cli("compress", g, mode="R"))[0]["blocks"] if "cabac" in b]
         assert blocks[j:j + 16] == sub, j
+
+
+@pytest.mark.parametrize("name", ["realshort.mp4", "paff_ipp.264"])
+def test_chained_family_ends_are_the_parallel_and_reference_models(tmp_path, name):
+    """Chains of one coded slice are the parallel model (a fresh model per slice), one chain over the
+    whole file is the reference model: the chained format sits between the two, and its re-coded
+    blocks equal theirs at both ends (AVR_ORACLE_CHAIN overrides the chain length of 16, oracle only)."""
+    import os
+    import avrecode_amd as avr
+    _, cli = build_oracle()
+
+    def blocks(mode, k=None):
+        o = tmp_path / f"{mode}{k}.avrc"
+        env = dict(os.environ, **({"AVR_ORACLE_CHAIN": str(k)} if k else {}))
+        flag = {"R": [], "P": ["-p"], "C": ["-c"]}[mode]
+        subprocess.run([str(cli), "compress"] + flag + [str(FIX / name), str(o)], check=True, env=env)
+        return [b["cabac"] for b in avr.describe_container(o.read_bytes())[0]["blocks"] if "cabac" in b]
+
+    assert blocks("C", 1) == blocks("P")
+    assert blocks("C", 1 << 30) == blocks("R")
