@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = (
     "avr_hook_get_bypass", "avr_hook_get_terminate", "avr_hook_skip_bytes", "avr_hook_frame_spec", "avr_hook_mb_xy",
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
     "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables", "avr_last_phase_times",
-    "avr_plan_decompress", "avr_splice_container", "avr_roundtrip_files",
+    "avr_plan_decompress", "avr_splice_container", "avr_roundtrip_files", "avr_slice_kernel",
 )
 
 # avr_slice_desc / avr_slice_result (include/avrecode.h), C layout
@@ -177,6 +177,7 @@ def lib() -> ctypes.CDLL:
     L.avr_roundtrip_slices.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, i32, vp]
     L.avr_derive_decompress_descs.argtypes = [vp, vp, vp, i32, vp, vp]
     L.avr_verify_slices.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
+    L.avr_slice_kernel.argtypes = [vp, i32, i32, i32, ctypes.POINTER(ctypes.c_int)]
     L.avr_pack_outputs.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
     L.avr_parse_stream.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
     L.avr_parse_stream_range.argtypes = [vp, sz, i32, i32, pp, pi, pp, psz, psz, pi, pi]
@@ -642,6 +643,16 @@ class Context:
         P = self._ptr
         self._check(lib().avr_verify_slices(self._h, P(d_desc), P(d_res_c), P(d_res_d), n, P(d_in), P(d_regen),
                                             P(d_verdict), self._stream(stream)), "verify_slices")
+
+    def slice_kernel(self, n: int, max_mb_width: int, decompress: bool, p32: bool = False) -> str:
+        """The kernel a parallel-model batch of n slices runs (avr_slice_kernel), named as rocprofv3
+        reports it: slices_parallel_kernel (resident) or slices_queue_kernel (persistent queue),
+        template <MODE, FLD = false, P32>."""
+        k = ctypes.c_int(-1)
+        self._check(lib().avr_slice_kernel(self._h, 1 if decompress else 0, n, max_mb_width, ctypes.byref(k)),
+                    "slice_kernel")
+        name = ("slices_parallel_kernel", "slices_queue_kernel")[k.value]
+        return f"{name}<{1 if decompress else 0}, false, {'true' if p32 else 'false'}>"
 
     def pack_outputs(self, d_desc, d_res, n, d_out, d_packed, d_offsets, stream=None):
         P = self._ptr

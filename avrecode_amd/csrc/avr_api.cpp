@@ -632,6 +632,14 @@ std::vector<SliceView> views_of(const ParsedFile& pf) {
   return v;
 }
 
+// Host threads for one file's bulk steps (trigram index, container copies): up to 16, or 1 inside a
+// parallel_files worker, which already spreads the files over the thread budget (a corpus of large
+// files would otherwise start ~16 x 16 threads at once).
+thread_local bool tl_in_file_pool = false;
+unsigned bulk_threads() {
+  return tl_in_file_pool ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
 // Every 00 00 0y trigram (y <= 3) of a file, keyed by y and the four bytes after it, then by
 // position.  In an escaped H.264 stream these occur only at start codes, emulation-prevention bytes
 // (00 00 03) and container bytes (MP4 lengths and boxes), so the index is small.
@@ -643,6 +651,15 @@ struct TrigramIndex {
     bool operator<(const Entry& o) const { return key != o.key ? key < o.key : pos < o.pos; }
   };
   std::vector<Entry> e;
+  // per y, every trigram position in ascending order: the lookups whose payload holds no four bytes
+  // after its trigram (built at the first such lookup)
+  bool pos_built = false;
+  std::vector<uint64_t> pos[4];
+  void build_pos() {
+    pos_built = true;
+    for (const Entry& x : e) pos[x.key >> 32].push_back(x.pos);
+    for (auto& v : pos) std::sort(v.begin(), v.end());
+  }
   static uint64_t key_at(const uint8_t* f, size_t n, size_t p) {   // trigram at p (p + 2 < n)
     uint32_t nx = 0;
     for (int k = 0; k < 4; k++) nx = nx << 8 | (p + 3 + k < n ? f[p + 3 + k] : 0u);
@@ -661,7 +678,7 @@ struct TrigramIndex {
   void build(const uint8_t* f, size_t n) {
     built = true;
     // a multi-GB file is scanned in chunks on host threads
-    const unsigned T = n < ((size_t)256 << 20) ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const unsigned T = n < ((size_t)256 << 20) ? 1u : bulk_threads();
     std::vector<std::vector<Entry>> part(T);
     std::vector<std::thread> th;
     for (unsigned t = 1; t < T; t++) th.emplace_back(scan, f, n, n * t / T, n * (t + 1) / T, &part[t]);
@@ -701,32 +718,30 @@ const uint8_t* find_payload(const uint8_t* in, size_t n, size_t from, const uint
     if (getenv("AVR_ASM_TIMING")) fprintf(stderr, "index build %.3f s, %zu entries\n", now_s() - tb, ix->e.size());
   }
   using E = TrigramIndex::Entry;
-  const bool keyed = j + 7 <= m;   // P holds the four bytes after its trigram
-  const uint64_t key = keyed ? TrigramIndex::key_at(P, m, j) : (uint64_t)P[j + 2] << 32;
-  const uint64_t key_end = keyed ? key : key + ((uint64_t)1 << 32) - 1;
+  if (j + 7 > m) {
+    // the trigram lies in P's last six bytes: no key beyond y; y's positions from from + j on, in
+    // ascending order -- the first that matches is memmem's answer
+    if (!ix->pos_built) ix->build_pos();
+    const std::vector<uint64_t>& ps = ix->pos[P[j + 2]];
+    for (auto it = std::lower_bound(ps.begin(), ps.end(), (uint64_t)(from + j)); it != ps.end(); ++it) {
+      const size_t q = (size_t)*it - j;
+      if (q + m > n) break;
+      if (memcmp(in + q, P, m) == 0) return in + q;
+    }
+    return nullptr;
+  }
+  const uint64_t key = TrigramIndex::key_at(P, m, j);   // P holds the four bytes after its trigram
   for (auto it = std::lower_bound(ix->e.begin(), ix->e.end(), E{key, (uint64_t)(from + j)}); it != ix->e.end(); ++it) {
-    if (it->key > key_end) break;
-    if (!keyed && it->pos < from + j) continue;   // entries of another next-four-bytes key, earlier positions
+    if (it->key != key) break;
     const size_t q = (size_t)it->pos - j;
-    if (q + m > n) {
-      if (keyed) break;
-      continue;
-    }
-    if (memcmp(in + q, P, m) == 0) {
-      if (keyed) return in + q;
-      // the y-only range is sorted by key, not position: keep the smallest match
-      const uint8_t* best = in + q;
-      for (++it; it != ix->e.end() && it->key <= key_end; ++it) {
-        const size_t q2 = (size_t)it->pos - j;
-        if (it->pos >= from + j && q2 + m <= n && in + q2 < best && memcmp(in + q2, P, m) == 0) best = in + q2;
-      }
-      return best;
-    }
+    if (q + m > n) break;
+    if (memcmp(in + q, P, m) == 0) return in + q;
   }
   return nullptr;
 }
 
-// memmem(in + from, n - from, P, m) for a payload the parse found verbatim at `own` >= from: memmem's
+// memmem(in + from, n - from, P, m) for a payload that stands verbatim at `own` >= from (segment
+// checks it): memmem's
 // answer is the first occurrence at or after `from` and `own` is one, so only [from, own) -- the
 // literal gap before the slice: start code or length, NAL and slice header, skipped NAL units --
 // needs a search.  Candidates are the gap's bytes equal to P[0] (memchr), each checked on its first
@@ -759,11 +774,37 @@ std::vector<const uint8_t*> segment(const uint8_t* in, size_t n, const std::vect
                                     const std::vector<char>& ok) {
   std::vector<const uint8_t*> found(sv.size(), nullptr);
   TrigramIndex ix;
+  // a recorded position is trusted only where the payload's bytes stand there (a payload that is a
+  // view of the file at that position trivially; a copy -- rank 0's parse arena, another revision
+  // of the file -- compared in full, on host threads); else the plain search
+  std::vector<char> own_ok(sv.size(), 0);
+  {
+    std::vector<size_t> chk;
+    for (size_t i = 0; i < sv.size(); i++) {
+      const uint64_t own = sv[i].file_pos;
+      if (!ok[i] || sv[i].size < (size_t)avr::kSurrogateMarkerBytes || own == ~(uint64_t)0 || own + sv[i].size > n) continue;
+      if (sv[i].payload == in + own) own_ok[i] = 1;
+      else chk.push_back(i);
+    }
+    uint64_t bytes = 0;
+    for (size_t i : chk) bytes += sv[i].size;
+    const unsigned T = bytes < ((uint64_t)64 << 20) ? 1u : bulk_threads();
+    auto work = [&](unsigned t) {
+      for (size_t k = t; k < chk.size(); k += T) {
+        const size_t i = chk[k];
+        own_ok[i] = memcmp(in + sv[i].file_pos, sv[i].payload, sv[i].size) == 0;
+      }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; t++) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+  }
   size_t prev_end = 0;
   for (size_t i = 0; i < sv.size(); i++) {
     if (!ok[i] || sv[i].size < (size_t)avr::kSurrogateMarkerBytes) continue;
     const uint64_t own = sv[i].file_pos;
-    const uint8_t* f = own != ~(uint64_t)0 && own >= prev_end && own + sv[i].size <= n
+    const uint8_t* f = own_ok[i] && own >= prev_end
                            ? find_before(in, prev_end, (size_t)own, sv[i].payload, sv[i].size)
                            : find_payload(in, n, prev_end, sv[i].payload, sv[i].size, &ix);
     if (f) {
@@ -799,8 +840,7 @@ void copy_part(uint8_t* dst, const uint8_t* src, size_t len, uint8_t fill) {
 void parallel_copies(const std::vector<avr::PbCopy>& jobs, uint8_t* base, uint8_t fill = 0) {
   uint64_t total = 0;
   for (const auto& j : jobs) total += j.len;
-  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  const unsigned T = total < ((uint64_t)64 << 20) ? 1u : hw;
+  const unsigned T = total < ((uint64_t)64 << 20) ? 1u : bulk_threads();
   if (T == 1) {
     for (const auto& j : jobs) copy_part(base + j.dst, j.src, j.len, fill);
     return;
@@ -836,6 +876,8 @@ void parallel_files(int nf, F&& fn) {
   std::exception_ptr err;
   std::mutex mu;
   auto work = [&]() {
+    const bool was = tl_in_file_pool;
+    tl_in_file_pool = true;   // each file's own bulk steps stay on this thread
     try {
       for (int f; (f = next.fetch_add(1)) < nf;) fn(f);
     } catch (...) {
@@ -843,6 +885,7 @@ void parallel_files(int nf, F&& fn) {
       if (!err) err = std::current_exception();
       next = nf;
     }
+    tl_in_file_pool = was;
   };
   std::vector<std::thread> th;
   for (unsigned t = 1; t < T; t++) th.emplace_back(work);
@@ -1978,6 +2021,13 @@ int avr_verify_slices(avr_ctx* c, const avr_slice_desc* d_desc, const avr_slice_
     return AVR_ERR_INVALID_ARGUMENT;
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, avr::launch_verify(d_desc, d_res_c, d_res_d, n, d_in, d_regen, d_verdict, (hipStream_t)stream));
+  return AVR_OK;
+}
+
+int avr_slice_kernel(avr_ctx* c, int decompress, int n, int max_mb_width, int* kind) {
+  if (!c || !kind || n < 0 || max_mb_width <= 0) return AVR_ERR_INVALID_ARGUMENT;
+  HIP_TRY(c, hipSetDevice(c->device));
+  *kind = avr::parallel_kernel_kind(decompress ? 1 : 0, n, max_mb_width);
   return AVR_OK;
 }
 

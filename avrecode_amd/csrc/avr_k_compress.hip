@@ -11,7 +11,7 @@ hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc*
 
 // AVR_PROFILE builds: read (and clear) this kernel's section cycle counters; zeros otherwise.
 hipError_t profile_parallel_compress(unsigned long long* out16) {
-#ifdef AVR_PROFILE
+#if defined(AVR_PROFILE) || defined(AVR_WATCHDOG)
   hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(avr_prof), sizeof(unsigned long long) * 64);
   unsigned long long z[64] = {};
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(avr_prof), z, sizeof(z));
@@ -34,3 +34,18 @@ hipError_t placement_parallel_compress(uint32_t* out, int n) {
 }
 
 }  // namespace avr
+
+#ifdef AVR_QTRACE
+// Queue trace builds: host-mapped coherent memory for the compress kernel's progress records (8
+// u32 per workgroup, avr_walker.h QTRACE), returned to the caller; nwg workgroups at most.
+extern "C" int avr_debug_qtrace(uint32_t** host, int nwg) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, (size_t)nwg * 32, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return -2;
+  for (size_t i = 0; i < (size_t)nwg * 8; i++) ((uint32_t*)p)[i] = 0;
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) return -2;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(avr::avr_qtrace), &dp, sizeof(dp)) != hipSuccess) return -2;
+  *host = (uint32_t*)p;
+  return 0;
+}
+#endif

@@ -18,7 +18,7 @@ hipError_t launch_sequential_decompress(const EngineTables* T, const avr_slice_d
 
 // AVR_PROFILE builds: read (and clear) this kernel's section cycle counters; zeros otherwise.
 hipError_t profile_sequential_decompress(unsigned long long* out16) {
-#ifdef AVR_PROFILE
+#if defined(AVR_PROFILE) || defined(AVR_WATCHDOG)
   hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(avr_prof), sizeof(unsigned long long) * 64);
   unsigned long long z[64] = {};
   if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(avr_prof), z, sizeof(z));

@@ -69,6 +69,7 @@ size_t queue_scratch_bytes(int n);
 int slots_per_cu(size_t lds);
 int resident_slices(size_t lds);
 int est_slots(int n, int max_mb_width);
+int parallel_kernel_kind(int mode, int n, int max_mb_width);
 // one per kernel translation unit (avr_k_*.hip); lds = shared_bytes(max_mb_width)
 hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,

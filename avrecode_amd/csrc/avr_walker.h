@@ -52,8 +52,13 @@
 
 namespace avr {
 
-#ifdef AVR_PROFILE
+#if defined(AVR_PROFILE) && defined(AVR_WATCHDOG)
+#error "AVR_WATCHDOG records share avr_prof with the AVR_PROFILE section counters: build one at a time"
+#endif
+#if defined(AVR_PROFILE) || defined(AVR_WATCHDOG)
 static __device__ unsigned long long avr_prof[64];
+#endif
+#ifdef AVR_PROFILE
 // wave placement per slice (AVR_PROFILE builds): HW_ID of waves 0..2, XCC_ID, walker start / end
 // (s_memtime low 32 bits), walker start / end (s_memrealtime, 100 MHz) -- scripts/placement.py
 constexpr int kPlaceSlices = 4096;
@@ -173,6 +178,12 @@ struct Shared {
   uint32_t elog_n;           // entries appended to the HBM table's write log by this model
   uint32_t prio;             // the slice's current wave priority (walker -> modeler / coder)
   uint32_t qnext;            // persistent launches: the queue entry this workgroup drew
+#if defined(AVR_QUEUE_EAGER) && AVR_QUEUE_EAGER == 1
+  uint32_t qcell;            // experiment build: the walker's board cell, set before the first draw
+#endif
+#ifdef AVR_WATCHDOG
+  uint32_t wd_epoch[4];      // watchdog build: barrier checkpoints passed, per wave
+#endif
   uint32_t c_len, c_last;
   uint32_t bill[6];          // the coder's h264_model billing by CodingType (kFlagBill launches)
   uint32_t blk[64];       // residual blocks of the current macroblock (packed, see push_block)
@@ -243,6 +254,66 @@ AVR_FI uint32_t op_level(int cat, int absl, int sign) {
 AVR_FI uint32_t op_mvd(int comp, int inc, int amvd, int sign) {
   return OPK_MACRO << 1 | 2u << 3 | (uint32_t)comp << 5 | (uint32_t)inc << 6 | (uint32_t)sign << 8 | (uint32_t)amvd << 9;
 }
+// Watchdog build (-DAVR_WATCHDOG, diagnostics only): every wait of a slice workgroup is bounded in
+// time, and the kernels check their own invariants.  A wait that lasts kWdTicks records where it
+// was (site, workgroup, wave, the counters it waited on, the queue entry, HW_ID) in avr_prof and
+// ends its wave, so a workgroup that would hang drains instead and the host reads the records
+// (avr_debug_profile).  Layout of avr_prof: [0] records written, [1 + 3 i .. 3 + 3 i] record i
+// (i < 16), [50] invariant violations, [51..53] the first one's record.  Sites: 1-4 ring waits
+// (push, push_v, take, modeler -> coder room); 10 board cell out of range; 11 ring overfilled;
+// 12 queue entries drawn out of order; 13 waves of a workgroup at different barriers.
+enum { WD_PUSH = 1, WD_PUSHV = 2, WD_TAKE = 3, WD_ROOM1 = 4, WD_CELL = 10, WD_RING = 11, WD_QORDER = 12,
+       WD_EPOCH = 13 };
+#ifdef AVR_WATCHDOG
+constexpr uint64_t kWdTicks = 300000000ull;   // s_memrealtime runs at 100 MHz: 3 s
+AVR_FI void wd_put(unsigned long long* rec, uint32_t site, uint32_t a, uint32_t b, uint32_t k) {
+  rec[0] = (unsigned long long)site << 48 | (unsigned long long)(threadIdx.x >> 6) << 40 | blockIdx.x;
+  rec[1] = (unsigned long long)a << 32 | b;
+  rec[2] = (unsigned long long)k << 32 | __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_REG_HW_ID
+}
+AVR_FI void wd_violation(uint32_t site, uint32_t a, uint32_t b, uint32_t k) {
+  if (__lane_id() != 0) return;
+  if (atomicAdd(&avr_prof[50], 1ull) == 0) wd_put(&avr_prof[51], site, a, b, k);
+  __threadfence();
+}
+// One poll of a wait that started at *t0 (0: not yet): past kWdTicks, record and end the wave.
+AVR_FI void wd_poll(uint64_t* t0, uint32_t site, uint32_t a, uint32_t b, uint32_t k) {
+  const uint64_t t = __builtin_amdgcn_s_memrealtime();
+  if (*t0 == 0) { *t0 = t; return; }
+  if (t - *t0 < kWdTicks) return;
+  if (__lane_id() == 0) {
+    const unsigned long long i = atomicAdd(&avr_prof[0], 1ull);
+    if (i < 16) wd_put(&avr_prof[1 + 3 * i], site, a, b, k);
+    __threadfence();
+  }
+  __builtin_amdgcn_endpgm();
+}
+#define WD_T0 uint64_t wd_t0 = 0
+#define WD_POLL(site, a, b, k) wd_poll(&wd_t0, site, a, b, k)
+#define WD_CHECK(cond, site, a, b, k) do { if (!(cond)) wd_violation(site, a, b, k); } while (0)
+#else
+#define WD_T0
+#define WD_POLL(site, a, b, k)
+#define WD_CHECK(cond, site, a, b, k)
+#endif
+
+// Queue trace build (-DAVR_QTRACE, diagnostics only): each workgroup of a persistent launch writes
+// its progress to host-mapped coherent memory (avr_debug_qtrace, compress kernel only), so the
+// host can read where every workgroup and wave is while a launch has not returned.  Per
+// workgroup 8 u32: [0..2] wave w's (slices drawn << 8 | phase), [3] the queue entry drawn, [4]
+// the walker's macroblocks of the current slice.  Phases: 1 drawn, 2 estimator table reset,
+// 3 slice state set up, 4 the wave's role done, 5 slice finished, 6 left the loop.
+#ifdef AVR_QTRACE
+static __device__ uint32_t* avr_qtrace;
+AVR_FI void qtrace(uint32_t slot, uint32_t v) {
+  uint32_t* t = avr_qtrace;
+  if (t && __lane_id() == 0) __hip_atomic_store(&t[blockIdx.x * 8 + slot], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define QTRACE(slot, v) qtrace(slot, v)
+#else
+#define QTRACE(slot, v)
+#endif
+
 // Ring counters: plain LDS accesses.  LDS is one memory per CU and executes each wave's accesses
 // in program order, so a counter store issued after the entry stores cannot be seen before them;
 // the asm statements only keep the compiler from reordering (an acquire/release fence would
@@ -401,9 +472,12 @@ struct RingOutT {
 #ifdef AVR_PROFILE
       const uint64_t tw = PROF_T();
 #endif
+      WD_T0;
       for (;;) {
         const uint32_t used = head - ld_volatile(&sh->fifo_tail[r]);
+        WD_CHECK(used <= (uint32_t)kFifo, WD_RING, head, used, (uint32_t)r);
         if (used < (uint32_t)kFifo) { room = kFifo - used; break; }
+        WD_POLL(WD_PUSH, head, used, sh->qnext);
         __builtin_amdgcn_s_sleep(1);
       }
 #ifdef AVR_PROFILE
@@ -422,9 +496,12 @@ struct RingOutT {
 #ifdef AVR_PROFILE
       const uint64_t tw = PROF_T();
 #endif
+      WD_T0;
       for (;;) {
         const uint32_t used = head - ld_volatile(&sh->fifo_tail[r]);
+        WD_CHECK(used <= (uint32_t)kFifo, WD_RING, head, used, (uint32_t)r);
         if (used + n <= (uint32_t)kFifo) { room = kFifo - used; break; }
+        WD_POLL(WD_PUSHV, head, used, sh->qnext);
         __builtin_amdgcn_s_sleep(1);
       }
 #ifdef AVR_PROFILE
@@ -444,11 +521,14 @@ AVR_FI uint32_t ring_take(Shared* sh, int r, uint32_t tail, uint32_t* op_v, uint
 #ifdef AVR_PROFILE
   const uint64_t tw = PROF_T();
 #endif
+  WD_T0;
   for (;;) {
     head = ld_volatile(&sh->fifo_head[r]);
     if (head != tail) break;
+    WD_POLL(WD_TAKE, head, tail, sh->qnext);
     __builtin_amdgcn_s_sleep(1);
   }
+  WD_CHECK(head - tail <= (uint32_t)kFifo, WD_RING, head, tail, (uint32_t)r | 0x100u);
 #ifdef AVR_PROFILE
   *waited += PROF_T() - tw;
 #endif
@@ -2164,6 +2244,7 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
     if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) {
       w.publish();
       if (!RM) w.update_prio();
+      QTRACE(4, (uint32_t)w.mbs_done);
     }
     // MBAFF: end_of_slice_flag follows the bottom macroblock of a pair only (7.3.4)
     const int eos = (!(FLD && w.mbaff) || (w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
@@ -2408,9 +2489,11 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
 #ifdef AVR_PROFILE
       const uint64_t tw = PROF_T();
 #endif
+      WD_T0;
       for (;;) {
         tail1 = ld_volatile(&sh->fifo_tail[1]);
         if (head1 + n - tail1 <= (uint32_t)kFifo) break;
+        WD_POLL(WD_ROOM1, head1, tail1, sh->qnext);
         __builtin_amdgcn_s_sleep(1);
       }
 #ifdef AVR_PROFILE
@@ -2757,7 +2840,8 @@ constexpr int slice_threads() {
 // launch uses); the resident kernel's row is always in LDS (a constant: no branch at its accesses).
 template <int MODE, bool FLD, bool P32, bool MG>
 AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice_desc* descs, int s, const uint8_t* in,
-                           uint8_t* out, avr_slice_result* res, uint16_t* est_g, uint32_t flags, uint32_t cell) {
+                           uint8_t* out, avr_slice_result* res, uint16_t* est_g, uint32_t flags, uint32_t cell,
+                           uint32_t qiter = 0) {
   const avr_slice_desc* d = &descs[s];
   Walker<MODE, false, FLD, P32> w;
   w.sh = (Shared*)smem;
@@ -2788,10 +2872,12 @@ AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice
   }
   // fresh model for this slice: undo the last model's stores to the HBM estimator table
   if (MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) est_table_reset(w.est_g, w.sh);
+  if (MG) QTRACE(threadIdx.x >> 6, qiter << 8 | 2);
   w.d = d;
   w.W = d->mb_width;
   if ((MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x == 0) w.sh->prio = 0;   // before init_slice_state's barrier
   init_slice_state(w, G);
+  if (MG) QTRACE(threadIdx.x >> 6, qiter << 8 | 3);
   if (MODE == MODE_GENERATE || MODE == MODE_TRACE) {
     run_slice_inline(w, d, in, out, &res[s]);
     return;
@@ -2805,7 +2891,9 @@ AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice
   }
   else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
   else coder_slice<MODE, P32>(w.sh, w.T, d, out, flags);
+  if (MG) QTRACE(wave, qiter << 8 | 4);
   __syncthreads();
+  if (MG) QTRACE(wave, qiter << 8 | 5);
   if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
 }
 
@@ -2852,10 +2940,35 @@ __global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables
   // (r05c/r05e probes), this order does not (r05d).
   uint32_t cell = kNoCell;
   bool loaded = false;
+  uint32_t qiter = 0;   // slices this workgroup drew (queue trace builds)
+#ifdef AVR_WATCHDOG
+  if ((threadIdx.x & 63) == 0) sh->wd_epoch[threadIdx.x >> 6] = 0;
+  uint32_t wd_prev_k = 0xffffffffu;
+#endif
+#ifdef AVR_QUEUE_EAGER   // experiment builds: the round-5 order that hung (r05c: 1, r05e: 2)
+  load_hot_tables(sh, G);
+  loaded = true;
+  if ((MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x < 64) {
+    cell = cu_cell();
+#if AVR_QUEUE_EAGER == 1
+    if (__lane_id() == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->qcell = cell;
+#endif
+  }
+#endif
   for (;;) {
     if (threadIdx.x == 0) *(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext = atomicAdd(qhead, 1u);
+#ifdef AVR_WATCHDOG
+    if ((threadIdx.x & 63) == 0) sh->wd_epoch[threadIdx.x >> 6]++;
+#endif
     __syncthreads();
     const uint32_t k = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->qnext);
+#ifdef AVR_WATCHDOG
+    if (threadIdx.x == 0)
+      for (uint32_t v = 1; v < blockDim.x / 64; v++)
+        WD_CHECK(sh->wd_epoch[v] == sh->wd_epoch[0], WD_EPOCH, sh->wd_epoch[0], sh->wd_epoch[v], k);
+    WD_CHECK(wd_prev_k == 0xffffffffu || k > wd_prev_k, WD_QORDER, wd_prev_k, k, k);
+    wd_prev_k = k;
+#endif
     __syncthreads();   // every thread has its entry before thread 0 draws again
     if (k >= (uint32_t)n) break;
     const int s = queue[k];
@@ -2865,9 +2978,19 @@ __global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables
       loaded = true;
       if ((MODE == MODE_COMPRESS || MODE == MODE_DECOMPRESS) && threadIdx.x < 64) cell = cu_cell();
     }
+#if defined(AVR_QUEUE_EAGER) && AVR_QUEUE_EAGER == 1
+    cell = __builtin_amdgcn_readfirstlane(*(volatile __attribute__((address_space(3))) uint32_t*)&sh->qcell);
+#endif
+    WD_CHECK(cell == kNoCell || cell < 4u * kCuIds, WD_CELL, cell, threadIdx.x, k);
+#ifdef AVR_QTRACE
+    qiter++;
+    if (threadIdx.x == 0) QTRACE(3, k);
+    QTRACE(threadIdx.x >> 6, qiter << 8 | 1);
+#endif
     parallel_slice<MODE, FLD, P32, true>(smem, G, descs, s, in, out, res, est_scratch + (size_t)blockIdx.x * kEstGlobal,
-                                         flags, cell);
+                                         flags, cell, qiter);
   }
+  QTRACE(threadIdx.x >> 6, qiter << 8 | 6);
 }
 
 // Host side of the parallel launches (instantiated in each kernel TU, avr_k_*.hip, with that TU's

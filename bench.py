@@ -52,9 +52,6 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, /opt/skills/guides/MI355X_MICROAR
 QPS = (22, 26, 30)
 METRIC = "input H.264 MB/s (compress+roundtrip) at 1/2/4/8 GPUs; bit-exact pass"
 WORKLOAD = "synthetic batch of independent 1080p CABAC I-slices (BASELINE configs[2])"
-# the progressive-slice kernels of the u64 coder (template <MODE, FLD, P32>), as rocprofv3 names them
-KERNEL_NAMES = {"compress": "slices_parallel_kernel<0, false, false>",
-                "decompress": "slices_parallel_kernel<1, false, false>"}
 
 
 def progress(msg):
@@ -572,7 +569,9 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     t_dec = sum(e[2].elapsed_time(e[3]) for e in evs) / len(evs) / 1e3
     S = int(part.descs["payload_size"].sum())
     dominant, t_dom = ("compress", t_comp) if t_comp >= t_dec else ("decompress", t_dec)
-    kernel_name = KERNEL_NAMES[dominant]
+    # the kernel this rank's launches ran (a 4K range of thousands of slices: the persistent queue)
+    kernel_name = ctx.slice_kernel(drange.n if dominant == "decompress" else n_mine, part.max_mb_width,
+                                   dominant == "decompress")
     rec = {
         "metric": METRIC, "value": len(data) * args.stream_steps / float(t[0]) / 1e6, "unit": "MB/s",
         "n_gpus": world, "steps": args.stream_steps, "warmup": args.warmup,
@@ -591,7 +590,8 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
                    "setup_by_rank": setup_by_rank,
                    "step_phases_s_rank0": {k: round(v / args.stream_steps, 3) for k, v in phases.items()}},
         "roofline": {"bound": "hbm", "kernel": kernel_name, "achieved": (S + C) / t_dom / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": (S + C) / t_dom / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": (S + C) / t_dom / 1e9 / HBM_PEAK_GBS,
+                     "traffic": load_stream_traffic(args, seconds, world, kernel_name),
                      "note": "rank 0's slice range: S + C per launch over the kernel's average HIP-event time"},
         "cpu_baseline": None,
     }
@@ -714,6 +714,37 @@ def _init_dist(world, dev):
         dist.init_process_group(_backend(), rank=0, world_size=1, **kw)
 
 
+GOLDEN_BATCH = ROOT / "tests" / "golden" / "bench_batch.json"
+
+
+def golden_check(batch, data, args):
+    """The headline batch against the oracle's answer for it, slice by slice (tests/golden/
+    bench_batch.json, tests/golden/make_bench_golden.py: the oracle run on every slice of this
+    exact batch): the CABAC bins each slice's parse decoded and the SHA-256 of its re-coded bytes.
+    The regeneration verdicts alone do not pin the parse (a walker that parses a different bin
+    sequence still round-trips); this does.  None when the batch is not the golden's
+    configuration (another seed, size or rank)."""
+    import hashlib
+    if not GOLDEN_BATCH.exists():
+        return None
+    g = json.loads(GOLDEN_BATCH.read_text())
+    c = g["config"]
+    if c["slices"] != args.slices or c["mb"] != [args.mb_width, args.mb_height] or c["seed"] != args.seed:
+        return None
+    rec = {"golden": str(GOLDEN_BATCH.relative_to(ROOT)), "slices": len(g["slices"])}
+    if hashlib.sha256(data).hexdigest() != g["stream_sha256"]:
+        return rec | {"match": None, "note": "the generator's stream differs from the golden's: regenerate it"}
+    res = batch.results("c")
+    recoded = batch.recoded()
+    bins_bad = [k for k, s in enumerate(g["slices"]) if int(res["bins"][k]) != s["bins"]]
+    sha_bad = [k for k, s in enumerate(g["slices"])
+               if len(recoded[k]) != s["recoded_len"] or hashlib.sha256(recoded[k]).hexdigest() != s["recoded_sha256"]]
+    return rec | {"bins_total": int(res["bins"].sum()), "bins_total_oracle": g["bins_total"],
+                  "recoded_total": sum(map(len, recoded)), "recoded_total_oracle": g["recoded_total"],
+                  "slices_bins_differ": len(bins_bad), "slices_recoded_differ": len(sha_bad),
+                  "match": not bins_bad and not sha_bad}
+
+
 def load_traffic(args, kernel):
     """HBM bytes per launch of `kernel` from profiles/<round>_pmc.json (scripts/pmc_traffic.py),
     only when that profile was taken on this batch shape AND on this build of the native sources
@@ -724,7 +755,29 @@ def load_traffic(args, kernel):
         return None
     try:
         j = json.loads(p.read_text())
-        if j.get("slices") != args.slices or j.get("mb") != [args.mb_width, args.mb_height]:
+        if j.get("leg", "headline") != "headline" or j.get("slices") != args.slices or \
+                j.get("mb") != [args.mb_width, args.mb_height]:
+            return None
+        if j.get("source_sha") != avr.source_sha():
+            progress(f"traffic: {p.name} is from another build of the sources; reporting null")
+            return None
+        return j["kernels"][kernel]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def load_stream_traffic(args, seconds, world, kernel):
+    """configs[3]'s kernel: HBM bytes per launch from profiles/<round>_stream_pmc.json
+    (scripts/pmc_traffic.py --leg stream_shard, passes over `bench.py --stream-shard` at N = 1), when
+    that profile is of this stream and this build of the sources and the leg runs on one GPU (at
+    N > 1 each rank's launch covers a different range); else None."""
+    import avrecode_amd as avr
+    p = ROOT / "profiles" / f"{args.round}_stream_pmc.json"
+    if world != 1 or not p.exists():
+        return None
+    try:
+        j = json.loads(p.read_text())
+        if j.get("leg") != "stream_shard" or j.get("seconds") != seconds or j.get("mb") != list(args.stream_mb):
             return None
         if j.get("source_sha") != avr.source_sha():
             progress(f"traffic: {p.name} is from another build of the sources; reporting null")
@@ -812,7 +865,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--round", default="r05")
+    ap.add_argument("--round", default="r06")
     ap.add_argument("--file-reps", type=int, default=3, help="timed reps of a whole-file call under 2 s")
     ap.add_argument("--no-files", action="store_true", help="skip the whole-file roundtrips")
     ap.add_argument("--no-clip", action="store_true", help="skip the configs[1] clip in the file roundtrips")
@@ -880,8 +933,11 @@ def main():
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
-    # the timed steps recomputed the same outputs: re-check them
+    # the timed steps recomputed the same outputs: re-check them, and against the oracle's answer
     bit_exact = bit_exact and bool((batch.verdicts() == 1).all())
+    gold = golden_check(batch, data, args) if rank == 0 else None
+    if gold is not None and gold.get("match") is False:
+        bit_exact = False
     t_comp = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps / 1e3
     t_dec = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps / 1e3
     # labelled extra, outside the headline's timed region: the same batch through the P32 coder
@@ -902,7 +958,7 @@ def main():
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         dominant, t_dom = ("compress", t_comp) if t_comp >= t_dec else ("decompress", t_dec)
-        kernel_name = KERNEL_NAMES[dominant]
+        kernel_name = ctx.slice_kernel(args.slices, ps.max_mb_width, dominant == "decompress")
         achieved = (S + C) / t_dom / 1e9
         line = {
             "metric": METRIC,
@@ -944,6 +1000,8 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if gold is not None:
+            line["oracle_parity"] = gold
         if p32 is not None:
             line["p32"] = p32
         progress(f"batch: {line['value']:.1f} MB/s")

@@ -237,6 +237,15 @@ int avr_verify_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, const avr_slic
                       const avr_slice_result* d_res_d, int n, const uint8_t* d_in, const uint8_t* d_regen,
                       int32_t* d_verdict, void* stream);
 
+/* Which device kernel a parallel-model batch of n slices (widest picture max_mb_width macroblocks)
+ * runs on this context's GPU, by the rule avr_compress_slices / avr_decompress_slices apply:
+ * *kind = 0 the resident kernel (slices_parallel_kernel: one workgroup per slice, the whole batch
+ * resident at once), 1 the persistent queue kernel (slices_queue_kernel: more slices than the chip
+ * holds at once, or pictures wide enough that their model row lives in global scratch).  For
+ * naming the measured kernel in profiles; no reference counterpart (the reference is one CPU
+ * thread). */
+int avr_slice_kernel(avr_ctx* ctx, int decompress, int n, int max_mb_width, int* kind);
+
 /* ------------------------------------------------------------ host-side slice extraction */
 /* What FFmpeg hands AVCodecHooks.cabac.init_decoder for every CABAC slice of a file
  * (av_decoder::decode_video, recode.cpp:73-135): demux (MP4/avcC or Annex-B), unescape, parse

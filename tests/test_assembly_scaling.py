@@ -46,7 +46,7 @@ def _escape(raw: bytes) -> bytes:
     return bytes(out)
 
 
-def _stream(n_slices: int, seed: int) -> bytes:
+def _stream(n_slices: int, seed: int, tail: bool = False) -> bytes:
     """A tiled Annex-B stream: the field fixture's parameter sets, then n_slices slices made from its
     first slice NAL with seeded bytes appended to the payload (kinds cycle: a run with 00 00 0y
     trigrams -> emulation-prevention bytes; the same, preceded by a filler NAL holding the slice's
@@ -58,7 +58,12 @@ def _stream(n_slices: int, seed: int) -> bytes:
     for i in range(n_slices):
         raw = bytearray(rng.integers(1, 256, size=int(rng.integers(3000, 9000)), dtype=np.uint8).tobytes())
         kind = i % 3
-        if kind in (0, 1):
+        if kind in (0, 1) and tail:
+            # the payload's only trigram in its last six bytes (no four bytes after it to key on)
+            at = len(raw) - int(rng.integers(2, 5))
+            raw[at:at + 3] = bytes([0, 0, int(rng.integers(2, 4))])
+            del raw[at + 3:]
+        elif kind in (0, 1):
             for _ in range(3):
                 at = int(rng.integers(16, len(raw) - 8))
                 raw[at:at + 3] = bytes([0, 0, int(rng.integers(2, 4)) if kind == 1 else int(rng.integers(0, 4))])
@@ -132,6 +137,43 @@ def test_segmentation_equals_reference_search():
     # the container restores the stream's layout (literals + coded sizes)
     desc, _ = avr.describe_container(a)
     assert sum(len(x.get("literal", "")) // 2 + (x["size"] if "cabac" in x else 0) for x in desc["blocks"]) == len(data)
+
+
+def test_segmentation_unkeyed_trigrams():
+    """Payloads whose only 00 00 0y trigram lies in their last six bytes (the index has no four
+    following bytes to key on: find_payload's by-position lists): memmem's answer, found in the
+    filler NAL or nowhere."""
+    data = _stream(60, seed=3, tail=True)
+    ps = avr.parse_stream(data)
+    a, ok = _assemble(data, ps, parsed=True)
+    exp = _expected_layout(data, ps, ok)
+    assert _layout_of(a) == exp
+    kinds = {("miss" if f is None else "filler" if k % 3 == 1 else "own") for k, f in enumerate(exp) if ok[k]}
+    assert kinds == {"miss", "filler", "own"}, kinds
+
+
+def test_parsed_assembly_checks_recorded_positions():
+    """avr_assemble_container_parsed takes rank 0's parse: each payload's recorded file position is
+    used only where the payload's bytes stand there.  An arena whose payload differs from the file
+    in its middle bytes (a stale parse, another revision of the file) gets memmem's answer for the
+    bytes it holds -- here: found nowhere, so the slice is a literal -- not a block at the recorded
+    position that would decompress to other bytes."""
+    import copy
+    data = _stream(60, seed=4)
+    ps = avr.parse_stream(data)
+    ps2 = copy.copy(ps)
+    ps2.arena = ps.arena.copy()
+    changed = []
+    for k in (2, 5, 11):   # kind 2: payloads found in their own NAL
+        d = ps.descs[k]
+        mid = int(d["payload_offset"]) + int(d["payload_size"]) // 2
+        ps2.arena[mid] ^= 0x5A
+        changed.append(k)
+    a, ok = _assemble(data, ps2, parsed=True)
+    exp = _expected_layout(data, ps2, ok)
+    lay = _layout_of(a)
+    assert lay == exp
+    assert all(lay[k] is None for k in changed) and all(_expected_layout(data, ps, ok)[k] is not None for k in changed)
 
 
 def test_assembly_scales_linearly():
