@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
     "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables", "avr_last_phase_times",
     "avr_plan_decompress", "avr_splice_container", "avr_roundtrip_files", "avr_slice_kernel",
+    "avr_compress_chain_range", "avr_decompress_chain_range",
 )
 
 # avr_slice_desc / avr_slice_result (include/avrecode.h), C layout
@@ -178,6 +179,8 @@ def lib() -> ctypes.CDLL:
     L.avr_derive_decompress_descs.argtypes = [vp, vp, vp, i32, vp, vp]
     L.avr_verify_slices.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, vp]
     L.avr_slice_kernel.argtypes = [vp, i32, i32, i32, ctypes.POINTER(ctypes.c_int)]
+    L.avr_compress_chain_range.argtypes = [vp, vp, sz, i32, i32] + [vp] * 7
+    L.avr_decompress_chain_range.argtypes = [vp, vp, sz, i32, i32] + [vp] * 7
     L.avr_pack_outputs.argtypes = [vp, vp, vp, i32, vp, vp, vp, vp]
     L.avr_parse_stream.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
     L.avr_parse_stream_range.argtypes = [vp, sz, i32, i32, pp, pi, pp, psz, psz, pi, pi]
@@ -436,9 +439,10 @@ def container_bound(n_file: int, n_slices: int, recoded_bytes: int) -> int:
 def assemble_container(data, status: np.ndarray, recoded, offsets: np.ndarray, lens: np.ndarray,
                        model: int = MODEL_PARALLEL, ps: "ParsedStream | None" = None, as_array: bool = False,
                        out: "np.ndarray | None" = None):
-    """PARALLEL-model Recoded container from per-slice outputs (avr_assemble_container; with ps =
+    """Recoded container from per-slice outputs gathered from the ranks (avr_assemble_container; with ps =
     parse_stream(data) already in hand, avr_assemble_container_parsed: no second parse).  recoded:
-    bytes or a uint8 array.  model: the coder the outputs were made with.  as_array: the container
+    bytes or a uint8 array.  model: the model / coder the outputs were made with (PARALLEL, PARALLEL32,
+    or CHAINED for Context.compress_chain_range's outputs).  as_array: the container
     as a uint8 array over the library's buffer (no copy into bytes).  out (with ps): a uint8 array
     the container is written into (avr_assemble_container_into; container_bound() bytes suffice);
     returns the view of it that holds the container.  Host only."""
@@ -643,6 +647,31 @@ class Context:
         P = self._ptr
         self._check(lib().avr_verify_slices(self._h, P(d_desc), P(d_res_c), P(d_res_d), n, P(d_in), P(d_regen),
                                             P(d_verdict), self._stream(stream)), "verify_slices")
+
+    def _chain_range(self, fn, name, data, world: int, rank: int):
+        p, n, keep = _buf(data)
+        lo, hi = ctypes.c_int(), ctypes.c_int()
+        st, blob, offs, lens = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        blen = ctypes.c_size_t()
+        r = fn(self._h, p, n, world, rank, ctypes.byref(lo), ctypes.byref(hi), ctypes.byref(st), ctypes.byref(blob),
+               ctypes.byref(blen), ctypes.byref(offs), ctypes.byref(lens))
+        del keep
+        self._check(r, name)
+        k = hi.value - lo.value
+        return (lo.value, hi.value, _take_array(st, 4 * k).view(np.int32), _take_array(blob, blen.value),
+                _take_array(offs, 8 * k).view(np.uint64), _take_array(lens, 4 * k).view(np.uint32))
+
+    def compress_chain_range(self, data, world: int, rank: int):
+        """This rank's chains of a chained-model compress of one file (avr_compress_chain_range):
+        (lo, hi, status int32, recoded uint8, offsets uint64, lens uint32) for the file's slices
+        [lo, hi); status 0 coded, -1 not coded, -2 failed (compress the file whole)."""
+        return self._chain_range(lib().avr_compress_chain_range, "compress_chain_range", data, world, rank)
+
+    def decompress_chain_range(self, avrc, world: int, rank: int):
+        """This rank's chains of a chained- (or reference-) model container
+        (avr_decompress_chain_range): (lo, hi, status, regen, offsets, lens) for the plan's slices
+        [lo, hi); status 0 regenerated, 1 not coded, < 0 failed."""
+        return self._chain_range(lib().avr_decompress_chain_range, "decompress_chain_range", avrc, world, rank)
 
     def slice_kernel(self, n: int, max_mb_width: int, decompress: bool, p32: bool = False) -> str:
         """The kernel a parallel-model batch of n slices runs (avr_slice_kernel), named as rocprofv3

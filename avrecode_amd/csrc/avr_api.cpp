@@ -102,6 +102,9 @@ bool valid_model(int m) {
 bool parallel_model(int m) { return m == AVR_MODEL_PARALLEL || m == AVR_MODEL_PARALLEL32; }
 // the reference model over a whole file, or in chains of AVR_CHAIN_SLICES coded slices
 bool reference_model(int m) { return m == AVR_MODEL_REFERENCE || m == AVR_MODEL_CHAINED; }
+// models whose per-slice outputs come from several ranks and are assembled on one: the parallel
+// models (slice ranges) and the chained model (chain ranges); the reference model is one unit
+bool assemblable(int m) { return parallel_model(m) || m == AVR_MODEL_CHAINED; }
 uint32_t coder_flag(int m) { return m == AVR_MODEL_PARALLEL32 ? avr::kFlagP32 : 0u; }
 constexpr size_t kLdsBudget = 160 * 1024;   // LDS per workgroup (one slice) on gfx950
 constexpr uint64_t kMaxSynthBytes = (uint64_t)1 << 35;   // avr_synthesize_stream's output cap (32 GiB)
@@ -1391,6 +1394,221 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
   return status ? AVR_OK : first_err;
 }
 
+// ------------------------------------------------------------ the chained model across GPUs
+// The chained model's chains are independent by construction (a fresh model -- estimators, frames --
+// before every AVR_CHAIN_SLICES-th coded slice of a file), so one file's chains can run on several
+// GPUs: each rank takes a contiguous range of chains, balanced by payload bytes, and the re-coded
+// (or regenerated) slices are gathered to rank 0, which assembles (splices) them as for the
+// parallel model.  Chain c of a file starts at slice first[c]: the slice holding the
+// (AVR_CHAIN_SLICES c)-th coded slice (uncoded slices before it stay in chain c - 1, where they
+// only turn the old chain's frames over); first.back() = the slice count.
+std::vector<int> chain_starts(const std::vector<char>& coded) {
+  std::vector<int> first{0};
+  int coded_n = 0;
+  for (size_t i = 0; i < coded.size(); i++) {
+    if (!coded[i]) continue;
+    if (coded_n > 0 && coded_n % AVR_CHAIN_SLICES == 0) first.push_back((int)i);
+    coded_n++;
+  }
+  first.push_back((int)coded.size());
+  return first;
+}
+
+// [lo, hi) of rank's contiguous range of units weighted w: shard.partition's rule (the owner of a
+// unit is the rank its byte-prefix midpoint falls in), so both sides cut identically.
+std::pair<int, int> partition_range(const std::vector<double>& w, int world, int rank) {
+  const int n = (int)w.size();
+  if (world <= 1) return rank == 0 ? std::make_pair(0, n) : std::make_pair(n, n);
+  double total = 0;
+  for (double x : w) total += x;
+  std::vector<int> cuts(world + 1, n);
+  if (total <= 0) {
+    for (int r = 0; r < world; r++) cuts[r] = (int)std::nearbyint((double)r * n / world);
+  } else {
+    std::vector<int> owner(n);
+    double acc = 0;
+    for (int i = 0; i < n; i++) {
+      acc += w[i];
+      const double mid = acc - w[i] / 2;
+      owner[i] = std::min((int)(mid * world / total), world - 1);
+    }
+    for (int r = 0; r < world; r++) cuts[r] = (int)(std::lower_bound(owner.begin(), owner.end(), r) - owner.begin());
+  }
+  return {cuts[rank], cuts[rank + 1]};
+}
+
+// One rank's outputs over its slice range [lo, hi) of the file (compress) or of the container's
+// plan (decompress): per slice a status and its bytes (blob + offsets[k], lens[k]).
+struct ChainRangeOut {
+  int lo = 0, hi = 0;
+  std::vector<int32_t> status;
+  std::vector<uint64_t> offsets;
+  std::vector<uint32_t> lens;
+  std::vector<uint8_t> blob;
+};
+
+// compressor::run (recode.cpp:1102-1132) of the chained model, this rank's chains only: the parse
+// and the segmentation of the whole file (the coded slices, hence the chains, depend on every block
+// before them), then the reference-model pass over the chains [clo, chi) (run_plan: one workgroup
+// per chain, or the parallel reference-model compress when it pays).  status: 0 coded (bytes),
+// -1 not coded, -2 a coded slice the pass failed (the whole-file call would demote it and
+// re-segment, moving every later chain: the caller compresses the file whole instead).
+int compress_chain_range(avr_ctx* c, const uint8_t* in, size_t n, int world, int rank, ChainRangeOut* o) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  ParsedFile pf;
+  if (int r = parse_file(c, in, n, &pf, /*views=*/true)) return r;
+  const size_t ns = pf.slices.size();
+  std::vector<char> ok(ns), coded(ns);
+  for (size_t i = 0; i < ns; i++) ok[i] = recodable_candidate(pf.slices[i]);
+  const std::vector<const uint8_t*> found = segment(in, n, pf, ok);
+  for (size_t i = 0; i < ns; i++) coded[i] = found[i] != nullptr;
+  const std::vector<int> first = chain_starts(coded);
+  const int nc = (int)first.size() - 1;
+  std::vector<double> w(nc, 0.0);
+  for (int ch = 0; ch < nc; ch++)
+    for (int i = first[ch]; i < first[ch + 1]; i++)
+      if (coded[i]) w[ch] += (double)pf.slices[i].size;
+  const auto [clo, chi] = partition_range(w, world, rank);
+  o->lo = first[clo];
+  o->hi = first[chi];
+  const int nr = o->hi - o->lo;
+  o->status.assign(nr, -1);
+  o->offsets.assign(nr, 0);
+  o->lens.assign(nr, 0);
+  o->blob.clear();
+  if (chi <= clo) return AVR_OK;
+  Plan rp;
+  for (int ch = clo; ch < chi; ch++) {
+    rp.file_first.push_back((int)rp.descs.size());
+    for (int i = first[ch]; i < first[ch + 1]; i++) {   // as compress_files builds a chain
+      const avr::SliceInfo& s = pf.slices[i];
+      avr_slice_desc d = desc_from_header(s);
+      d.coded = coded[i];
+      if (d.coded) {
+        append_aligned(&rp.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
+        d.payload_size = (uint32_t)s.size;
+        d.read_limit = (uint32_t)s.read_limit;
+        d.out_capacity = (uint32_t)(s.size * 4 + 4096);
+        rp.max_w = std::max(rp.max_w, ring_cols(d));
+      }
+      rp.descs.push_back(d);
+    }
+  }
+  rp.file_first.push_back((int)rp.descs.size());
+  std::vector<avr_slice_result> rr;
+  Bytes ro;
+  if (int r = run_plan(c, 0, true, rp, &rr, &ro, false, 0)) return r;
+  uint64_t total = 0;
+  for (int k = 0; k < nr; k++)
+    if (rp.descs[k].coded && rr[k].status == 0) total += rr[k].out_len;
+  o->blob.resize(total);
+  uint64_t at = 0;
+  for (int k = 0; k < nr; k++) {
+    if (!rp.descs[k].coded) continue;
+    if (rr[k].status != 0) {
+      o->status[k] = -2;
+      continue;
+    }
+    o->status[k] = 0;
+    o->offsets[k] = at;
+    o->lens[k] = rr[k].out_len;
+    if (rr[k].out_len) memcpy(o->blob.data() + at, ro.data() + rp.descs[k].out_offset, rr[k].out_len);
+    at += rr[k].out_len;
+  }
+  return AVR_OK;
+}
+
+// decompressor::run (recode.cpp:1312-1357) of a chained-model container, this rank's chains only:
+// the container planned as the whole-file call plans it (every slice, coded or not: the reference
+// model turns frames over on uncoded ones), the chains cut by the same rule, and the plan's slices
+// [lo, hi) of this rank's chains regenerated on the device (one workgroup per chain).  status per
+// plan slice: 0 regenerated (bytes), 1 not coded, < 0 failed.  The caller splices the gathered
+// slices with avr_dec_plan_splice (rank 0's plan of the same container).
+int decompress_chain_range(avr_ctx* c, const uint8_t* avrc, size_t n, int world, int rank, ChainRangeOut* o) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  DecJob j;
+  Plan full;
+  full.layout_only = true;
+  if (int r = decompress_setup(c, avrc, n, &j, &full)) return r;
+  if (!reference_model(j.model)) return fail(c, AVR_ERR_UNSUPPORTED, "not a reference- or chained-model container");
+  const int ns = (int)full.descs.size();
+  std::vector<char> coded(ns);
+  for (int k = 0; k < ns; k++) coded[k] = full.descs[k].coded != 0;
+  // the reference model (one chain per file) is a single unit; the chained model's chains
+  const std::vector<int> first = j.model == AVR_MODEL_CHAINED ? chain_starts(coded) : std::vector<int>{0, ns};
+  const int nc = (int)first.size() - 1;
+  std::vector<double> w(nc, 0.0);
+  for (int ch = 0; ch < nc; ch++)
+    for (int k = first[ch]; k < first[ch + 1]; k++)
+      if (coded[k]) w[ch] += (double)full.descs[k].payload_size;
+  const auto [clo, chi] = partition_range(w, world, rank);
+  o->lo = first[clo];
+  o->hi = first[chi];
+  const int nr = o->hi - o->lo;
+  o->status.assign(nr, 1);
+  o->offsets.assign(nr, 0);
+  o->lens.assign(nr, 0);
+  o->blob.clear();
+  if (chi <= clo) return AVR_OK;
+  // the range's re-coded streams: decompress_setup listed every coded slice's copy in plan order
+  Plan sub;
+  size_t ci = 0;
+  for (int k = 0; k < ns && k < o->hi; k++) {
+    avr_slice_desc d = full.descs[k];
+    const avr::PbCopy* cp = d.coded ? &full.arena_copies[ci++] : nullptr;
+    if (k < o->lo) continue;
+    if (cp) {
+      append_aligned(&sub.arena, cp->src, cp->len, 16, &d.payload_offset);
+      sub.max_w = std::max(sub.max_w, ring_cols(d));
+    }
+    sub.descs.push_back(d);
+  }
+  for (int ch = clo; ch <= chi; ch++) sub.file_first.push_back(first[ch] - o->lo);
+  std::vector<avr_slice_result> rr;
+  Bytes ro;
+  if (int r = run_plan(c, 1, true, sub, &rr, &ro, false, 0)) return r;
+  uint64_t total = 0;
+  for (int k = 0; k < nr; k++)
+    if (sub.descs[k].coded && rr[k].status == 0) total += rr[k].out_len;
+  o->blob.resize(total);
+  uint64_t at = 0;
+  for (int k = 0; k < nr; k++) {
+    if (!sub.descs[k].coded) continue;
+    o->status[k] = rr[k].status == 0 ? 0 : std::min(-1, (int)rr[k].status);
+    if (rr[k].status != 0) continue;
+    o->offsets[k] = at;
+    o->lens[k] = rr[k].out_len;
+    if (rr[k].out_len) memcpy(o->blob.data() + at, ro.data() + sub.descs[k].out_offset, rr[k].out_len);
+    at += rr[k].out_len;
+  }
+  return AVR_OK;
+}
+
+// a ChainRangeOut to the caller's malloc'd buffers (avr_free)
+int export_range(const ChainRangeOut& o, int* lo, int* hi, int32_t** status, uint8_t** blob, size_t* blob_len,
+                 uint64_t** offsets, uint32_t** lens) {
+  const size_t nr = (size_t)(o.hi - o.lo);
+  *status = (int32_t*)malloc(sizeof(int32_t) * std::max<size_t>(1, nr));
+  *offsets = (uint64_t*)malloc(sizeof(uint64_t) * std::max<size_t>(1, nr));
+  *lens = (uint32_t*)malloc(sizeof(uint32_t) * std::max<size_t>(1, nr));
+  *blob = host_alloc(std::max<size_t>(1, o.blob.size()));
+  if (!*status || !*offsets || !*lens || !*blob) {
+    free(*status), free(*offsets), free(*lens), free(*blob);
+    *status = nullptr, *offsets = nullptr, *lens = nullptr, *blob = nullptr;
+    return AVR_ERR_OUT_OF_MEMORY;
+  }
+  if (nr) {
+    memcpy(*status, o.status.data(), sizeof(int32_t) * nr);
+    memcpy(*offsets, o.offsets.data(), sizeof(uint64_t) * nr);
+    memcpy(*lens, o.lens.data(), sizeof(uint32_t) * nr);
+  }
+  if (!o.blob.empty()) memcpy(*blob, o.blob.data(), o.blob.size());
+  *blob_len = o.blob.size();
+  *lo = o.lo;
+  *hi = o.hi;
+  return AVR_OK;
+}
+
 }  // namespace
 
 // ================================================================================ C ABI
@@ -1471,7 +1689,6 @@ int avr_dec_plan_load(avr_dec_plan* h, const uint8_t* avrc, size_t n, int* n_sli
     h->plan.max_w = 1;
     h->plan.layout_only = true;
     if (int r = decompress_setup(nullptr, avrc, n, &h->job, &h->plan)) return r;
-    if (!h->job.parallel) return AVR_ERR_UNSUPPORTED;   // the reference model's slices chain: no split
     uint64_t w = 0;
     int mh = 1;
     for (auto& d : h->plan.descs) {
@@ -1585,6 +1802,9 @@ int avr_plan_decompress(const uint8_t* avrc, size_t n, avr_slice_desc** descs, i
     int ns = 0;
     size_t al = 0;
     if (int r = avr_dec_plan_load(&h, avrc, n, &ns, &al, work_len, max_mb_width, max_mb_height)) return r;
+    // a slice batch for slice-range sharding: the parallel models only (the reference model's
+    // slices chain; the chained model shards by chains, avr_decompress_chain_range)
+    if (!h.job.parallel) return AVR_ERR_UNSUPPORTED;
     *descs = (avr_slice_desc*)malloc(sizeof(avr_slice_desc) * std::max(1, ns));
     *arena = host_alloc(al);
     if (!*descs || !*arena) {
@@ -1691,8 +1911,7 @@ int assemble(const uint8_t* file, size_t n, int model, const std::vector<SliceVi
 int avr_assemble_container(const uint8_t* file, size_t n, int model, int n_slices, const int32_t* status,
                            const uint8_t* recoded, size_t recoded_len, const uint64_t* offsets, const uint32_t* lens,
                            uint8_t** out, size_t* out_len) {
-  if (!file || !out || !out_len || n_slices < 0 || (n_slices && (!status || !offsets || !lens)) ||
-      !parallel_model(model))
+  if (!file || !out || !out_len || n_slices < 0 || (n_slices && (!status || !offsets || !lens)) || !assemblable(model))
     return AVR_ERR_INVALID_ARGUMENT;
   return guarded(nullptr, [&]() -> int {
     ParsedFile pf;
@@ -1708,7 +1927,7 @@ int assemble_parsed(const uint8_t* file, size_t n, int model, const avr_slice_de
                     size_t recoded_len, const uint64_t* offsets, const uint32_t* lens, uint8_t** out, size_t* out_len,
                     uint8_t* dst, size_t cap) {
   if (!file || !out_len || n_slices < 0 || (n_slices && (!descs || !arena || !status || !offsets || !lens)) ||
-      !parallel_model(model))
+      !assemblable(model))
     return AVR_ERR_INVALID_ARGUMENT;
   return guarded(nullptr, [&]() -> int {
     std::vector<SliceView> sv((size_t)n_slices);
@@ -2022,6 +2241,34 @@ int avr_verify_slices(avr_ctx* c, const avr_slice_desc* d_desc, const avr_slice_
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, avr::launch_verify(d_desc, d_res_c, d_res_d, n, d_in, d_regen, d_verdict, (hipStream_t)stream));
   return AVR_OK;
+}
+
+int avr_compress_chain_range(avr_ctx* c, const uint8_t* file, size_t n, int world, int rank, int* lo, int* hi,
+                             int32_t** status, uint8_t** recoded, size_t* recoded_len, uint64_t** offsets,
+                             uint32_t** lens) {
+  if (!c || !file || world < 1 || rank < 0 || rank >= world || !lo || !hi || !status || !recoded || !recoded_len ||
+      !offsets || !lens)
+    return AVR_ERR_INVALID_ARGUMENT;
+  *status = nullptr, *recoded = nullptr, *offsets = nullptr, *lens = nullptr;
+  return guarded(c, [&]() -> int {
+    ChainRangeOut o;
+    if (int r = compress_chain_range(c, file, n, world, rank, &o)) return r;
+    return export_range(o, lo, hi, status, recoded, recoded_len, offsets, lens);
+  });
+}
+
+int avr_decompress_chain_range(avr_ctx* c, const uint8_t* avrc, size_t n, int world, int rank, int* lo, int* hi,
+                               int32_t** status, uint8_t** regen, size_t* regen_len, uint64_t** offsets,
+                               uint32_t** lens) {
+  if (!c || !avrc || world < 1 || rank < 0 || rank >= world || !lo || !hi || !status || !regen || !regen_len ||
+      !offsets || !lens)
+    return AVR_ERR_INVALID_ARGUMENT;
+  *status = nullptr, *regen = nullptr, *offsets = nullptr, *lens = nullptr;
+  return guarded(c, [&]() -> int {
+    ChainRangeOut o;
+    if (int r = decompress_chain_range(c, avrc, n, world, rank, &o)) return r;
+    return export_range(o, lo, hi, status, regen, regen_len, offsets, lens);
+  });
 }
 
 int avr_slice_kernel(avr_ctx* c, int decompress, int n, int max_mb_width, int* kind) {

@@ -303,14 +303,22 @@ AVR_FI void wd_poll(uint64_t* t0, uint32_t site, uint32_t a, uint32_t b, uint32_
 // workgroup 8 u32: [0..2] wave w's (slices drawn << 8 | phase), [3] the queue entry drawn, [4]
 // the walker's macroblocks of the current slice.  Phases: 1 drawn, 2 estimator table reset,
 // 3 slice state set up, 4 the wave's role done, 5 slice finished, 6 left the loop.
+// -DAVR_QTRACE=1 records only the queue entries drawn and the exit (the least perturbation),
+// -DAVR_QTRACE=2 every phase and the walker's macroblocks too.
 #ifdef AVR_QTRACE
 static __device__ uint32_t* avr_qtrace;
 AVR_FI void qtrace(uint32_t slot, uint32_t v) {
   uint32_t* t = avr_qtrace;
   if (t && __lane_id() == 0) __hip_atomic_store(&t[blockIdx.x * 8 + slot], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+#define QTRACE1(slot, v) qtrace(slot, v)
+#if AVR_QTRACE >= 2
 #define QTRACE(slot, v) qtrace(slot, v)
 #else
+#define QTRACE(slot, v)
+#endif
+#else
+#define QTRACE1(slot, v)
 #define QTRACE(slot, v)
 #endif
 
@@ -2984,13 +2992,13 @@ __global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables
     WD_CHECK(cell == kNoCell || cell < 4u * kCuIds, WD_CELL, cell, threadIdx.x, k);
 #ifdef AVR_QTRACE
     qiter++;
-    if (threadIdx.x == 0) QTRACE(3, k);
+    if (threadIdx.x == 0) QTRACE1(3, k);
     QTRACE(threadIdx.x >> 6, qiter << 8 | 1);
 #endif
     parallel_slice<MODE, FLD, P32, true>(smem, G, descs, s, in, out, res, est_scratch + (size_t)blockIdx.x * kEstGlobal,
                                          flags, cell, qiter);
   }
-  QTRACE(threadIdx.x >> 6, qiter << 8 | 6);
+  QTRACE1(threadIdx.x >> 6, qiter << 8 | 6);
 }
 
 // Host side of the parallel launches (instantiated in each kernel TU, avr_k_*.hip, with that TU's

@@ -10,6 +10,14 @@ rank 0 (point-to-point send/recv over xGMI with backend "nccl" = RCCL; CPU tenso
                       literals and applies the last-byte patch (avr_splice_container)
 Both are byte-identical to the single-GPU calls.
 
+CHAINED model (the reference model restarted every AVR_CHAIN_SLICES coded slices), one file over
+the ranks, both directions: its chains are independent, so a file's chains are cut into contiguous
+ranges balanced by bytes (the library applies partition()'s rule), each rank runs its chains on its
+GPU (avr_compress_chain_range / avr_decompress_chain_range), and the same gather brings the
+re-coded (regenerated) slices to rank 0, which assembles (splices) them:
+  sharded_compress_chained / sharded_decompress_chained: byte-identical to ctx.compress(data,
+  MODEL_CHAINED) / ctx.decompress(avrc).
+
 A corpus of files (BASELINE configs[4]): files are dealt to ranks whole (deal_files, LPT by
 bytes) and each rank runs its files through the batched corpus calls; the reference model's
 unit of sequential work is a file (its estimators carry across slices, recode.cpp:662-665), so
@@ -19,8 +27,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import (MODEL_PARALLEL, ParsedStream, assemble_container, container_model, parse_stream, plan_decompress,
-               splice_container)
+from . import (MODEL_CHAINED, MODEL_PARALLEL, DecompressPlan, ParsedStream, assemble_container, container_model,
+               parse_stream, plan_decompress, splice_container)
 
 
 def partition(sizes, world: int) -> list[tuple[int, int]]:
@@ -42,15 +50,28 @@ def partition(sizes, world: int) -> list[tuple[int, int]]:
     return [(cuts[r], cuts[r + 1]) for r in range(world)]
 
 
-def gather_flat(flat, status, offsets, lens, dst: int = 0, device=None):
+def pinned(nbytes: int):
+    """A page-locked host buffer (uint8 numpy view of a pinned torch tensor): device copies into and
+    out of it run as DMA at the link's rate, and one allocation is reused from step to step (a
+    fresh multi-GB numpy array costs its page faults on every step)."""
+    import torch
+    t = torch.empty(max(1, nbytes), dtype=torch.uint8, pin_memory=True)
+    return t.numpy()
+
+
+def gather_flat(flat, status, offsets, lens, dst: int = 0, device=None, out=None):
     """Gather every rank's per-slice (status, bytes) to `dst`, in rank order.
 
     flat: this rank's outputs packed in one uint8 tensor (device tensor with RCCL), slice k's bytes
     at flat[offsets[k] : offsets[k] + lens[k]].  Returns (status int32[n_total], blob uint8 array,
-    offsets uint64, lens uint32) on dst, None elsewhere (the blob is one host array written in
-    place: a multi-GB gather is copied once, device to host).  Counts first (a fixed-size all_gather),
-    then one send/recv of the per-slice metadata and one of the flat bytes per rank: RCCL has no
-    gatherv, and the payload moves device to device over xGMI."""
+    offsets uint64, lens uint32) on dst, None elsewhere.  The blob is one host array written in
+    place (out: a caller's buffer of at least the total size, ideally pinned(): reused across steps,
+    copied into by DMA); a multi-GB gather is copied once, device to host.  Counts first (a
+    fixed-size all_gather), then one send/recv of the per-slice metadata and one of the flat bytes
+    per rank: RCCL has no gatherv, and the payload moves device to device over xGMI.
+    On dst the receives are posted for all ranks at once (each peer's xGMI link carries its own)
+    and each rank's bytes go to the host on a copy stream as soon as they have arrived, while the
+    later ranks' are still in flight."""
     import torch
     import torch.distributed as dist
 
@@ -74,38 +95,64 @@ def gather_flat(flat, status, offsets, lens, dst: int = 0, device=None):
         if sizes[rank]:
             dist.send(body, dst)
         return None
-    st, offs, ln, base = [], [], [], 0
-    blob = np.empty(sum(sizes), dtype=np.uint8)
+    total = sum(sizes)
+    if out is not None and out.nbytes >= total:
+        blob = out[:total]
+    else:
+        blob = np.empty(total, dtype=np.uint8)
+    # post every receive, then drain them in rank order
+    bufs, works = [], []
     for r in range(world):
         if r == rank:
-            m, f = meta, body
-        else:
-            m = torch.empty(3 * counts[r], dtype=torch.int64, device=dev)
-            f = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
-            if counts[r]:
-                dist.recv(m, r)
-            if sizes[r]:
-                dist.recv(f, r)
-        m = m.cpu().numpy()
-        c = counts[r]
-        st.append(m[:c])
-        offs.append(m[c:2 * c] + base)
-        ln.append(m[2 * c:])
+            bufs.append((meta, body))
+            continue
+        m = torch.empty(3 * counts[r], dtype=torch.int64, device=dev)
+        f = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
+        if counts[r]:
+            works.append(dist.irecv(m, r))
         if sizes[r]:
-            torch.from_numpy(blob[base:base + sizes[r]]).copy_(f)
+            works.append(dist.irecv(f, r))
+        bufs.append((m, f))
+    on_gpu = dev.type == "cuda"
+    copy_stream = torch.cuda.Stream(dev) if on_gpu else None
+    st, offs, ln, base, wi = [], [], [], 0, 0
+    for r in range(world):
+        m, f = bufs[r]
+        if r != rank:
+            for _ in range(int(counts[r] > 0) + int(sizes[r] > 0)):
+                works[wi].wait()
+                wi += 1
+        c = counts[r]
+        if sizes[r]:
+            dst_t = torch.from_numpy(blob[base:base + sizes[r]])
+            if on_gpu:
+                # after the receive (waited on the current stream), on the copy stream: this rank's
+                # D2H overlaps the next ranks' receives
+                copy_stream.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(copy_stream):
+                    dst_t.copy_(f, non_blocking=dst_t.is_pinned())
+                    f.record_stream(copy_stream)
+            else:
+                dst_t.copy_(f)
+        mh = m.cpu().numpy()
+        st.append(mh[:c])
+        offs.append(mh[c:2 * c] + base)
+        ln.append(mh[2 * c:])
         base += sizes[r]
+    if on_gpu:
+        copy_stream.synchronize()
     cat = lambda xs, t: np.concatenate(xs).astype(t) if xs else np.zeros(0, t)  # noqa: E731
     return cat(st, np.int32), blob, cat(offs, np.uint64), cat(ln, np.uint32)
 
 
-def gather_blocks(local: list[bytes], status: list[int], dst: int = 0, device=None):
+def gather_blocks(local: list[bytes], status: list[int], dst: int = 0, device=None, out=None):
     """gather_flat for host byte strings (one per slice)."""
     import torch
     lens = np.array([len(b) for b in local], dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if len(lens) else lens
     flat = torch.from_numpy(np.frombuffer(b"".join(local), dtype=np.uint8).copy())
     dev = device if device is not None else torch.device("cpu")
-    return gather_flat(flat, status, offs, lens, dst=dst, device=dev)
+    return gather_flat(flat, status, offs, lens, dst=dst, device=dev, out=out)
 
 
 def subset(ps: ParsedStream, lo: int, hi: int) -> ParsedStream:
@@ -219,6 +266,59 @@ def sharded_decompress(ctx, avrc: bytes, device=None, run_range=None) -> bytes |
         return None
     st, blob, offs, lens = g
     return splice_container(avrc, st, blob, offs, lens)
+
+
+def _host_to_gather(blob, dev):
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(blob) if len(blob) else np.zeros(16, np.uint8))
+    return t.to(dev) if dev.type == "cuda" else t
+
+
+def sharded_compress_chained(ctx, data, device=None, run_range=None) -> bytes | None:
+    """CHAINED-model compress of one file across all ranks; the container is returned on rank 0.
+
+    Every rank runs its contiguous range of the file's chains on its GPU
+    (Context.compress_chain_range: parse and segmentation of the whole file, the reference-model
+    pass over its chains), the re-coded slices go to rank 0 (gather_flat over RCCL), which assembles
+    the Recoded container (avr_assemble_container, model CHAINED).  Byte-identical to
+    ctx.compress(data, MODEL_CHAINED).  A coded slice that failed on its rank (status -2: the
+    whole-file call would demote it and re-segment, moving every later chain) makes rank 0 compress
+    the file whole.  run_range() -> compress_chain_range's tuple replaces the device step (tests)."""
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = _gather_device(ctx, device)
+    lo, hi, st, blob, offs, lens = (run_range or (lambda: ctx.compress_chain_range(data, world, rank)))()
+    g = gather_flat(_host_to_gather(blob, dev), st.astype(np.int64), offs.astype(np.int64), lens.astype(np.int64),
+                    dst=0, device=dev)
+    if g is None:
+        return None
+    st, blob, offs, lens = g
+    if (st < -1).any():
+        return ctx.compress(data, MODEL_CHAINED)
+    return assemble_container(data, st, blob, offs, lens, model=MODEL_CHAINED)
+
+
+def sharded_decompress_chained(ctx, avrc, device=None, run_range=None) -> bytes | None:
+    """CHAINED-model decompress of one container across all ranks; the file is returned on rank 0.
+
+    Every rank plans the container and regenerates its contiguous range of chains on its GPU
+    (Context.decompress_chain_range); the regenerated slices go to rank 0 (gather_flat), which
+    splices them with the literals and the last-byte patch on its plan of the same container
+    (DecompressPlan.splice, recode.cpp:1338-1357).  Byte-identical to ctx.decompress(avrc).
+    A reference-model container is one unit: rank 0 decodes it whole."""
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = _gather_device(ctx, device)
+    lo, hi, st, regen, offs, lens = (run_range or (lambda: ctx.decompress_chain_range(avrc, world, rank)))()
+    g = gather_flat(_host_to_gather(regen, dev), st.astype(np.int64), offs.astype(np.int64), lens.astype(np.int64),
+                    dst=0, device=dev)
+    if g is None:
+        return None
+    st, blob, offs, lens = g
+    out = DecompressPlan().load(avrc).splice(st, blob, offs, lens)
+    return out.tobytes()
 
 
 def scatter_parsed(ps: "ParsedStream | None", ranges, device, src: int = 0):

@@ -468,13 +468,21 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     gdev = _coll(dev)
     n_mine = hi - lo
     dplan = avr.DecompressPlan() if rank == 0 else None
-    bufs = {}   # rank 0's container, arena and file buffers: allocated at the first step, then reused
+    # rank 0's host buffers, allocated at the first step and reused: the container and the file
+    # (host only) and, page-locked (shard.pinned), the two gathers' destinations and the arena that
+    # goes back to the devices -- their copies run as DMA without page faults
+    bufs = {}
 
-    def buf(name, need):
+    def buf(name, need, pin=False):
         b = bufs.get(name)
         if b is None or b.nbytes < need:
-            b = bufs[name] = np.empty(need + need // 64 + 4096, dtype=np.uint8)
+            n = need + need // 64 + 4096
+            b = bufs[name] = shard.pinned(n) if pin else np.empty(n, dtype=np.uint8)
         return b
+
+    # the compress gather's total: every rank's packed re-coded bytes (at most their payloads' 2x + 256
+    # capacity, in practice ~ the stream), sized on the first step
+    total_c = len(data) + (1 << 24)
 
     def step(ev, ph):
         marks = [time.perf_counter()]
@@ -496,7 +504,8 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
         lens = np.where(ok_c, res["out_len"], 0).astype(np.int64)
         st = np.where(ok_c, 0, -1).astype(np.int64)
         mark("results_d2h_s")
-        g = shard.gather_flat(flat, st, offs, lens, dst=0, device=gdev)
+        g = shard.gather_flat(flat, st, offs, lens, dst=0, device=gdev,
+                              out=buf("gather", total_c, pin=True) if rank == 0 else None)
         mark("gather_s")
         avrc = pp = dranges = None
         if g is not None:
@@ -506,7 +515,7 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
         # decompress: rank 0 plans the container, every rank regenerates its range
         if rank == 0:
             dplan.load(avrc)
-            pp = dplan.parsed(buf("arena", dplan.arena_len))
+            pp = dplan.parsed(buf("arena", dplan.arena_len, pin=True))
             dranges = shard.partition(pp.descs["payload_size"], world)
         mark("plan_s")
         descs, arena, nd, wl, mw, mh = shard.scatter_parsed(pp, dranges, gdev)
@@ -522,7 +531,8 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
         dres = drange.results()
         dlens = np.where(dres["status"] == 0, dres["out_len"], 0).astype(np.int64)
         doffs = dd_off[:nd].cpu().numpy().astype(np.int64)
-        gd = shard.gather_flat(dflat, dres["status"].astype(np.int64), doffs, dlens, dst=0, device=gdev)
+        gd = shard.gather_flat(dflat, dres["status"].astype(np.int64), doffs, dlens, dst=0, device=gdev,
+                               out=buf("gather_d", len(data) + (1 << 20), pin=True) if rank == 0 else None)
         mark("gather_d_s")
         out = None
         if gd is not None:

@@ -62,7 +62,8 @@ typedef enum {
  * 16 slices: realshort.mp4 0.998, cockatoo.mp4 0.994 of the input, against 0.990 / 0.991 for the
  * reference model and 1.041 / 1.010 for the parallel one), and a file's chains decode on as many
  * workgroups at once.  Whole-file calls only (avr_compress_file(s), avr_decompress_file(s),
- * avr_roundtrip_file(s), and the whole-file hooks sessions); the device slice-batch calls and the
+ * avr_roundtrip_file(s), the whole-file hooks sessions, and the per-rank chain ranges of one file,
+ * avr_compress_chain_range / avr_decompress_chain_range); the device slice-batch calls and the
  * streaming hooks session refuse it with AVR_ERR_INVALID_ARGUMENT. */
 typedef enum { AVR_MODEL_REFERENCE = 0, AVR_MODEL_PARALLEL = 1, AVR_MODEL_PARALLEL32 = 2, AVR_MODEL_CHAINED = 3 } avr_model;
 #define AVR_CHAIN_SLICES 16
@@ -237,6 +238,32 @@ int avr_verify_slices(avr_ctx* ctx, const avr_slice_desc* d_desc, const avr_slic
                       const avr_slice_result* d_res_d, int n, const uint8_t* d_in, const uint8_t* d_regen,
                       int32_t* d_verdict, void* stream);
 
+/* The chained model (AVR_MODEL_CHAINED) across GPUs, within one file.  Its chains are independent
+ * (a fresh reference model before every AVR_CHAIN_SLICES-th coded slice), so a file's chains are cut
+ * into `world` contiguous ranges balanced by payload bytes (the rule of the Python shard.partition)
+ * and rank `rank` runs its range on this context's GPU:
+ *   avr_compress_chain_range: the file parsed and segmented as avr_compress_file does it, then the
+ *     reference-model pass over this rank's chains (compressor::run, recode.cpp:1102-1132, with the
+ *     model restarted per chain, 662-665).  Outputs for the file's slices [*lo, *hi): status 0 =
+ *     coded (its re-coded bytes at recoded + offsets[k], lens[k]), -1 = not coded, -2 = a coded
+ *     slice the pass failed (avr_compress_file would demote it and re-segment, which moves every
+ *     later chain: compress the file whole instead).  The ranks' outputs, concatenated in rank order,
+ *     are avr_assemble_container's status / recoded / offsets / lens for model AVR_MODEL_CHAINED:
+ *     byte-identical to avr_compress_file(file, AVR_MODEL_CHAINED).
+ *   avr_decompress_chain_range: the container planned as avr_decompress_file plans it (every slice,
+ *     coded or not), this rank's chains regenerated (decompressor::cabac_decoder, recode.cpp:
+ *     1411-1520, one chain per workgroup).  Outputs for the plan's slices [*lo, *hi): status 0 =
+ *     regenerated (bytes at regen + offsets[k], lens[k]), 1 = not coded, < 0 failed.  Concatenated in
+ *     rank order they are avr_dec_plan_splice's inputs on a plan of the same container.  A
+ *     reference-model container is one unit (rank 0 takes it whole).
+ * Buffers are allocated here (avr_free).  No reference counterpart: the reference is one CPU thread. */
+int avr_compress_chain_range(avr_ctx* ctx, const uint8_t* file, size_t n, int world, int rank, int* lo, int* hi,
+                             int32_t** status, uint8_t** recoded, size_t* recoded_len, uint64_t** offsets,
+                             uint32_t** lens);
+int avr_decompress_chain_range(avr_ctx* ctx, const uint8_t* avrc, size_t n, int world, int rank, int* lo, int* hi,
+                               int32_t** status, uint8_t** regen, size_t* regen_len, uint64_t** offsets,
+                               uint32_t** lens);
+
 /* Which device kernel a parallel-model batch of n slices (widest picture max_mb_width macroblocks)
  * runs on this context's GPU, by the rule avr_compress_slices / avr_decompress_slices apply:
  * *kind = 0 the resident kernel (slices_parallel_kernel: one workgroup per slice, the whole batch
@@ -268,8 +295,9 @@ int avr_slice_payload_sizes(const uint8_t* file, size_t n, uint32_t** sizes, int
 
 /* Rank 0 of a sharded PARALLEL-model compress: build the Recoded container from per-slice outputs
  * gathered from every rank (compressor::run + find_next_coded_block_and_emit_literal,
- * recode.cpp:1115-1132, 1275-1297).  Host only.  model = AVR_MODEL_PARALLEL or _PARALLEL32 (the
- * coder the outputs were made with: the container's tag).  Slice k (avr_parse_stream order) is
+ * recode.cpp:1115-1132, 1275-1297).  Host only.  model = the model the outputs were made with (the
+ * container's tag): AVR_MODEL_PARALLEL / _PARALLEL32 (avr_compress_slices on each rank's slice
+ * range), or AVR_MODEL_CHAINED (avr_compress_chain_range on each rank's chains).  Slice k (avr_parse_stream order) is
  * coded when it is a candidate and status[k] == 0; its re-coded bytes are recoded[offsets[k] ..
  * + lens[k]), inside recoded_len (AVR_ERR_INVALID_ARGUMENT otherwise).  The result is
  * byte-identical to avr_compress_file(..., model).  avr_assemble_container parses `file` again;
@@ -317,7 +345,7 @@ int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int3
                          size_t* out_len);
 
 /* The sharded decompress's host halves on one parse (decompressor::run, recode.cpp:1338-1409):
- * a plan handle loads a PARALLEL-model container -- read_packet's surrogate stream parsed and
+ * a plan handle loads a container -- read_packet's surrogate stream parsed and
  * matched to the coded blocks, as avr_plan_decompress, but without copying any bytes yet -- then
  * writes the descriptors and the re-coded streams' arena where the caller wants them (the arena
  * with host threads), and splices the regenerated slices with the literals and the last-byte patch
@@ -326,7 +354,10 @@ int avr_splice_container(const uint8_t* avrc, size_t n, int n_slices, const int3
  * (the surrogate stream's buffer) for the next load.  arena_len / work_len / max_mb_* as
  * avr_plan_decompress.  avr_dec_plan_splice: *out_len = the file's size; AVR_ERR_INVALID_ARGUMENT
  * when out_cap is smaller (nothing written) or a slice's bytes lie outside regen or past its
- * capacity, AVR_ERR_FORMAT when a coded block has no slice or a slice's status is not 0. */
+ * capacity, AVR_ERR_FORMAT when a coded block has no slice or a slice's status is not 0.  A
+ * parallel-model plan lists the coded slices (one device batch); a reference- or chained-model plan
+ * lists every slice, coded or not (the reference model turns frames over on uncoded ones), which is
+ * the indexing avr_decompress_chain_range's outputs use. */
 typedef struct avr_dec_plan avr_dec_plan;
 int avr_dec_plan_new(avr_dec_plan** out);
 void avr_dec_plan_free(avr_dec_plan* plan);

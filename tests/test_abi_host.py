@@ -147,8 +147,12 @@ def _gloo_worker(rank, world, port, name, outdir):
         _, recs = slices_p(data, lo, hi)          # stands in for this rank's device output
         st = [0 if r["recodable"] else -1 for r in recs]
         blobs = [r["recoded"] if r["recodable"] else b"" for r in recs]
-        g = shard.gather_blocks(blobs, st, dst=0)
+        # at world 8, rank 0 gathers into a caller's (reused) buffer, as the bench's stream leg does
+        out = np.full(len(data) * 2 + 4096, 0xEE, np.uint8) if rank == 0 and world == 8 else None
+        g = shard.gather_blocks(blobs, st, dst=0, out=out)
         if rank == 0:
+            if out is not None:
+                assert np.shares_memory(g[1], out)
             c = avr.assemble_container(data, *g)
             with open(os.path.join(outdir, "out.avrc"), "wb") as f:
                 f.write(c)
@@ -161,7 +165,8 @@ def _gloo_worker(rank, world, port, name, outdir):
 @pytest.mark.parametrize("name,world", [("realshort.mp4", 2), ("cockatoo.mp4", 2), ("realshort.mp4", 8)])
 def test_gloo_world2_sharded_assembly(name, world):
     """The gather's message sequence (size all_gather, then per rank one metadata and one byte
-    send/recv in rank order) at world 2 and at the node's 8 ranks."""
+    send / receive, the receives posted at once and drained in rank order) at world 2 and at the
+    node's 8 ranks (there into a caller's buffer)."""
     import socket
 
     import torch.multiprocessing as mp

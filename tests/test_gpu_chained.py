@@ -105,3 +105,63 @@ def test_chained_refused_by_slice_batches_and_streaming_hooks(ctx):
     s = ctypes.c_void_p()
     assert avr.lib().avr_hooks_compress_stream_begin(ctx._h, avr.MODEL_CHAINED, ctypes.byref(s)) == -1   # AVR_ERR_INVALID_ARGUMENT
     assert not s.value
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_chain_ranges_in_one_process_equal_whole_file(ctx, world):
+    """Every rank's chain range run in this process (avr_compress_chain_range /
+    avr_decompress_chain_range), concatenated in rank order, assembles / splices to exactly the
+    whole-file container and file: the chained model sharded within a file."""
+    import numpy as np
+    data = _tiled(copies=6, lead=3)   # 51 slices: 4 chains
+    whole = ctx.compress(data, avr.MODEL_CHAINED)
+    parts = [ctx.compress_chain_range(data, world, r) for r in range(world)]
+    assert parts[0][0] == 0 and all(parts[r][1] == parts[r + 1][0] for r in range(world - 1))
+    st = np.concatenate([p[2] for p in parts])
+    assert len(st) == parts[-1][1] and not (st < -1).any()
+    if world > 1:
+        assert sum(p[1] > p[0] for p in parts) > 1, "the chains should spread over the ranks"
+    blob, offs, base = [], [], 0
+    for p in parts:
+        blob.append(p[3])
+        offs.append(p[4].astype(np.uint64) + base)
+        base += len(p[3])
+    avrc = avr.assemble_container(data, st, np.concatenate(blob), np.concatenate(offs),
+                                  np.concatenate([p[5] for p in parts]), model=avr.MODEL_CHAINED)
+    assert avrc == whole
+    dparts = [ctx.decompress_chain_range(whole, world, r) for r in range(world)]
+    dst = np.concatenate([p[2] for p in dparts])
+    dblob, doffs, base = [], [], 0
+    for p in dparts:
+        dblob.append(p[3])
+        doffs.append(p[4].astype(np.uint64) + base)
+        base += len(p[3])
+    out = avr.DecompressPlan().load(whole).splice(dst, np.concatenate(dblob), np.concatenate(doffs),
+                                                  np.concatenate([p[5] for p in dparts]))
+    assert out.tobytes() == data
+
+
+@pytest.mark.parametrize("name,world", [("cockatoo.mp4", 2), ("cockatoo.mp4", 3), ("realshort.mp4", 2)])
+def test_sharded_chained_multirank_gloo(name, world, tmp_path):
+    """The chained model across ranks in separate processes (all on cuda:0, gloo for the gathers):
+    shard.sharded_compress_chained equals the single-GPU container (and the oracle's), and
+    shard.sharded_decompress_chained restores the file."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "out.avrc"
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE=str(world), LOCAL_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).parent / "_shard_worker.py"),
+                                       str(FIX / name), str(out), "C"], env=env))
+    rcs = [p.wait(timeout=110) for p in procs]
+    assert rcs == [0] * world, rcs
+    assert out.read_bytes() == oracle_cli("compress", FIX / name, mode="C")
+    assert Path(str(out) + ".dec").read_bytes() == (FIX / name).read_bytes()

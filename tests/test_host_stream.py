@@ -94,8 +94,13 @@ def test_dec_plan_handle_equals_plan_and_splice():
         st[len(st) // 2] = -9
         with pytest.raises(avr.AvrError):
             h.splice(st, regen, offs, lens)
-    with pytest.raises(avr.AvrError) as e:
-        h.load(oracle_cli("compress", FIX / "realshort.mp4", mode="R"))
+    # a reference- or chained-model container plans every slice, coded or not (the reference
+    # model turns frames over on uncoded ones): the indexing of avr_decompress_chain_range's outputs
+    data = (FIX / "realshort.mp4").read_bytes()
+    for mode in ("R", "C"):
+        assert h.load(oracle_cli("compress", FIX / "realshort.mp4", mode=mode)).n_slices == len(avr.parse_stream(data).descs)
+    with pytest.raises(avr.AvrError) as e:   # the one-shot slice batch stays parallel-model only
+        avr.plan_decompress(oracle_cli("compress", FIX / "realshort.mp4", mode="C"))
     assert e.value.code == -6
     h.close()
 
