@@ -2943,9 +2943,11 @@ __global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables
   extern __shared__ __align__(16) uint8_t smem[];
   Shared* sh = (Shared*)smem;
   // the hot tables and the walker wave's CU-board cell are set up at the first slice this
-  // workgroup takes (a field-kernel workgroup that finds no field slice does neither).  Measured:
-  // setting them up before the first draw instead made the compress kernel hang on the GPU
-  // (r05c/r05e probes), this order does not (r05d).
+  // workgroup takes (a field-kernel workgroup that finds no field slice does neither).  The other
+  // order (-DAVR_QUEUE_EAGER) hangs the first queue launch of a process in its
+  // uninstrumented build only: every instrumented build of it (bounded waits with invariant checks,
+  // host-mapped progress records) runs clean and sees no invariant violated, so the hang follows
+  // that build's code generation, not an ordering rule of the protocol below.
   uint32_t cell = kNoCell;
   bool loaded = false;
   uint32_t qiter = 0;   // slices this workgroup drew (queue trace builds)
