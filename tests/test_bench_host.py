@@ -34,3 +34,21 @@ def test_standalone_slices_match_the_stream():
         assert one[0]["bins"] == whole[i]["bins"]
         assert one[0]["recoded"] == whole[i]["recoded"]
         assert one[0]["regen"] == whole[i]["regen"]
+
+
+def test_bench_golden_is_consistent():
+    """tests/golden/bench_batch.json (the oracle's answer for the headline batch, made by
+    tests/golden/make_bench_golden.py): one record per slice, totals equal to the sums, every slice
+    coded by the oracle; bench.golden_check applies it only to the batch it was made for."""
+    import json
+
+    import bench
+    g = json.loads(bench.GOLDEN_BATCH.read_text())
+    assert g["config"]["slices"] == len(g["slices"]) == 1024 and g["config"]["seed"] == 0
+    assert g["bins_total"] == sum(s["bins"] for s in g["slices"])
+    assert g["recoded_total"] == sum(s["recoded_len"] for s in g["slices"])
+    assert all(s["status"] == 0 and len(s["recoded_sha256"]) == 64 for s in g["slices"])
+
+    class A:
+        slices, mb_width, mb_height, seed = 1024, 120, 68, 1
+    assert bench.golden_check(None, b"", A) is None   # another seed: not this golden's batch
