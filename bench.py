@@ -829,11 +829,13 @@ def p32_extra(batch, args, stream, mk, n_bytes, C64):
 
 
 def corpus_sharded(ctx, args, world, rank, dev):
-    """BASELINE configs[4] on N GPUs: the corpus's files dealt whole to the ranks (shard.deal_files,
-    LPT by bytes) and each rank's files run as one batch per model (avr_roundtrip_files: compress,
-    decompress and byte compare, as the N = 1 corpus leg).  No collective in the timed region; MB/s = corpus bytes /
-    max-over-ranks wall time.  The reference model runs here as replicas over files (its only
-    split)."""
+    """BASELINE configs[4] on N GPUs.  R and P: the corpus's files dealt whole to the ranks
+    (shard.deal_files, LPT by bytes), each rank's files run as one batch per model
+    (avr_roundtrip_files: compress, decompress and byte compare, as the N = 1 corpus leg), no
+    collective in the timed region; the reference model runs here as replicas over files (its only
+    split).  C: every file's chains split over all ranks (the chained model's
+    within-file split: chain ranges on each GPU, RCCL gathers, rank 0 assembles and splices).  MB/s =
+    corpus bytes / max-over-ranks wall time."""
     import torch
     import torch.distributed as dist
 
@@ -844,13 +846,33 @@ def corpus_sharded(ctx, args, world, rank, dev):
     mine = shard.deal_files([len(d) for _, d in files], world)[rank]
     datas = [files[i][1] for i in mine]
     rec = {"files": len(files), "bytes": total, "n_gpus": world, "scaling": "strong",
-           "files_rank0": [files[i][0] for i in shard.deal_files([len(d) for _, d in files], world)[0]]}
+           "files_rank0": [files[i][0] for i in shard.deal_files([len(d) for _, d in files], world)[0]],
+           "C_split": "every file's chains over all ranks (shard.sharded_compress_chained / _decompress_chained)"}
+    gdev = _coll(dev)
+
+    def chained_roundtrip():
+        # the chained model within each file: every rank runs its range of the file's chains, rank 0
+        # assembles the container and splices the file back (compared with the input there)
+        good = True
+        for _, d in files:
+            avrc = shard.sharded_compress_chained(ctx, d, device=gdev)
+            if rank == 0:
+                avrc = bytes(avrc)
+            obj = [avrc]
+            dist.broadcast_object_list(obj, src=0)   # the container every rank decompresses
+            out = shard.sharded_decompress_chained(ctx, obj[0], device=gdev)
+            if rank == 0:
+                good = good and out == d
+        return good
+
     for tag, model in (("R", avr.MODEL_REFERENCE), ("P", avr.MODEL_PARALLEL), ("C", avr.MODEL_CHAINED)):
         for it in range(2):   # one warm-up pass, one timed
             dist.barrier()
             t0 = time.perf_counter()
             ok = True
-            if datas:
+            if model == avr.MODEL_CHAINED:
+                ok = chained_roundtrip()
+            elif datas:
                 outs, _ = ctx.roundtrip_files(datas, model)   # compress, decompress, compare
                 ok = all(isinstance(o, bytes) for o in outs)
             dt = time.perf_counter() - t0

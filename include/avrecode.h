@@ -392,7 +392,14 @@ int avr_neighbor_tables(avr_ctx* ctx, uint8_t out[96]);
  * traces: get() returns the bin and advances *state the way ff_get_cabac / cabac::encoder::put
  * would (recode.cpp:1176, 1443).  Every callback checks the caller's parse against the device's
  * (state byte before each decision, bin kinds, sub-MB / coding-type pairing, recode.cpp:185-189,
- * 933-947); a mismatch makes avr_hooks_end fail with AVR_ERR_FORMAT.  Not thread-safe. */
+ * 933-947); a mismatch makes avr_hooks_end fail with AVR_ERR_FORMAT.  Not thread-safe.
+ * LIMITATION (by design): the caller's parse never drives the model.  In the reference the
+ * decoder's own calls decide the model keys bin by bin (recode.cpp:1435-1449); here the device's
+ * parse (avr_walker.h) has decided every bin, key and coding-type event before the first callback,
+ * and the callbacks only replay and verify it.  A caller whose decoder parses a slice differently
+ * (another FFmpeg revision's syntax handling, a damaged stream it conceals) is refused with
+ * AVR_ERR_FORMAT instead of being followed; and the streaming session does not take the chained
+ * model (AVR_ERR_INVALID_ARGUMENT). */
 typedef struct avr_hooks_session avr_hooks_session;
 
 /* CodingType (EACH_PIP_CODING_TYPE, recode.cpp:616) */

@@ -44,6 +44,7 @@ def test_bench_default_mode_two_ranks():
     assert line["scaling"] == "weak" and line["value"] > 0
     assert line["corpus"]["n_gpus"] == 2
     assert all(line["corpus"][m]["bit_exact"] is True for m in ("R", "P", "C"))
+    assert "chains" in line["corpus"]["C_split"]   # C: each file's chains over both ranks
     # the configs[3] leg sharded over both ranks inside the default run
     st = line["stream_shard"]
     assert st["n_gpus"] == 2 and st["bit_exact"] is True and st["config"]["slices"] == 30
