@@ -596,10 +596,12 @@ struct ParsedFile {
 
 // views: slices without emulation-prevention bytes point into `in` instead of holding a copy (the
 // caller keeps `in` alive while it uses pf)
-int parse_file(avr_ctx* c, const uint8_t* in, size_t n, ParsedFile* pf, bool views = false) {
+int parse_file(avr_ctx* c, const uint8_t* in, size_t n, ParsedFile* pf, bool views = false,
+               const avr::SkipRanges* skips = nullptr) {
   std::vector<avr::NalRef> nals;
-  if (!avr::demux(in, n, &nals)) return fail(c, AVR_ERR_FORMAT, "not an MP4/avcC or Annex-B H.264 stream");
+  if (!avr::demux(in, n, &nals, skips)) return fail(c, AVR_ERR_FORMAT, "not an MP4/avcC or Annex-B H.264 stream");
   avr::StreamParser sp;
+  sp.set_skips(in, skips);
   for (auto& nr : nals) {
     avr::SliceInfo s;
     if (sp.next(in + nr.offset, nr.size, &s, views)) {
@@ -1186,6 +1188,8 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
     }
   }
   j->stream.resize(total);
+  // the surrogate fills: no 0x00 / 0x03 byte in them ('X'), so the parse steps over them
+  avr::SkipRanges skips;
   {
     std::vector<avr::PbCopy> fills;
     fills.reserve(j->blocks.size());
@@ -1197,14 +1201,16 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
       } else if (b.has_cabac) {
         avr::surrogate_marker(seq++, j->stream.data() + at);
         fills.push_back({at + 8, nullptr, (size_t)b.size - 8});
+        if (b.size > 8) skips.push_back({at + 8, at + (size_t)b.size});
         at += (size_t)b.size;
       }
     }
     parallel_copies(fills, j->stream.data(), (uint8_t)'X');
   }
+  static_assert('X' != 0 && 'X' != 3, "surrogate fill: no start-code or emulation-prevention byte");
   if (tm) fprintf(stderr, "setup: pb+stream %.3f s\n", now_s() - t0), t0 = now_s();
   ParsedFile pf;
-  if (int r = parse_file(c, j->stream.data(), j->stream.size(), &pf, /*views=*/true)) return r;
+  if (int r = parse_file(c, j->stream.data(), j->stream.size(), &pf, /*views=*/true, &skips)) return r;
   if (tm) fprintf(stderr, "setup: parse %.3f s\n", now_s() - t0), t0 = now_s();
   // recognize_coded_block (recode.cpp:1546-1573): slices claim coded blocks in order
   j->desc_of_block.assign(j->blocks.size(), -1);

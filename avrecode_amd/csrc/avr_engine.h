@@ -81,7 +81,11 @@ __device__ __noinline__ uint32_t in_fill_call(uint8_t* lds, const uint8_t* g, ui
 #pragma unroll
   for (int k = 0; k < per; k++) {
     uint32_t i = base + k;
+#ifdef AVR_NT_IN
+    lds[per * lane + k] = i < limit ? __builtin_nontemporal_load(&g[i]) : 0;
+#else
     lds[per * lane + k] = i < limit ? g[i] : 0;
+#endif
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("" ::: "memory");
@@ -108,7 +112,11 @@ struct OutStream {
   uint32_t last;       // last byte emitted
 };
 __device__ __forceinline__ void out_byte(OutStream& o, uint32_t v) {
+#ifdef AVR_NT_OUT
+  if (o.n < o.cap && __lane_id() == 0) __builtin_nontemporal_store((uint8_t)v, &o.g[o.n]);
+#else
   if (o.n < o.cap && __lane_id() == 0) o.g[o.n] = (uint8_t)v;
+#endif
   o.n++;
   o.last = v & 0xff;
 }

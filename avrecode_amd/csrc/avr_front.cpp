@@ -4,6 +4,7 @@
 // decides init_decoder's (buf, size), recode.cpp:143).
 #include "avr_front.h"
 
+#include <algorithm>
 #include <cstring>
 
 namespace avr {
@@ -513,14 +514,39 @@ size_t scan_start(const uint8_t* f, size_t n, size_t k, bool zero3) {
   return n;
 }
 
-void demux_annexb(const uint8_t* f, size_t n, std::vector<NalRef>* nals) {
-  size_t i = scan_start(f, n, 0, false);
+// scan_start over f with skip ranges: the same answer, without reading the ranges (a start code
+// needs a 0x00 at j and j + 1 and a 0x00 / 0x01 at j + 2, and the ranges hold none of those --
+// the surrogate fill is 'X', its marker stays outside the range).  *r: the first range not yet
+// passed (scans only move forward).
+size_t scan_start_skip(const uint8_t* f, size_t n, size_t k, bool zero3, const SkipRanges& sk, size_t* r) {
+  while (k + 3 <= n) {
+    while (*r < sk.size() && sk[*r].second <= k) ++*r;
+    if (*r < sk.size() && sk[*r].first <= k) {   // inside a range: continue at its end
+      k = sk[*r].second;
+      continue;
+    }
+    const size_t lim = *r < sk.size() ? std::min(n, sk[*r].first + 2) : n;   // a code may end 2 bytes in
+    const size_t j = scan_start(f, lim, k, zero3);
+    if (j < lim) return j;
+    if (lim == n) return n;
+    k = std::max(k, lim - 2);
+    if (*r < sk.size() && k < sk[*r].second) k = sk[*r].second;
+  }
+  return n;
+}
+
+void demux_annexb(const uint8_t* f, size_t n, std::vector<NalRef>* nals, const SkipRanges* skips) {
+  size_t r = 0;
+  auto scan = [&](size_t k, bool zero3) {
+    return skips ? scan_start_skip(f, n, k, zero3, *skips, &r) : scan_start(f, n, k, zero3);
+  };
+  size_t i = scan(0, false);
   while (i + 3 <= n) {
-    const size_t start = i + 3, j = scan_start(f, n, start, true);
+    const size_t start = i + 3, j = scan(start, true);
     size_t end = j + 3 <= n ? j : n;
     while (end > start && f[end - 1] == 0) end--;
     if (end > start) nals->push_back({start, end - start});
-    i = scan_start(f, n, j, false);
+    i = scan(j, false);
   }
 }
 
@@ -531,11 +557,27 @@ bool is_mp4(const uint8_t* file, size_t n) {
                     rd32(file + 4) == fourcc("mdat") || rd32(file + 4) == fourcc("free"));
 }
 
-bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals) {
+bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals, const SkipRanges* skips) {
   nals->clear();
   if (is_mp4(file, n)) return demux_mp4(file, n, nals) && !nals->empty();
-  demux_annexb(file, n, nals);
+  demux_annexb(file, n, nals, skips);
   return !nals->empty();   // nothing H.264 in it: av_decoder::run throws (recode.cpp:92-93)
+}
+
+// has_epb over the NAL's bytes outside the skip ranges: exact, since a 00 00 03 cannot touch a
+// range's bytes (neither 0x00 nor 0x03 occurs in them)
+bool StreamParser::nal_has_epb(const uint8_t* src, size_t n) const {
+  if (!skips_ || src < skip_base_) return has_epb(src, n);
+  const size_t a = (size_t)(src - skip_base_), b = a + n;
+  const SkipRanges& sk = *skips_;
+  size_t r = (size_t)(std::upper_bound(sk.begin(), sk.end(), std::make_pair(a, ~(size_t)0)) - sk.begin());
+  if (r > 0 && sk[r - 1].second > a) r--;   // a range that starts before the NAL and reaches into it
+  size_t k = a;
+  for (; r < sk.size() && sk[r].first < b; r++) {
+    if (sk[r].first > k && has_epb(skip_base_ + k, sk[r].first - k)) return true;
+    k = std::max(k, sk[r].second);
+  }
+  return k < b && has_epb(skip_base_ + k, b - k);
 }
 
 bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s, bool views) {
@@ -543,7 +585,7 @@ bool StreamParser::next(const uint8_t* nal, size_t n, SliceInfo* s, bool views) 
   const int type = nal[0] & 0x1f, ref_idc = (nal[0] >> 5) & 3;
   if (type != 1 && type != 5 && type != 6 && type != 7 && type != 8) return false;
   // a slice NAL without emulation-prevention bytes is its own RBSP: no copy when views are allowed
-  const bool view = views && (type == 1 || type == 5) && !has_epb(nal + 1, n - 1);
+  const bool view = views && (type == 1 || type == 5) && !nal_has_epb(nal + 1, n - 1);
   std::vector<uint8_t> rbsp = view ? std::vector<uint8_t>() : unescape(nal + 1, n - 1);
   const uint8_t* rd = view ? nal + 1 : rbsp.data();
   const size_t rn = view ? n - 1 : rbsp.size();

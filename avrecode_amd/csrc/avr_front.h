@@ -5,6 +5,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace avr {
@@ -57,7 +58,12 @@ struct NalRef {
 };
 
 // MP4 (avcC) or Annex-B; returns false on a malformed container.
-bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals);
+// Byte ranges [first, second) of a buffer, sorted, known to hold no 0x00 and no 0x03 byte (the
+// decompressor's surrogate fill, read_packet's stream): no start code and no emulation-prevention
+// byte can begin, end or lie in them, so the Annex-B scan and the emulation-prevention check step
+// over them instead of reading them.
+typedef std::vector<std::pair<size_t, size_t>> SkipRanges;
+bool demux(const uint8_t* file, size_t n, std::vector<NalRef>* nals, const SkipRanges* skips = nullptr);
 bool is_mp4(const uint8_t* file, size_t n);
 // The video track's layout in an MP4 file: the avcC parameter sets and every sample's (offset,
 // size) in decode order, from the moov box's sample tables -- what the mov demuxer knows before
@@ -78,8 +84,13 @@ class StreamParser {
   // NAL without emulation-prevention bytes is not copied (SliceInfo::view points into nal, which
   // must outlive *s).
   bool next(const uint8_t* nal, size_t n, SliceInfo* s, bool views = false);
+  // the NALs passed to next() lie in base[...] with these skip ranges (demux's)
+  void set_skips(const uint8_t* base, const SkipRanges* skips) { skip_base_ = base, skips_ = skips; }
 
  private:
+  bool nal_has_epb(const uint8_t* nal, size_t n) const;
+  const uint8_t* skip_base_ = nullptr;
+  const SkipRanges* skips_ = nullptr;
   Sps sps_[32];
   Pps pps_[256];
   int x264_build_ = -1;

@@ -484,6 +484,8 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
     # capacity, in practice ~ the stream), sized on the first step
     total_c = len(data) + (1 << 24)
 
+    bins_c = 0   # CABAC bins of this rank's compress (the last step's)
+
     def step(ev, ph):
         marks = [time.perf_counter()]
 
@@ -499,6 +501,8 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
         stream.synchronize()
         mark("compress_s")
         res = batch.results("c")
+        nonlocal bins_c
+        bins_c = int(res["bins"].sum())
         offs = d_off[:n_mine].cpu().numpy().astype(np.int64)
         ok_c = res["status"] == 0
         lens = np.where(ok_c, res["out_len"], 0).astype(np.int64)
@@ -594,7 +598,8 @@ def stream_shard_leg(ctx, args, seconds, world, rank, dev, with_cpu):
                    "seconds": seconds, "fps": 30, "mb": list(args.stream_mb), "slices": len(ps.descs),
                    "stream_bytes": len(data), "container_bytes": len(avrc), "model": "parallel",
                    "parallelism": f"slice ranges over {world} GPU(s)", "payload_bytes_S_rank0": S,
-                   "recoded_bytes_C_rank0": C, "compress_ms": t_comp * 1e3, "decompress_ms": t_dec * 1e3,
+                   "recoded_bytes_C_rank0": C, "bins_rank0": bins_c, "compress_ms": t_comp * 1e3,
+                   "decompress_ms": t_dec * 1e3,
                    "coder": "arithmetic_code<uint64_t,uint8_t>",
                    "setup_s_rank0": {k: round(v, 3) for k, v in setup.items()},
                    "setup_by_rank": setup_by_rank,

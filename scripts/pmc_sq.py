@@ -12,7 +12,9 @@ from collections import defaultdict
 
 # progressive-slice kernels of the u64 coder (template <MODE, FLD, P32> since round 4; the
 # field-capable instantiations return at once on a progressive batch)
-KERNELS = {"slices_parallel_kernel<0, false, false>": "compress", "slices_parallel_kernel<1, false, false>": "decompress"}
+# (the resident kernel of the headline batch, the persistent queue kernel of the configs[3] stream)
+KERNELS = {"slices_parallel_kernel<0, false, false>": "compress", "slices_parallel_kernel<1, false, false>": "decompress",
+           "slices_queue_kernel<0, false, false>": "compress", "slices_queue_kernel<1, false, false>": "decompress"}
 
 
 def main():

@@ -225,3 +225,28 @@ def test_parse_range_equals_subset(name):
         if hi > lo:
             assert a.arena.tobytes()[:len(b.arena)] == b.arena.tobytes()
         assert a.work_len == b.work_len
+
+
+@pytest.mark.parametrize("name", ["paff_ipp.264", "mbaff_ib.264"])
+def test_dec_plan_of_annexb_containers(name):
+    """An Annex-B container's plan (decompressor::run's read_packet parse, recode.cpp:1338-1409):
+    the surrogate fills are stepped over by the start-code scan and the emulation-prevention check
+    (avr_front SkipRanges), and the slices it finds carry the headers of the original file's coded
+    slices, in order; the splice restores the file."""
+    from _oracle import oracle_cli
+    import test_assembly_scaling as tas
+    data = (FIX / name).read_bytes()
+    ps = avr.parse_stream(data)
+    avrc = oracle_cli("compress", FIX / name, mode="P")
+    h = avr.DecompressPlan().load(avrc)
+    mine = [k for k, f in enumerate(tas._layout_of(avrc)) if f is not None]   # the coded slices
+    assert len(mine) == h.n_slices > 0
+    hdr = ("slice_type", "slice_qp", "cabac_init_idc", "first_mb", "mb_width", "mb_height", "picture_id",
+           "structure", "transform_8x8_mode", "num_ref_idx_l0", "num_ref_idx_l1")
+    for j, k in enumerate(mine):
+        for f in hdr:
+            assert h.descs[j][f] == ps.descs[k][f], (name, j, k, f)
+    pays = _container_payloads(data, avrc)
+    lens = np.array([len(p) for p in pays], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    assert h.splice(np.zeros(len(pays), np.int32), b"".join(pays), offs, lens).tobytes() == data
