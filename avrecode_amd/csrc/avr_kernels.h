@@ -19,7 +19,7 @@ constexpr int kEstLog = kEstTable + 2;
 constexpr int kEstLogCap = 8191;
 constexpr uint32_t kEstLogOverflow = 0xffffffffu;
 // then, for the progressive parallel kernels of wide launches (kFlagMringGlobal), the upper row's
-// model bytes (Walker::mring: 52 B per macroblock column, up to kMringCols columns)
+// model bytes (Walker::mring: 28 B per macroblock column -- 52 reserved -- up to kMringCols columns)
 constexpr int kEstMring = kEstLog + 2 * kEstLogCap;
 constexpr int kMringCols = 288;
 constexpr int kEstGlobal = kEstMring + kMringCols * 26;

@@ -129,10 +129,14 @@ struct EdgeRec {
 };
 static_assert(sizeof(EdgeRec) == 92, "EdgeRec layout");
 // The progressive walkers' ring holds EdgeRec's first ten dwords only (the parse's neighbour
-// fields); the 52 model bytes of each column (EdgeRec::mnnz, read by the NZ-tree keys of the
-// parallel model) live in a row of their own, `mring` (13 dwords per column): in LDS after the
-// ring, or -- when that is what lets four wide workgroups share a CU's LDS (4K: 240 columns x 92 B
-// would leave room for three) -- in the workgroup's global scratch (kFlagMringGlobal).
+// fields); the model bytes of each column (EdgeRec::mnnz, read by the NZ-tree keys of the parallel
+// model) live in a row of their own, `mring`: in LDS after the ring, or -- when that is what lets
+// four wide workgroups share a CU's LDS (4K: 240 columns x 92 B would leave room for three) -- in
+// the workgroup's global scratch (kFlagMringGlobal).  Only the upper macroblock's bottom-row
+// blocks and DC entries are ever read there (get_neighbor_sub_mb's upper neighbours: mnnz bytes
+// 8-15, 24-31, 40-50, i.e. dwords 2, 3, 6, 7, 10, 11, 12 -- tests/test_oracle_geometry.py checks
+// the table), so a column keeps those 7 dwords, dword d at ((d >> 2) << 1) | (d & 1): 28 B instead
+// of 52 (round 6: the 4K stream's model-row write-backs were most of its HBM writes).
 struct EdgeCore {
   uint8_t flags, pad;
   uint16_t cbp;
@@ -142,7 +146,9 @@ struct EdgeCore {
   uint8_t direct8[2], pad2[2];
 };
 static_assert(sizeof(EdgeCore) == 40 && offsetof(EdgeRec, mnnz) == 40, "EdgeCore = EdgeRec's first ten dwords");
-constexpr int kMringDwords = 13;   // per column: EdgeRec::mnnz
+constexpr int kMringDwords = 7;      // per column: the read dwords of EdgeRec::mnnz
+constexpr uint32_t kMringUsed = 0x1CCCu;   // those dwords (2, 3, 6, 7, 10, 11, 12) of the 13
+AVR_FI uint32_t mring_dword(uint32_t d) { return (d >> 2) << 1 | (d & 1); }
 static_assert(sizeof(MbRec) == 180, "MbRec layout (dword map in Walker::edge_src)");
 
 // LDS layout (per workgroup = one slice); the ring is sized by mb_width at launch.
@@ -1268,7 +1274,7 @@ struct Walker {
       return (top_ok | mbaff) ? ring[mb_x].mnnz[idx] : 0;   // MBAFF: the view holds the model's upper macroblock
     } else {
       if (!top_ok) return 0;
-      const uint32_t at = (uint32_t)mb_x * (kMringDwords * 4) + (uint32_t)idx;
+      const uint32_t at = (uint32_t)mb_x * (kMringDwords * 4) + mring_dword((uint32_t)idx >> 2) * 4 + ((uint32_t)idx & 3);
       if (mring_global) return ((const __attribute__((address_space(1))) uint8_t*)mring)[at];
       return ((const __attribute__((address_space(3))) uint8_t*)mring)[at];
     }
@@ -2221,8 +2227,8 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
           if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
         } else {
           if (lane < 10) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
-          else if (!RM && lane < 10 + kMringDwords) {   // the model row (RM reads the frame instead)
-            const uint32_t at = (uint32_t)w.mb_x * kMringDwords + (lane - 10);
+          else if (!RM && lane < 23 && ((kMringUsed >> (lane - 10)) & 1)) {   // the model row (RM reads the frame)
+            const uint32_t at = (uint32_t)w.mb_x * kMringDwords + mring_dword((uint32_t)lane - 10);
             if (w.mring_global) ((__attribute__((address_space(1))) uint32_t*)w.mring)[at] = ev;
             else ((__attribute__((address_space(3))) uint32_t*)w.mring)[at] = ev;
           }

@@ -18,10 +18,18 @@ NAMES = ["slice", "mb_syntax", "residual", "map_decode", "nnz_bins", "map_recode
 def main():
     import avrecode_amd as avr
     path = sys.argv[1] if len(sys.argv) > 1 else str(ROOT / "tests/fixtures/cockatoo.mp4")
-    data = Path(path).read_bytes()
     L = avr.lib()
     buf = (ctypes.c_ulonglong * 64)()
     with avr.Context(0) as ctx:
+        if path == "clip":   # BASELINE configs[1]: bench.make_clip (1080p, 64 frames, I + 31 P twice)
+            sys.path.insert(0, str(ROOT))
+            import bench
+
+            class A:
+                mb_width, mb_height = 120, 68
+            data = bench.make_clip(ctx, A)
+        else:
+            data = Path(path).read_bytes()
         avrc = ctx.compress(data, avr.MODEL_REFERENCE)
         L.avr_debug_profile(4, buf)
         t0 = time.perf_counter()

@@ -83,3 +83,15 @@ def test_table_check_detects_a_wrong_entry():
     broken = bytearray(nb_up)
     broken[5] ^= 1
     assert check_table(nb_left, bytes(broken))
+
+
+def test_upper_neighbours_read_only_the_kept_model_row_dwords():
+    """The parallel model's walkers keep, per macroblock column, only the model bytes an upper
+    neighbour lookup can reach (avr_walker.h kMringUsed: mnnz dwords 2, 3, 6, 7, 10, 11, 12).
+    Pinned by the reference's own answer: every upper neighbour recode.cpp:233-471 returns in the
+    macroblock above (tests/golden/geometry.json) lies in those dwords."""
+    kept = {2, 3, 6, 7, 10, 11, 12}
+    assert sum(1 << d for d in kept) == 0x1CCC
+    reached = {oidx // 4 for above, size, idx, x, y, ok, ox, oy, oidx in GOLD["neighbors"]
+               if above and ok and oy == y - 1}
+    assert reached and reached <= kept, sorted(reached - kept)
