@@ -147,6 +147,7 @@ struct EdgeCore {
 };
 static_assert(sizeof(EdgeCore) == 40 && offsetof(EdgeRec, mnnz) == 40, "EdgeCore = EdgeRec's first ten dwords");
 constexpr int kMringDwords = 7;      // per column: the read dwords of EdgeRec::mnnz
+constexpr uint32_t kEdgeMringNz = 0x200u;   // EdgeCore dword 0: the column's model row was stored (global row)
 constexpr uint32_t kMringUsed = 0x1CCCu;   // those dwords (2, 3, 6, 7, 10, 11, 12) of the 13
 AVR_FI uint32_t mring_dword(uint32_t d) { return (d >> 2) << 1 | (d & 1); }
 static_assert(sizeof(MbRec) == 180, "MbRec layout (dword map in Walker::edge_src)");
@@ -1275,7 +1276,7 @@ struct Walker {
     } else {
       if (!top_ok) return 0;
       const uint32_t at = (uint32_t)mb_x * (kMringDwords * 4) + mring_dword((uint32_t)idx >> 2) * 4 + ((uint32_t)idx & 3);
-      if (mring_global) return ((const __attribute__((address_space(1))) uint8_t*)mring)[at];
+      if (mring_global) return (tf & kEdgeMringNz) ? ((const __attribute__((address_space(1))) uint8_t*)mring)[at] : 0;
       return ((const __attribute__((address_space(3))) uint8_t*)mring)[at];
     }
   }
@@ -2226,11 +2227,19 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
         if constexpr (FLD) {
           if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
         } else {
-          if (lane < 10) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;   // dword 0: flags, pad, cbp
+          // a model row in global scratch: a column whose kept model bytes are all zero (a skipped or
+          // residual-free bottom row) is not stored; bit 9 of the edge's dword 0 (EdgeCore::pad)
+          // says which, and the lookups under it read zero without a load (4K P-slices: most rows)
+          const bool mz = !RM && w.mring_global &&
+                          __ballot(lane >= 10 && lane < 23 && ((kMringUsed >> (lane - 10)) & 1) && ev != 0) != 0;
+          if (lane < 10) e32[lane] = lane == 0 ? ((w.cf & 0xffff017fu) | (mz ? kEdgeMringNz : 0u)) : ev;
           else if (!RM && lane < 23 && ((kMringUsed >> (lane - 10)) & 1)) {   // the model row (RM reads the frame)
             const uint32_t at = (uint32_t)w.mb_x * kMringDwords + mring_dword((uint32_t)lane - 10);
-            if (w.mring_global) ((__attribute__((address_space(1))) uint32_t*)w.mring)[at] = ev;
-            else ((__attribute__((address_space(3))) uint32_t*)w.mring)[at] = ev;
+            if (w.mring_global) {
+              if (mz) ((__attribute__((address_space(1))) uint32_t*)w.mring)[at] = ev;
+            } else {
+              ((__attribute__((address_space(3))) uint32_t*)w.mring)[at] = ev;
+            }
           }
         }
         w.lf = w.cf;

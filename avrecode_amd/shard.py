@@ -155,8 +155,9 @@ def gather_blocks(local: list[bytes], status: list[int], dst: int = 0, device=No
     return gather_flat(flat, status, offs, lens, dst=dst, device=dev, out=out)
 
 
-def subset(ps: ParsedStream, lo: int, hi: int) -> ParsedStream:
-    """The slices [lo, hi) of a parsed stream as a self-contained batch (offsets rebased)."""
+def subset(ps: ParsedStream, lo: int, hi: int, copy_arena: bool = True) -> ParsedStream:
+    """The slices [lo, hi) of a parsed stream as a self-contained batch (offsets rebased).
+    copy_arena False: the arena is a view of ps.arena's range (valid while ps.arena is)."""
     d = ps.descs[lo:hi].copy()
     if len(d) == 0:
         return ParsedStream(d, np.zeros(16, np.uint8), 0, ps.max_mb_width, ps.max_mb_height)
@@ -166,7 +167,8 @@ def subset(ps: ParsedStream, lo: int, hi: int) -> ParsedStream:
     w1 = int(d[-1]["out_offset"]) + ((int(d[-1]["out_capacity"]) + 15) & ~15)
     d["payload_offset"] -= a0
     d["out_offset"] -= w0
-    return ParsedStream(d, ps.arena[a0:a1].copy(), w1 - w0, ps.max_mb_width, ps.max_mb_height)
+    arena = ps.arena[a0:a1]
+    return ParsedStream(d, arena.copy() if copy_arena else arena, w1 - w0, ps.max_mb_width, ps.max_mb_height)
 
 
 def sharded_compress(ctx, data: bytes, device=None, ps: ParsedStream | None = None,
@@ -335,18 +337,24 @@ def scatter_parsed(ps: "ParsedStream | None", ranges, device, src: int = 0):
     rank, world = dist.get_rank(), dist.get_world_size()
     if rank == src:
         mine = None
+        pending = []   # every rank's messages in flight at once (each peer has its own xGMI link)
         for r in range(world):
             lo, hi = ranges[r]
-            sub = ps if (lo, hi) == (0, len(ps.descs)) else subset(ps, lo, hi)
+            sub = ps if (lo, hi) == (0, len(ps.descs)) else subset(ps, lo, hi, copy_arena=r == rank)
             if r == rank:
                 mine = sub
                 continue
             hdr = torch.tensor([hi - lo, sub.arena.nbytes, sub.work_len, sub.max_mb_width, sub.max_mb_height],
                                dtype=torch.int64, device=device)
-            dist.send(hdr, r)
+            msgs = [hdr]
             if hi > lo:
-                dist.send(torch.from_numpy(np.ascontiguousarray(sub.descs).view(np.uint8).reshape(-1)).to(device), r)
-                dist.send(torch.from_numpy(sub.arena).to(device), r)
+                # the arena range is a view of rank src's (pinned) arena: one DMA to the device
+                msgs.append(torch.from_numpy(np.ascontiguousarray(sub.descs).view(np.uint8).reshape(-1)).to(device))
+                msgs.append(torch.from_numpy(sub.arena).to(device, non_blocking=True))
+            for t in msgs:
+                pending.append((dist.isend(t, r), t))
+        for w, _ in pending:
+            w.wait()
         return (mine.descs, mine.arena, len(mine.descs), mine.work_len, mine.max_mb_width, mine.max_mb_height)
     hdr = torch.zeros(5, dtype=torch.int64, device=device)
     dist.recv(hdr, src)
