@@ -3077,7 +3077,7 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
 
 int avr_hooks_compress_stream_begin(avr_ctx* c, int model, avr_hooks_session** out) {
   if (!c || !out) return AVR_ERR_INVALID_ARGUMENT;
-  if (!valid_model(model) || model == AVR_MODEL_CHAINED) return AVR_ERR_INVALID_ARGUMENT;   // whole-file sessions only
+  if (!valid_model(model)) return AVR_ERR_INVALID_ARGUMENT;
   *out = nullptr;
   avr_hooks_session* hs = new (std::nothrow) avr_hooks_session;
   if (!hs) return AVR_ERR_OUT_OF_MEMORY;

@@ -62,9 +62,10 @@ typedef enum {
  * 16 slices: realshort.mp4 0.998, cockatoo.mp4 0.994 of the input, against 0.990 / 0.991 for the
  * reference model and 1.041 / 1.010 for the parallel one), and a file's chains decode on as many
  * workgroups at once.  Whole-file calls only (avr_compress_file(s), avr_decompress_file(s),
- * avr_roundtrip_file(s), the whole-file hooks sessions, and the per-rank chain ranges of one file,
- * avr_compress_chain_range / avr_decompress_chain_range); the device slice-batch calls and the
- * streaming hooks session refuse it with AVR_ERR_INVALID_ARGUMENT. */
+ * avr_roundtrip_file(s), the hooks sessions -- the streaming one makes its container at
+ * avr_hooks_end from the complete file, as for the reference model -- and the per-rank chain
+ * ranges of one file, avr_compress_chain_range / avr_decompress_chain_range); the device
+ * slice-batch calls refuse it with AVR_ERR_INVALID_ARGUMENT. */
 typedef enum { AVR_MODEL_REFERENCE = 0, AVR_MODEL_PARALLEL = 1, AVR_MODEL_PARALLEL32 = 2, AVR_MODEL_CHAINED = 3 } avr_model;
 #define AVR_CHAIN_SLICES 16
 
@@ -398,8 +399,7 @@ int avr_neighbor_tables(avr_ctx* ctx, uint8_t out[96]);
  * parse (avr_walker.h) has decided every bin, key and coding-type event before the first callback,
  * and the callbacks only replay and verify it.  A caller whose decoder parses a slice differently
  * (another FFmpeg revision's syntax handling, a damaged stream it conceals) is refused with
- * AVR_ERR_FORMAT instead of being followed; and the streaming session does not take the chained
- * model (AVR_ERR_INVALID_ARGUMENT). */
+ * AVR_ERR_FORMAT instead of being followed. */
 typedef struct avr_hooks_session avr_hooks_session;
 
 /* CodingType (EACH_PIP_CODING_TYPE, recode.cpp:616) */

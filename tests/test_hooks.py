@@ -131,7 +131,7 @@ def test_hooks_field_streams(name, mode, model):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["paff_ipp.264", "mbaff_ib.264", "realshort.mp4"])
-@pytest.mark.parametrize("mode,model", [("R", 0), ("P", 1)])
+@pytest.mark.parametrize("mode,model", [("R", 0), ("P", 1), ("C", 3)])
 def test_hooks_streaming_compress(name, mode, model):
     """A streaming session: the driver hands the file to avr_hooks_feed only as far as the slice it
     is about to decode (Annex-B: through that slice's NAL unit, in two pieces; MP4 with its moov
