@@ -32,6 +32,8 @@ I + 31 P twice, QP 26) -- in both model modes, with the CPU oracle's R-mode sing
 beside each, and each call's phase breakdown (demux / upload / kernels / download / container).
 corpus: BASELINE configs[4] (N=1: one batch per model; N>1: files dealt to ranks, LPT by bytes).
 rmode_files (N=1): the reference model over 256 heterogeneous files at once.
+rmode_clips (N=1): the reference model over 512 copies of a real x264 clip, beside the CPU oracle on
+every host thread.
 stream_shard: BASELINE configs[3] at full length (--stream-leg-seconds, default the config's 600 s of
 4K, 18,000 slices, 4.47 GB), one timed step of the sharded container roundtrip, with its own
 roofline (and, at N=1, a CPU baseline); at N > 1 the stream is sharded over the ranks (strong
@@ -329,6 +331,39 @@ def corpus_section(ctx, args):
             tot += sum(cpu)
         if tot:
             rec["cpu_oracle_R_1core"] = {"MB_s": total / tot / 1e6, "wall_s": tot, "cores": 1, "kind": "port"}
+    return rec
+
+
+def rmode_clips_section(ctx, args):
+    """The reference model's throughput on a library of short real clips: args.rclips copies of the
+    x264 fixture realshort.mp4 (97 KB, 36 slices) as independent files through avr_compress_files /
+    avr_decompress_files (the same calls as rmode_files), next to the CPU oracle's R-mode roundtrip
+    of the same files on every host thread in the same run.  Each file is one serial chain of the
+    reference model (recode.cpp:662-665) on either side; the GPU runs hundreds of chains at once."""
+    import avrecode_amd as avr
+    clip = (ROOT / "tests" / "fixtures" / "realshort.mp4").read_bytes()
+    datas = [clip] * args.rclips
+    total = sum(map(len, datas))
+    walls, tc, td = [], [], []
+    for it in range(1 + args.file_reps):
+        t0 = time.perf_counter()
+        outs = ctx.compress_files(datas, avr.MODEL_REFERENCE)
+        t1 = time.perf_counter()
+        back = ctx.decompress_files(outs)
+        t2 = time.perf_counter()
+        assert back == datas, "R-mode clips: decompress did not restore every file"
+        if it == 0:
+            continue   # warm-up (buffer allocation)
+        walls.append(t2 - t0)
+        tc.append(t1 - t0)
+        td.append(t2 - t1)
+    k = sorted(range(len(walls)), key=walls.__getitem__)[len(walls) // 2]
+    progress(f"R-mode clips: {total / walls[k] / 1e6:.2f} MB/s")
+    rec = {"files": len(datas), "file": "tests/fixtures/realshort.mp4 (x264, 36 slices)", "bytes": total,
+           "model": "reference (R)", "MB_s": total / walls[k] / 1e6, "wall_s": walls[k], "compress_s": tc[k],
+           "decompress_s": td[k], "avrc_bytes": sum(map(len, outs)), "bit_exact": True}
+    if not args.no_cpu_baseline:
+        rec["cpu_baseline"] = rmode_files_cpu(datas)
     return rec
 
 
@@ -909,6 +944,7 @@ def main():
     ap.add_argument("--no-corpus", action="store_true", help="skip the configs[4] corpus")
     ap.add_argument("--corpus-scale", type=float, default=1.0)
     ap.add_argument("--rfiles", type=int, default=256, help="files in the R-mode many-files leg (0: skip)")
+    ap.add_argument("--rclips", type=int, default=512, help="copies of realshort.mp4 in the R-mode clips leg (0: skip)")
     ap.add_argument("--stream-leg-seconds", type=int, default=600,
                     help="length of the configs[3] stream leg of the default run (0: skip)")
     ap.add_argument("--no-p32", action="store_true", help="skip the P32-coder extra measurement")
@@ -1051,6 +1087,8 @@ def main():
             line["corpus"] = corpus_section(ctx, args)
         if world == 1 and args.rfiles > 0 and not args.no_files:
             line["rmode_files"] = rmode_files_section(ctx, args)
+        if world == 1 and args.rclips > 0 and not args.no_files:
+            line["rmode_clips"] = rmode_clips_section(ctx, args)
     if world > 1 and not args.no_corpus:
         rec = corpus_sharded(ctx, args, world, rank, dev)
         if rank == 0:
