@@ -230,12 +230,26 @@ typedef struct {
   void (*end_sub_mb)(void *opaque, int cat, int scan8index, int max_coeff, int is_dc, int chroma422);
   void (*begin_coding_type)(void *opaque, avr_coding_type ct, int zigzag_index, int param0, int param1);
   void (*end_coding_type)(void *opaque, avr_coding_type ct);
+  /* NOT a reference hook (optional, NULL: not called): the start of a macroblock row of a progressive
+   * frame slice other than its first macroblock, before that row's mb_xy -- where the parallel
+   * model's long-slice split may begin a piece (avr_seam_t below).  state: the 1024 CABAC context
+   * bytes; edge_row: AVR_EDGE_BYTES per column, the upper row's bottom edges (avr_edge_row);
+   * last_dqp_nz: the previous macroblock's mb_qp_delta != 0. */
+  void (*row_start)(void *opaque, int mb_addr, const uint8_t *state, const uint8_t *edge_row, int last_dqp_nz);
 } avr_hooks_t;
 
 /* Parse slice_data() of one slice, pulling every bin through hooks.  The parser owns the     */
 /* 1024 CABAC context bytes (FFmpeg's sl->cabac_state).  Returns 0 on success (end_of_slice   */
 /* reached at a legal MB), <0 on a syntax error / unsupported syntax / overrun.               */
 int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int picture_id);
+/* One piece of a split slice (avr_seam_t): the walk from start_mb (a row start) for n_mbs
+ * macroblocks (0: to end_of_slice), the CABAC contexts, the upper row and last_dqp_nz from the
+ * seam (edge == NULL: the slice's own start).  Returns 1 when it stopped after n_mbs. */
+typedef struct {
+  int start_mb, n_mbs, last_dqp_nz;
+  const uint8_t *state, *edge;
+} avr_piece_start_t;
+int avr_walk_piece(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int picture_id, const avr_piece_start_t *ps);
 
 /* ------------------------------------------------------------------------------------------ */
 /* The predictor (recode.cpp:615-1059) and the two drivers                                   */
@@ -286,10 +300,71 @@ int avr_cabac_regenerate(const avr_slice_hdr_t *h, const uint8_t *payload, size_
 long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int check_recodable, int p32, uint8_t **out,
                          size_t *out_len);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Long-slice split of the parallel model (NOT part of the reference: this library's own format,  */
+/* restated here as the checker; avrecode_amd/csrc/avr_api.cpp "seams").  A progressive-frame     */
+/* slice is cut at macroblock-row starts into pieces, each re-coded with a fresh parallel model  */
+/* (its estimators reset, its upper row's model bytes zero, as at a slice start), so that the     */
+/* pieces decompress side by side.  A cut (a "seam") comes at the first row start with at least   */
+/* 8 * split_bytes CABAC bits decoded since the previous seam (or the slice start) and at least   */
+/* 4 * split_bytes bits of the payload still ahead.  Block field 16 ("seams", zlib) carries what   */
+/* a piece's decompressor needs from before it (avr_seams_encode); Block.cabac holds the pieces'   */
+/* re-coded streams one after the other.                                                         */
+#define AVR_EDGE_BYTES 40          /* one column of the upper row: flags | cbp << 16, nnz[3][4] (bottom
+                                    * rows), mvd[2][4][2], ref[2][2], direct8[2], 2 zero bytes */
+#define AVR_SPLIT_BYTES_DEFAULT 131072
+typedef struct {
+  uint32_t first_mb;               /* the piece's first macroblock (a row start) */
+  uint32_t q;                      /* where its regenerated bytes begin in the slice's CABAC bytes */
+  uint32_t last_dqp_nz;
+  /* the CABAC re-encoder at the cut (avr_engine.h CabacEncoder: cache byte, outstanding 0xFF bytes,
+   * low = pending bits + 10-bit window, queue = pending bits - 8, range) */
+  uint32_t ce_low, ce_outstanding, ce_cache, ce_range;
+  int32_t ce_queue;
+  uint8_t state[1024];             /* CABAC context bytes */
+  uint8_t *edge;                   /* AVR_EDGE_BYTES * mb_width (malloc'd) */
+} avr_seam_t;
+/* split_bytes of the whole-file compress (0: no split): AVR_SPLIT_BYTES from the environment, else
+ * AVR_SPLIT_BYTES_DEFAULT; avr_set_split_bytes overrides both */
+size_t avr_split_bytes(void);
+void avr_set_split_bytes(size_t bytes);
+/* The re-encoder's state where the CABAC decoder stands after `bitpos` bits (9 + renormalisation
+ * shifts) with codIOffset `offset` and codIRange `range` on this payload: 0, or -1 when the cut
+ * cannot be placed there (the arithmetic's pending digits reach too far back). */
+int avr_seam_encoder(const uint8_t *payload, size_t n, size_t bitpos, uint32_t offset, uint32_t range,
+                     avr_seam_t *s);
+/* the seams blob: zlib of { u32 1, u32 seams, u32 mb_width, u32 piece_len[seams + 1], per seam
+ * { u32 first_mb, q, last_dqp_nz, ce_low, ce_queue, ce_outstanding, ce_cache, ce_range,
+ * u8 state[1024], u8 edge[40 * mb_width] } }, little-endian */
+int avr_seams_encode(const avr_seam_t *s, int n_seams, int mb_width, const uint32_t *piece_len, obuf_t *out);
+/* parses a seams blob: 0 and *s (malloc'd, n_seams entries), *piece_len (malloc'd, n_seams + 1); -1 */
+int avr_seams_decode(const uint8_t *p, size_t n, int mb_width, avr_seam_t **s, int *n_seams, uint32_t **piece_len);
+void avr_seams_free(avr_seam_t *s, int n_seams);
+/* the device's CABAC re-encoder in byte form (avr_engine.h CabacEncoder), which a piece starts from a
+ * seam's state (s == NULL: a slice start) and ends with avr_ce_seam_flush */
+typedef struct {
+  uint32_t low, range, outstanding, cache;
+  int queue, have_cache, err;
+  obuf_t *out;
+} avr_ce_t;
+void avr_ce_init(avr_ce_t *e, obuf_t *out, const avr_seam_t *s);
+void avr_ce_decision(avr_ce_t *e, int bin, uint8_t *state);
+void avr_ce_bypass(avr_ce_t *e, int bin);
+void avr_ce_terminate(avr_ce_t *e, int bin);
+void avr_ce_seam_flush(avr_ce_t *e);
+/* One piece of a split P-mode slice decompressed on its own, as the device does it: a fresh model on
+ * the piece's stream rc[0..n), the walk from the seam (NULL: the slice start) for n_mbs macroblocks (0:
+ * to the slice's end), the byte-form re-encoder from the seam's state.  *out: the regenerated bytes
+ * from the seam's q (a last piece without its trailing 0x80, recode.cpp:1503-1505). */
+int avr_decompress_piece(const avr_slice_hdr_t *h, int picture_id, const uint8_t *rc, size_t n, const avr_seam_t *seam,
+                         int n_mbs, obuf_t *out);
+/* every split slice of a file (split_bytes) decompressed piece by piece and compared (oracle_recode.c) */
+int avr_check_pieces(const uint8_t *file, size_t n, size_t split_bytes, int *n_split, int *n_pieces);
+
 /* protobuf wire codec for recode.proto */
 typedef struct {
   int64_t size;
-  int has_size, has_literal, has_skip, has_cabac, has_parity, has_last_byte;
+  int has_size, has_literal, has_skip, has_cabac, has_parity, has_last_byte, has_seams;
   int skip_coded, length_parity;
   const uint8_t *literal;
   size_t literal_len;
@@ -297,6 +372,8 @@ typedef struct {
   size_t cabac_len;
   uint8_t last_byte;
   int last_byte_len;
+  const uint8_t *seams;   /* field 16 (this library's parallel-model long-slice split), zlib */
+  size_t seams_len;
 } avr_pb_block_t;
 void avr_pb_put_block(obuf_t *o, const avr_pb_block_t *b);
 /* model mode recorded in Recoded.metadata.version (R-mode: absent, as the reference writes):

@@ -5,6 +5,8 @@
  *   recode_oracle decompress           <input> [output]
  *   recode_oracle roundtrip  [-p|-p32|-c] <input> [output]
  *   recode_oracle slices          <input>          per-slice parse / regeneration report
+ *   recode_oracle pieces          <input>          the parallel model's split slices (AVR_SPLIT_BYTES),
+ *                                                  each piece decompressed on its own, compared
  *
  * -p selects the parallel model (fresh model per slice) on arithmetic_code<uint64_t, uint8_t>, -p32 the
  * parallel model on the P-format coder, -c the reference model in chains of 16 coded slices (a
@@ -134,6 +136,12 @@ int main(int argc, char **argv) {
   uint8_t *file = read_file(in, &n);
   if (!file) { fprintf(stderr, "Failed to open file: %s\n", in); return 1; }
   if (!strcmp(cmd, "slices")) return cmd_slices(file, n);
+  if (!strcmp(cmd, "pieces")) {   /* the parallel model's long-slice split, piece by piece */
+    int ns = 0, np = 0;
+    int bad = avr_check_pieces(file, n, avr_split_bytes(), &ns, &np);
+    printf("split slices %d pieces %d mismatches %d\n", ns, np, bad);
+    return bad != 0;
+  }
   if (!strcmp(cmd, "compress")) {
     uint8_t *o; size_t on;
     if (avr_compress(file, n, mode, &o, &on)) { fprintf(stderr, "compress failed\n"); return 1; }

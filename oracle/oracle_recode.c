@@ -51,6 +51,7 @@ void avr_pb_put_block(obuf_t *o, const avr_pb_block_t *b) {
   if (b->has_cabac) pb_bytes(&m, 4, b->cabac, b->cabac_len);
   if (b->has_parity) { pb_varint(&m, 5 << 3 | 0); pb_varint(&m, (uint64_t)b->length_parity); }
   if (b->has_last_byte) pb_bytes(&m, 6, &b->last_byte, (size_t)b->last_byte_len);
+  if (b->has_seams) pb_bytes(&m, 16, b->seams, b->seams_len);
   pb_bytes(o, 2, m.data, m.len);
   ob_free(&m);
 }
@@ -86,11 +87,12 @@ static int pb_parse_block(const uint8_t *p, const uint8_t *e, avr_pb_block_t *b)
       if (field == 1) { b->has_size = 1; b->size = (int64_t)v; }
       if (field == 3) { b->has_skip = 1; b->skip_coded = v != 0; }
       if (field == 5) { b->has_parity = 1; b->length_parity = v != 0; }
-    } else if (wt == 2 && (field == 2 || field == 4 || field == 6)) {
+    } else if (wt == 2 && (field == 2 || field == 4 || field == 6 || field == 16)) {
       if (pb_rd_varint(&p, e, &v) || (uint64_t)(e - p) < v) return -1;
       if (field == 2) { b->has_literal = 1; b->literal = p; b->literal_len = v; }
       if (field == 4) { b->has_cabac = 1; b->cabac = p; b->cabac_len = v; }
       if (field == 6) { b->has_last_byte = 1; b->last_byte_len = (int)v; b->last_byte = v ? p[0] : 0; }
+      if (field == 16) { b->has_seams = 1; b->seams = p; b->seams_len = v; }
       p += v;
     } else if (pb_skip(&p, e, wt)) {
       return -1;
@@ -154,6 +156,8 @@ fail:
   return -1;
 }
 
+static avr_model_t *model_new_p(int p32);
+
 /* ============================================================ shared model-hook plumbing */
 static void h_frame_spec(void *o, int fn, int w, int h);
 static void h_mb_xy(void *o, int x, int y);
@@ -203,6 +207,15 @@ typedef struct {
   int *bsym, *bctx, nbuf, capbuf;
   int finished;
   size_t bins;
+  /* the parallel model's long-slice split (avr_oracle.h; split_bits = 0: none) */
+  size_t split_bits, last_cut, payload_bits;
+  const uint8_t *payload;
+  size_t payload_n;
+  int picture_id, mb_width, mb_height;
+  avr_model_t *first_model;     /* piece 0's model (the caller's); later pieces' are freed here */
+  avr_seam_t *seams;
+  uint32_t *piece_end;          /* enc_out.len at each seam */
+  int n_seams, cap_seams;
 } cdrv_t;
 
 static size_t c_put(cdrv_t *c, int symbol, model_key_t key) { /* encoder::put of the model's coder */
@@ -256,6 +269,43 @@ static int c_get_terminate(void *o) {
   c_execute_symbol(c, s, K_TERMINATE);
   return s;
 }
+/* a row start: a cut candidate every 8 split_bytes decoded bits (with half a piece still ahead); the
+ * cut happens where the re-encoder's state can be placed (avr_seam_encoder) and moves forward */
+static void c_row_start(void *o, int addr, const uint8_t *state, const uint8_t *edge, int last_dqp_nz) {
+  cdrv_t *c = (cdrv_t *)o;
+  const size_t pos = c->dec.pos;
+  if (!c->split_bits || pos - c->last_cut < c->split_bits || pos + c->split_bits / 2 > c->payload_bits) return;
+  c->last_cut = pos;
+  avr_seam_t t;
+  memset(&t, 0, sizeof(t));
+  if (avr_seam_encoder(c->payload, c->payload_n, pos, c->dec.offset, c->dec.range, &t)) return;
+  if (c->n_seams && t.q <= c->seams[c->n_seams - 1].q) return;
+  if (c->nbuf || c->queueing != PIP_UNKNOWN) abort();   /* no significance map spans a row start */
+  t.first_mb = (uint32_t)addr;
+  t.last_dqp_nz = (uint32_t)last_dqp_nz;
+  memcpy(t.state, state, 1024);
+  t.edge = (uint8_t *)malloc((size_t)AVR_EDGE_BYTES * c->mb_width);
+  memcpy(t.edge, edge, (size_t)AVR_EDGE_BYTES * c->mb_width);
+  if (c->n_seams == c->cap_seams) {
+    c->cap_seams = c->cap_seams ? 2 * c->cap_seams : 8;
+    c->seams = (avr_seam_t *)realloc(c->seams, sizeof(avr_seam_t) * (size_t)c->cap_seams);
+    c->piece_end = (uint32_t *)realloc(c->piece_end, sizeof(uint32_t) * (size_t)c->cap_seams);
+  }
+  /* the piece ends: encoder::finish; the next one starts with a fresh model and coder */
+  ac_enc_finish(&c->enc);
+  ac_enc_free(&c->enc);
+  c->piece_end[c->n_seams] = (uint32_t)c->enc_out.len;
+  c->seams[c->n_seams++] = t;
+  if (c->model != c->first_model) {
+    size_t unused[8] = {0};
+    avr_model_bills(c->model, avr_last_bill, unused);
+    avr_model_free(c->model);
+  }
+  c->model = model_new_p(0);
+  model_update_frame_spec(c->model, c->picture_id, c->mb_width, c->mb_height);
+  rc_enc_init(&c->enc, &c->enc_out);
+}
+
 static void c_put_nz(void *ctx, avr_model_t *m, model_key_t key, int *symbol) { /* 1213-1221 */
   cdrv_t *c = (cdrv_t *)ctx;
   size_t billable = c_put(c, *symbol, key);
@@ -291,6 +341,16 @@ typedef struct {
   cabac_enc_t cenc;
   obuf_t cabac_out;
   int finished;
+  /* a split slice (avr_oracle.h): the pieces' streams one after the other; a fresh model and decoder at
+   * each seam's first macroblock, the CABAC encoder carrying on */
+  const avr_seam_t *seams;
+  const uint32_t *piece_len;
+  const uint8_t *rc;
+  size_t rc_off;
+  int n_seams, next_seam;
+  int picture_id, mb_width, mb_height;
+  avr_model_t *first_model;
+  avr_ce_t *ce;         /* avr_decompress_piece: the byte-form re-encoder instead of cenc */
 } ddrv_t;
 
 static int d_dec(ddrv_t *d, model_key_t key) { /* decoder::get of the model's coder */
@@ -308,7 +368,8 @@ static int d_get(void *o, uint8_t *state, int ctx) {
   } else {
     s = d_dec(d, model_get_key(m, ctx));
   }
-  m->cabac_bill[m->coding_type] += cabac_enc_put(&d->cenc, s, state);
+  if (d->ce) avr_ce_decision(d->ce, s, state);
+  else m->cabac_bill[m->coding_type] += cabac_enc_put(&d->cenc, s, state);
   model_update_state(m, s, ctx);
   return s;
 }
@@ -316,20 +377,38 @@ static int d_get_bypass(void *o) {
   ddrv_t *d = (ddrv_t *)o;
   int s = d_dec(d, model_get_key(d->model, K_BYPASS));
   model_update_state(d->model, s, K_BYPASS);
-  d->model->cabac_bill[d->model->coding_type] += cabac_enc_put_bypass(&d->cenc, s);
+  if (d->ce) avr_ce_bypass(d->ce, s);
+  else d->model->cabac_bill[d->model->coding_type] += cabac_enc_put_bypass(&d->cenc, s);
   return s;
 }
 static int d_get_terminate(void *o) {
   ddrv_t *d = (ddrv_t *)o;
   int s = d_dec(d, model_get_key(d->model, K_TERMINATE));
   model_update_state(d->model, s, K_TERMINATE);
-  d->model->cabac_bill[d->model->coding_type] += cabac_enc_put_terminate(&d->cenc, s);
+  if (d->ce) avr_ce_terminate(d->ce, s);
+  else d->model->cabac_bill[d->model->coding_type] += cabac_enc_put_terminate(&d->cenc, s);
   if (s) {
     if (d->cabac_out.len && d->cabac_out.data[d->cabac_out.len - 1] == 0x80) d->cabac_out.len--; /* 1503-1505 */
     d->finished = 1;
   }
   return s;
 }
+static void d_row_start(void *o, int addr, const uint8_t *state, const uint8_t *edge, int last_dqp_nz) {
+  ddrv_t *d = (ddrv_t *)o;
+  if (d->next_seam >= d->n_seams || (uint32_t)addr != d->seams[d->next_seam].first_mb) return;
+  if (d->model != d->first_model) {
+    size_t unused[8] = {0};
+    avr_model_bills(d->model, unused, avr_last_cabac_bill);
+    avr_model_free(d->model);
+  }
+  d->model = model_new_p(0);
+  d->model->decompress_side = 1;
+  model_update_frame_spec(d->model, d->picture_id, d->mb_width, d->mb_height);
+  d->rc_off += d->piece_len[d->next_seam];
+  d->next_seam++;
+  rc_dec_init(&d->dec, d->rc + d->rc_off, d->piece_len[d->next_seam]);
+}
+
 static void d_get_nz(void *ctx, avr_model_t *m, model_key_t key, int *symbol) { /* 1481-1486 */
   ddrv_t *d = (ddrv_t *)ctx;
   *symbol = d_dec(d, key);
@@ -399,7 +478,7 @@ int avr_cabac_regenerate(const avr_slice_hdr_t *h, const uint8_t *rbsp_from_caba
   ob_init(&r.out);
   cabac_enc_init(&r.cenc, &r.out);
   avr_hooks_t hk = {&r, r_get, r_get_bypass, r_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
-                    h_end_sub_mb, nop_bct, nop_ect};
+                    h_end_sub_mb, nop_bct, nop_ect, NULL};
   int ret = avr_walk_slice(h, &hk, 0);
   cabac_enc_free(&r.cenc);
   if (bins) *bins = r.bins;
@@ -494,44 +573,134 @@ static avr_model_t *model_new_p(int p32) {
   return m;
 }
 
-static int compress_slice_with_model(avr_model_t *m, const slice_t *s, obuf_t *recoded, size_t *bins) {
+/* split_bytes > 0 (parallel model on arithmetic_code<uint64_t, uint8_t>, progressive frame slices):
+ * the long-slice split; *seams gets the block's seams field (empty: the slice was not cut) */
+static int compress_slice_split(avr_model_t *m, const slice_t *s, obuf_t *recoded, size_t *bins, size_t split_bytes,
+                                obuf_t *seams) {
   cdrv_t c;
   memset(&c, 0, sizeof(c));
   c.model = m;
+  c.first_model = m;
   cabac_dec_init(&c.dec, s->payload, s->rbsp_len - s->h.cabac_start);
   ob_init(&c.enc_out);
   if (m->p32) pc_enc_init(&c.penc, &c.enc_out);
   else rc_enc_init(&c.enc, &c.enc_out);
   c.queueing = PIP_UNKNOWN;
+  const int split = split_bytes && !m->p32 && !s->h.field_pic && !s->h.mbaff;
+  if (split) {
+    c.split_bits = 8 * split_bytes;
+    c.payload_bits = 8 * s->size;
+    c.payload = s->payload;
+    c.payload_n = s->size;
+    c.picture_id = s->picture_id;
+    c.mb_width = s->h.mb_width;
+    c.mb_height = s->h.mb_height;
+  }
   avr_hooks_t hk = {&c, c_get, c_get_bypass, c_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
-                    h_end_sub_mb, c_begin_coding_type, c_end_coding_type};
+                    h_end_sub_mb, c_begin_coding_type, c_end_coding_type, split ? c_row_start : NULL};
   int ret = avr_walk_slice(&s->h, &hk, s->picture_id);
   if (!m->p32) ac_enc_free(&c.enc);
   else if (c.penc.err) ret = -23;   /* carry into a finished digit: cannot happen */
   free(c.bsym);
   free(c.bctx);
   if (ret == 0 && !c.finished) ret = -21;
+  if (c.model != c.first_model) {
+    size_t unused[8] = {0};
+    avr_model_bills(c.model, avr_last_bill, unused);
+    avr_model_free(c.model);
+  }
+  if (seams) ob_init(seams);
+  if (c.n_seams && seams && ret == 0) {
+    uint32_t *pl = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)c.n_seams + 1));
+    uint32_t prev = 0;
+    for (int i = 0; i < c.n_seams; i++) { pl[i] = c.piece_end[i] - prev; prev = c.piece_end[i]; }
+    pl[c.n_seams] = (uint32_t)c.enc_out.len - prev;
+    if (avr_seams_encode(c.seams, c.n_seams, s->h.mb_width, pl, seams)) ret = -24;
+    free(pl);
+  }
+  avr_seams_free(c.seams, c.n_seams);
+  free(c.piece_end);
   *recoded = c.enc_out;
   if (bins) *bins = c.bins;
   return ret;
 }
+static int compress_slice_with_model(avr_model_t *m, const slice_t *s, obuf_t *recoded, size_t *bins) {
+  return compress_slice_split(m, s, recoded, bins, 0, NULL);
+}
 
-static int decompress_slice_with_model(avr_model_t *m, const avr_slice_hdr_t *h, int picture_id,
-                                       const uint8_t *rc, size_t rn, obuf_t *cabac) {
+/* seams != NULL: a split slice (avr_seams_decode's pieces of the stream rc) */
+static int decompress_slice_pieces(avr_model_t *m, const avr_slice_hdr_t *h, int picture_id, const uint8_t *rc,
+                                   size_t rn, obuf_t *cabac, const avr_seam_t *seams, int n_seams,
+                                   const uint32_t *piece_len) {
   ddrv_t d;
   memset(&d, 0, sizeof(d));
   d.model = m;
+  d.first_model = m;
   m->decompress_side = 1;
+  if (n_seams) {
+    size_t tot = 0;
+    for (int i = 0; i <= n_seams; i++) tot += piece_len[i];
+    if (tot != rn || m->p32 || h->field_pic || h->mbaff) return -25;
+    d.seams = seams;
+    d.n_seams = n_seams;
+    d.piece_len = piece_len;
+    d.rc = rc;
+    d.picture_id = picture_id;
+    d.mb_width = h->mb_width;
+    d.mb_height = h->mb_height;
+    rn = piece_len[0];
+  }
   if (m->p32) pc_dec_init(&d.pdec, rc, rn);
   else rc_dec_init(&d.dec, rc, rn);
   ob_init(&d.cabac_out);
   cabac_enc_init(&d.cenc, &d.cabac_out);
   avr_hooks_t hk = {&d, d_get, d_get_bypass, d_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
-                    h_end_sub_mb, d_begin_coding_type, d_end_coding_type};
+                    h_end_sub_mb, d_begin_coding_type, d_end_coding_type, n_seams ? d_row_start : NULL};
   int ret = avr_walk_slice(h, &hk, picture_id);
   cabac_enc_free(&d.cenc);
   if (ret == 0 && !d.finished) ret = -22;
+  if (ret == 0 && d.next_seam != n_seams) ret = -26;   /* a seam the parse never reached */
+  if (d.model != d.first_model) {
+    size_t unused[8] = {0};
+    avr_model_bills(d.model, unused, avr_last_cabac_bill);
+    avr_model_free(d.model);
+  }
   *cabac = d.cabac_out;
+  return ret;
+}
+static int decompress_slice_with_model(avr_model_t *m, const avr_slice_hdr_t *h, int picture_id,
+                                       const uint8_t *rc, size_t rn, obuf_t *cabac) {
+  return decompress_slice_pieces(m, h, picture_id, rc, rn, cabac, NULL, 0, NULL);
+}
+
+int avr_decompress_piece(const avr_slice_hdr_t *h, int picture_id, const uint8_t *rc, size_t n, const avr_seam_t *seam,
+                         int n_mbs, obuf_t *out) {
+  ddrv_t d;
+  memset(&d, 0, sizeof(d));
+  avr_model_t *m = model_new_p(0);
+  m->decompress_side = 1;
+  d.model = m;
+  d.first_model = m;
+  rc_dec_init(&d.dec, rc, n);
+  ob_init(out);
+  avr_ce_t ce;
+  avr_ce_init(&ce, out, seam);
+  d.ce = &ce;
+  d.cabac_out = *out;   /* d_get_terminate's trailing-0x80 rule works on cabac_out */
+  avr_piece_start_t ps = {seam ? (int)seam->first_mb : h->first_mb, n_mbs, seam ? (int)seam->last_dqp_nz : 0,
+                          seam ? seam->state : NULL, seam ? seam->edge : NULL};
+  avr_hooks_t hk = {&d, d_get, d_get_bypass, d_get_terminate, h_frame_spec, h_mb_xy, h_begin_sub_mb,
+                    h_end_sub_mb, d_begin_coding_type, d_end_coding_type, NULL};
+  int ret = avr_walk_piece(h, &hk, picture_id, &ps);
+  if (ret == 1) {   /* stopped at the next seam */
+    avr_ce_seam_flush(&ce);
+    ret = d.finished ? -28 : 0;
+  } else if (ret == 0) {
+    if (!d.finished) ret = -22;
+    else if (out->len && out->data[out->len - 1] == 0x80) out->len--;   /* recode.cpp:1503-1505 */
+  }
+  if (ce.err) ret = -29;
+  avr_model_free(m);
   return ret;
 }
 
@@ -673,9 +842,9 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
       }
       chain_n++;
       avr_model_t *m = ref ? model : model_new_p(mode == AVR_MODE_P32);
-      obuf_t rc;
+      obuf_t rc, seams;
       size_t bins = 0;
-      int r = compress_slice_with_model(m, &s, &rc, &bins);
+      int r = compress_slice_split(m, &s, &rc, &bins, mode == AVR_MODE_P ? avr_split_bytes() : 0, &seams);
       if (!ref) {
         size_t unused[8] = {0};
         avr_model_bills(m, avr_last_bill, unused);
@@ -691,12 +860,14 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
       b.has_cabac = 1;
       b.cabac = rc.data;
       b.cabac_len = rc.len;
+      if (seams.len) { b.has_seams = 1; b.seams = seams.data; b.seams_len = seams.len; }
       avr_pb_put_block(&o, &b);
       avr_last_stats.coded_slices++;
       avr_last_stats.payload_bytes += s.size;
       avr_last_stats.recoded_bytes += rc.len;
       avr_last_stats.bins += bins;
       ob_free(&rc);
+      ob_free(&seams);
     } else {
       avr_pb_block_t b = {0};
       b.has_skip = 1;
@@ -795,7 +966,19 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
       avr_model_t *fresh = NULL;
       if (!mode_r) m = fresh = model_new_p(mode == AVR_MODE_P32);
       obuf_t cab;
-      int r = decompress_slice_with_model(m, &s.h, s.picture_id, b->cabac, b->cabac_len, &cab);
+      avr_seam_t *seams = NULL;
+      uint32_t *piece_len = NULL;
+      int n_seams = 0;
+      int r = 0;
+      if (b->has_seams && (mode != AVR_MODE_P ||
+                           avr_seams_decode(b->seams, b->seams_len, s.h.mb_width, &seams, &n_seams, &piece_len)))
+        r = -27;
+      if (r == 0)
+        r = decompress_slice_pieces(m, &s.h, s.picture_id, b->cabac, b->cabac_len, &cab, seams, n_seams, piece_len);
+      else
+        ob_init(&cab);
+      avr_seams_free(seams, n_seams);
+      free(piece_len);
       if (fresh) {
         avr_model_bills(fresh, unused_bill, avr_last_cabac_bill);
         avr_model_free(fresh);
@@ -835,4 +1018,72 @@ done:
   ob_free(&stream);
   free(blocks);
   return ret;
+}
+
+/* ============================================== the long-slice split, piece by piece (tests) */
+/* Every recodable slice of the file compressed as avr_compress's parallel model does (split_bytes),
+ * and every split one decompressed the device's way: each piece on its own from its seam
+ * (avr_decompress_piece), piece i cut at seam i's q, the last-byte rule (1345-1356), compared with
+ * the payload.  Returns the number of mismatching slices (0), or -1; *n_split / *n_pieces count the
+ * split slices and their pieces. */
+int avr_check_pieces(const uint8_t *file, size_t n, size_t split_bytes, int *n_split, int *n_pieces) {
+  avr_nal_t *nals;
+  int nn = avr_demux(file, n, &nals);
+  if (nn < 0) return -1;
+  stream_state_t *st = (stream_state_t *)calloc(1, sizeof(stream_state_t));
+  st->x264_build = -1;
+  int bad = 0;
+  *n_split = *n_pieces = 0;
+  for (int i = 0; i < nn; i++) {
+    slice_t s;
+    if (!nal_to_slice(st, file + nals[i].offset, nals[i].size, &s)) continue;
+    if (s.size >= (size_t)SURROGATE_MARKER_BYTES && slice_recodable(&s)) {
+      avr_model_t *m = model_new_p(0);
+      obuf_t rc, sb;
+      int r = compress_slice_split(m, &s, &rc, NULL, split_bytes, &sb);
+      avr_model_free(m);
+      avr_seam_t *seams = NULL;
+      uint32_t *pl = NULL;
+      int k = 0;
+      if (r == 0 && sb.len && avr_seams_decode(sb.data, sb.len, s.h.mb_width, &seams, &k, &pl) == 0) {
+        (*n_split)++;
+        *n_pieces += k + 1;
+        obuf_t all;
+        ob_init(&all);
+        size_t off = 0;
+        for (int p = 0; p <= k && !r; p++) {
+          const avr_seam_t *sm = p ? &seams[p - 1] : NULL;
+          const int first = p ? (int)sm->first_mb : s.h.first_mb;
+          const int n_mbs = p < k ? (int)seams[p].first_mb - first : 0;
+          obuf_t piece;
+          r = avr_decompress_piece(&s.h, s.picture_id, rc.data + off, pl[p], sm, n_mbs, &piece);
+          off += pl[p];
+          const size_t start = p ? sm->q : 0;
+          if (!r && all.len != start) r = -40;
+          size_t keep = p < k ? seams[p].q - start : piece.len;
+          if (!r && keep > piece.len) r = -41;
+          if (!r) ob_append(&all, piece.data, keep);
+          ob_free(&piece);
+        }
+        if (!r) {
+          if (s.size > 1) {
+            int parity = (int)(s.size & 1);
+            if (parity != (int)(all.len & 1)) ob_put(&all, s.payload[s.size - 1]);
+            else if (all.len) all.data[all.len - 1] = s.payload[s.size - 1];
+          }
+          if (all.len != s.size || memcmp(all.data, s.payload, s.size)) r = -42;
+        }
+        ob_free(&all);
+      }
+      if (r) bad++;
+      avr_seams_free(seams, k);
+      free(pl);
+      ob_free(&rc);
+      ob_free(&sb);
+    }
+    free(s.rbsp);
+  }
+  free(st);
+  free(nals);
+  return bad;
 }

@@ -1,0 +1,255 @@
+/*
+ * Oracle: the parallel model's long-slice split ("seams").  TEST INFRASTRUCTURE ONLY.
+ *
+ * Not part of the reference: recode.cpp decodes a slice as one chain (1411-1520).  This library's
+ * parallel model may cut a long progressive slice at macroblock-row starts into pieces that are
+ * re-coded with fresh models and decompressed side by side (avr_oracle.h); this file restates the
+ * format's arithmetic so the tests can check the device's containers byte for byte.
+ *
+ * The re-encoder state at a cut.  The CABAC decoder after `bitpos` bits holds codIOffset = V - L,
+ * V the first bitpos bits of the slice's bytes and L the spec encoder's low at the same precision
+ * with every carry already in it (ITU-T H.264 9.3.1.2 / 9.3.4.2), so L = V - offset is known from the
+ * payload.  The re-encoder (avrecode_amd/csrc/avr_engine.h CabacEncoder) keeps the bits of L in a
+ * byte form: m = (bitpos - 10) / 8 whole bytes have gone to its byte queue, the rest (queue + 8
+ * pending bits and the 10-bit window, queue = bitpos - 18 - 8 m) in `low`.  Bytes before the last
+ * byte of L below m that is not 0xFF are final (a later carry stops there), so the piece after the
+ * cut starts its output at that byte q with it as the cache and the 0xFF bytes after it outstanding;
+ * the piece before the cut writes its pending bytes out at its end and is cut at q.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+#include "avr_oracle.h"
+
+static long split_override = -1;
+
+size_t avr_split_bytes(void) {
+  if (split_override >= 0) return (size_t)split_override;
+  const char *e = getenv("AVR_SPLIT_BYTES");
+  return e ? (size_t)strtoull(e, NULL, 10) : (size_t)AVR_SPLIT_BYTES_DEFAULT;
+}
+void avr_set_split_bytes(size_t bytes) { split_override = (long)bytes; }
+
+int avr_seam_encoder(const uint8_t *payload, size_t n, size_t bitpos, uint32_t offset, uint32_t range,
+                     avr_seam_t *s) {
+  if (bitpos < 26) return -1;
+  const size_t m = (bitpos - 10) / 8;
+  const size_t sb = m > 12 ? m - 12 : 0;    /* the bytes of L looked at: [sb, m) */
+  const size_t e = (bitpos + 7) / 8;
+  unsigned __int128 x = 0;
+  for (size_t j = sb; j < e; j++) x = x << 8 | (j < n ? payload[j] : 0);
+  x >>= 8 * e - bitpos;
+  if (x < offset) return -1;               /* the borrow would reach before the window */
+  const unsigned __int128 y = x - offset;  /* L's bits from byte sb to bitpos */
+  long q = -1;
+  uint32_t qb = 0;
+  for (size_t j = m; j-- > sb;) {
+    const uint32_t b = (uint32_t)(y >> (bitpos - 8 * j - 8)) & 0xff;
+    if (b != 0xff) { q = (long)j; qb = b; break; }
+  }
+  if (q < 0) return -1;
+  const unsigned lowbits = (unsigned)(bitpos - 8 * m);   /* queue + 18 <= 17 */
+  s->q = (uint32_t)q;
+  s->ce_cache = qb;
+  s->ce_outstanding = (uint32_t)(m - 1 - (size_t)q);
+  s->ce_low = (uint32_t)(y & (((unsigned __int128)1 << lowbits) - 1));
+  s->ce_queue = (int32_t)lowbits - 18;
+  s->ce_range = range;
+  return 0;
+}
+
+static void put32(obuf_t *o, uint32_t v) {
+  for (int k = 0; k < 4; k++) ob_put(o, (uint8_t)(v >> (8 * k)));
+}
+static uint32_t get32(const uint8_t *p) {
+  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+int avr_seams_encode(const avr_seam_t *s, int n_seams, int mb_width, const uint32_t *piece_len, obuf_t *out) {
+  obuf_t raw;
+  ob_init(&raw);
+  put32(&raw, 1);
+  put32(&raw, (uint32_t)n_seams);
+  put32(&raw, (uint32_t)mb_width);
+  for (int i = 0; i <= n_seams; i++) put32(&raw, piece_len[i]);
+  for (int i = 0; i < n_seams; i++) {
+    const avr_seam_t *t = &s[i];
+    put32(&raw, t->first_mb);
+    put32(&raw, t->q);
+    put32(&raw, t->last_dqp_nz);
+    put32(&raw, t->ce_low);
+    put32(&raw, (uint32_t)t->ce_queue);
+    put32(&raw, t->ce_outstanding);
+    put32(&raw, t->ce_cache);
+    put32(&raw, t->ce_range);
+    ob_append(&raw, t->state, 1024);
+    ob_append(&raw, t->edge, (size_t)AVR_EDGE_BYTES * mb_width);
+  }
+  uLongf zl = compressBound(raw.len);
+  uint8_t *z = (uint8_t *)malloc(zl);
+  int r = compress2(z, &zl, raw.data, raw.len, 9);
+  if (r == Z_OK) {
+    put32(out, (uint32_t)raw.len);
+    ob_append(out, z, zl);
+  }
+  free(z);
+  ob_free(&raw);
+  return r == Z_OK ? 0 : -1;
+}
+
+void avr_seams_free(avr_seam_t *s, int n_seams) {
+  if (!s) return;
+  for (int i = 0; i < n_seams; i++) free(s[i].edge);
+  free(s);
+}
+
+int avr_seams_decode(const uint8_t *p, size_t n, int mb_width, avr_seam_t **out, int *n_seams, uint32_t **piece_len) {
+  *out = NULL;
+  *piece_len = NULL;
+  *n_seams = 0;
+  if (n < 4) return -1;
+  const uint32_t rl = get32(p);
+  if (rl < 12 || rl > (1u << 30)) return -1;
+  uint8_t *raw = (uint8_t *)malloc(rl);
+  uLongf got = rl;
+  if (uncompress(raw, &got, p + 4, n - 4) != Z_OK || got != rl || get32(raw) != 1) { free(raw); return -1; }
+  const uint32_t k = get32(raw + 4), w = get32(raw + 8);
+  const size_t per = 32 + 1024 + (size_t)AVR_EDGE_BYTES * w;
+  if ((int)w != mb_width || k == 0 || k > 65536 || 12 + 4 * ((size_t)k + 1) + per * k != rl) { free(raw); return -1; }
+  uint32_t *pl = (uint32_t *)malloc(sizeof(uint32_t) * (k + 1));
+  avr_seam_t *s = (avr_seam_t *)calloc(k, sizeof(avr_seam_t));
+  const uint8_t *q = raw + 12;
+  for (uint32_t i = 0; i <= k; i++, q += 4) pl[i] = get32(q);
+  for (uint32_t i = 0; i < k; i++) {
+    avr_seam_t *t = &s[i];
+    t->first_mb = get32(q);
+    t->q = get32(q + 4);
+    t->last_dqp_nz = get32(q + 8);
+    t->ce_low = get32(q + 12);
+    t->ce_queue = (int32_t)get32(q + 16);
+    t->ce_outstanding = get32(q + 20);
+    t->ce_cache = get32(q + 24);
+    t->ce_range = get32(q + 28);
+    memcpy(t->state, q + 32, 1024);
+    t->edge = (uint8_t *)malloc((size_t)AVR_EDGE_BYTES * w);
+    memcpy(t->edge, q + 32 + 1024, (size_t)AVR_EDGE_BYTES * w);
+    q += per;
+  }
+  free(raw);
+  *out = s;
+  *n_seams = (int)k;
+  *piece_len = pl;
+  return 0;
+}
+
+/* ------------------------------------------------------- a piece's CABAC re-encoder (byte form) */
+/* avr_engine.h CabacEncoder restated: the arithmetic of 9.3.4.2 with the spec's outstanding bits kept
+ * as whole bytes (a cache byte that a carry may still reach and the 0xFF bytes after it), so a piece
+ * can start from a seam's state and end with its pending bytes written (avr_ce_seam_flush). */
+void avr_ce_init(avr_ce_t *e, obuf_t *out, const avr_seam_t *s) {
+  memset(e, 0, sizeof(*e));
+  e->out = out;
+  if (!s) {
+    e->range = 510;
+    e->queue = -9;
+    return;
+  }
+  e->low = s->ce_low;
+  e->range = s->ce_range;
+  e->queue = s->ce_queue;
+  e->outstanding = s->ce_outstanding;
+  e->cache = s->ce_cache;
+  e->have_cache = 1;
+}
+static void ce_emit(avr_ce_t *e, uint32_t out) {   /* one byte (and a carry) out of the window */
+  const uint32_t carry = out >> 8, byte = out & 0xff;
+  if (byte == 0xff && !carry) {
+    e->outstanding++;
+    return;
+  }
+  if (e->have_cache) {
+    if (e->cache + carry > 0xff) e->err = 1;
+    ob_put(e->out, (uint8_t)(e->cache + carry));
+  } else if (carry) {
+    e->err = 1;
+  }
+  for (; e->outstanding; e->outstanding--) ob_put(e->out, (uint8_t)(0xff + carry));
+  e->cache = byte;
+  e->have_cache = 1;
+}
+static void ce_renorm(avr_ce_t *e, int n) {
+  e->range <<= n;
+  e->low <<= n;
+  e->queue += n;
+  if (e->queue >= 0) {
+    const uint32_t out = e->low >> (e->queue + 10);
+    e->low &= (0x400u << e->queue) - 1;
+    e->queue -= 8;
+    ce_emit(e, out);
+  }
+}
+static int ce_shift(uint32_t range) {
+  int n = 0;
+  while ((range << n) < 256) n++;
+  return n;
+}
+void avr_ce_decision(avr_ce_t *e, int bin, uint8_t *state) {
+  const uint32_t s = *state;
+  const uint32_t lps = avr_lps_range[((e->range >> 6) & 3) * 128 + s];
+  const uint32_t rmps = e->range - lps;
+  if ((uint32_t)bin != (s & 1)) {
+    e->low += rmps;
+    e->range = lps;
+    *state = avr_mlps_state[127 - s];
+  } else {
+    e->range = rmps;
+    *state = avr_mlps_state[128 + s];
+  }
+  ce_renorm(e, ce_shift(e->range));
+}
+void avr_ce_bypass(avr_ce_t *e, int bin) {
+  e->low = (e->low << 1) + (bin ? e->range : 0);
+  e->queue += 1;
+  if (e->queue >= 0) {
+    const uint32_t out = e->low >> (e->queue + 10);
+    e->low &= (0x400u << e->queue) - 1;
+    e->queue -= 8;
+    ce_emit(e, out);
+  }
+}
+void avr_ce_terminate(avr_ce_t *e, int bin) {
+  e->range -= 2;
+  if (!bin) {
+    ce_renorm(e, ce_shift(e->range));
+    return;
+  }
+  /* flush: x = (low + range) | 1 written through its last set bit, padded to a byte */
+  uint64_t low = (uint64_t)((e->low + e->range) | 1) << 10;
+  int queue = e->queue + 10;
+  const int total = queue + 8;
+  const int pad = (8 - (total & 7)) & 7;
+  low <<= pad;
+  queue += pad;
+  while (queue >= 0) {
+    const uint32_t out = (uint32_t)(low >> (queue + 10));
+    low &= (0x400ull << queue) - 1;
+    queue -= 8;
+    ce_emit(e, out);
+  }
+  if (e->have_cache) ob_put(e->out, (uint8_t)e->cache);
+  for (; e->outstanding; e->outstanding--) ob_put(e->out, 0xff);
+  e->have_cache = 0;
+}
+/* a piece that ends at a seam: its pending bytes (the cache with the window's carry, the 0xFF run) */
+void avr_ce_seam_flush(avr_ce_t *e) {
+  const uint32_t carry = e->low >> (e->queue + 18);
+  if (e->have_cache) {
+    if (e->cache + carry > 0xff) e->err = 1;
+    ob_put(e->out, (uint8_t)(e->cache + carry));
+  } else if (carry) {
+    e->err = 1;
+  }
+  for (; e->outstanding; e->outstanding--) ob_put(e->out, (uint8_t)(0xff + carry));
+  e->have_cache = 0;
+}

@@ -774,7 +774,73 @@ static void decode_mb_layer(walker_t *w) {
   }
 }
 
-int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int picture_id) {
+/* The upper row's bottom edges as the device walkers keep them (avr_walker.h EdgeCore, one per column;
+ * zero where that macroblock is not in the slice): the fields the CABAC context selection of the
+ * row below reads (9.3.3.1.1), AVR_EDGE_BYTES each. */
+static void edge_row(const walker_t *w, int y, uint8_t *out) {
+  const int ph_c = (w->h->chroma_array_type == 2 || w->h->chroma_array_type == 3) ? 4 : 2;
+  memset(out, 0, (size_t)AVR_EDGE_BYTES * w->W);
+  for (int c = 0; c < w->W; c++) {
+    const wmb_t *m = &w->mbs[(size_t)(y - 1) * w->W + c];
+    uint8_t *e = out + (size_t)AVR_EDGE_BYTES * c;
+    if (!m->decoded) continue;
+    e[0] = (uint8_t)(1 | m->skip << 1 | m->intra << 2 | m->i16 << 3 | m->direct16 << 4 | m->t8x8 << 5 |
+                     (m->chroma_pred != 0) << 6);
+    e[2] = (uint8_t)m->cbp;
+    e[3] = (uint8_t)(m->cbp >> 8);
+    memcpy(e + 4, &m->nnz[0][12], 4);
+    memcpy(e + 8, &m->nnz[1][4 * (ph_c - 1)], 4);
+    memcpy(e + 12, &m->nnz[2][4 * (ph_c - 1)], 4);
+    for (int l = 0; l < 2; l++)
+      for (int i = 0; i < 4; i++) {
+        e[16 + 8 * l + 2 * i] = m->mvd[l][12 + i][0];
+        e[17 + 8 * l + 2 * i] = m->mvd[l][12 + i][1];
+      }
+    e[32] = (uint8_t)m->ref[0][2];
+    e[33] = (uint8_t)m->ref[0][3];
+    e[34] = (uint8_t)m->ref[1][2];
+    e[35] = (uint8_t)m->ref[1][3];
+    e[36] = m->direct8[2];
+    e[37] = m->direct8[3];
+  }
+}
+
+/* A piece of a split slice (avr_oracle.h): the upper row rebuilt from its edges (the fields the
+ * parse reads of an upper neighbour), then the walk from `start` */
+static void edge_unrow(walker_t *w, int y, const uint8_t *in) {
+  const int ph_c = (w->h->chroma_array_type == 2 || w->h->chroma_array_type == 3) ? 4 : 2;
+  for (int c = 0; c < w->W; c++) {
+    wmb_t *m = &w->mbs[(size_t)(y - 1) * w->W + c];
+    const uint8_t *e = in + (size_t)AVR_EDGE_BYTES * c;
+    memset(m, 0, sizeof(*m));
+    if (!(e[0] & 1)) continue;
+    m->decoded = 1;
+    m->skip = (e[0] >> 1) & 1;
+    m->intra = (e[0] >> 2) & 1;
+    m->i16 = (e[0] >> 3) & 1;
+    m->direct16 = (e[0] >> 4) & 1;
+    m->t8x8 = (e[0] >> 5) & 1;
+    m->chroma_pred = (e[0] >> 6) & 1;
+    m->cbp = (uint16_t)(e[2] | e[3] << 8);
+    memcpy(&m->nnz[0][12], e + 4, 4);
+    memcpy(&m->nnz[1][4 * (ph_c - 1)], e + 8, 4);
+    memcpy(&m->nnz[2][4 * (ph_c - 1)], e + 12, 4);
+    for (int l = 0; l < 2; l++)
+      for (int i = 0; i < 4; i++) {
+        m->mvd[l][12 + i][0] = e[16 + 8 * l + 2 * i];
+        m->mvd[l][12 + i][1] = e[17 + 8 * l + 2 * i];
+      }
+    memset(m->ref, -1, sizeof(m->ref));
+    m->ref[0][2] = (int8_t)e[32];
+    m->ref[0][3] = (int8_t)e[33];
+    m->ref[1][2] = (int8_t)e[34];
+    m->ref[1][3] = (int8_t)e[35];
+    m->direct8[2] = e[36];
+    m->direct8[3] = e[37];
+  }
+}
+
+static int walk(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int picture_id, const avr_piece_start_t *ps) {
   if (!h->supported) return -1;
   walker_t w;
   memset(&w, 0, sizeof(w));
@@ -792,6 +858,18 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
   avr_cabac_init_states(w.state, h->slice_type == AVR_SLICE_I ? -1 : h->cabac_init_idc, h->slice_qp);
   hooks->frame_spec(hooks->opaque, picture_id, w.W, h->mb_height);
   int addr = h->first_mb;
+  int stop_after = 0;
+  if (ps) {
+    if (h->field_pic || h->mbaff) { free(w.mbs); return -1; }
+    addr = ps->start_mb;
+    stop_after = ps->n_mbs;
+    if (ps->edge) {
+      if (addr % w.W || addr < w.W) { free(w.mbs); return -1; }
+      memcpy(w.state, ps->state, 1024);
+      w.last_dqp_nz = ps->last_dqp_nz;
+      edge_unrow(&w, addr / w.W, ps->edge);
+    }
+  }
   int ret = 0;
   avr_walk_mbs_done = 0;
   w.mbaff = h->mbaff;
@@ -816,6 +894,12 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
     w.cur = &w.mbs[addr];
     w.left = x > 0 && w.mbs[addr - 1].decoded ? &w.mbs[addr - 1] : NULL;
     w.top = y > 0 && w.mbs[addr - w.W].decoded ? &w.mbs[addr - w.W] : NULL;
+    if (hooks->row_start && !h->field_pic && x == 0 && addr != h->first_mb) {
+      uint8_t *row = (uint8_t *)malloc((size_t)AVR_EDGE_BYTES * w.W);
+      edge_row(&w, y, row);
+      hooks->row_start(hooks->opaque, addr, w.state, row, w.last_dqp_nz);
+      free(row);
+    }
     hooks->mb_xy(hooks->opaque, x, h->field_pic ? 2 * y + h->bottom_field : y);
     decode_mb(&w);
     if (getenv("AVR_WALK_DEBUG"))
@@ -826,8 +910,16 @@ int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int pictu
     avr_walk_mbs_done++;
     avr_walk_last_mb = addr + 1 >= w.W * w.H;
     if (term(&w, SE_EOS)) break;
+    if (stop_after && avr_walk_mbs_done == stop_after) { ret = 1; break; }   /* the piece's end */
     addr++;
   }
   free(w.mbs);
   return ret;
+}
+
+int avr_walk_slice(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int picture_id) {
+  return walk(h, hooks, picture_id, NULL);
+}
+int avr_walk_piece(const avr_slice_hdr_t *h, const avr_hooks_t *hooks, int picture_id, const avr_piece_start_t *ps) {
+  return walk(h, hooks, picture_id, ps);
 }

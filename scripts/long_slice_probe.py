@@ -1,0 +1,45 @@
+"""Where the configs[4] corpus's P-model time goes: each file's slice payload sizes (largest
+first) and its P compress / decompress wall time alone, then the whole corpus as one batch.
+Run on the GPU box: python3 scripts/long_slice_probe.py > gpurun_out/<tag>/long_slice.json"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import avrecode_amd as avr  # noqa: E402
+from avrecode_amd import workloads  # noqa: E402
+
+
+def main():
+    ctx = avr.Context(0)
+    files = workloads.corpus(ctx)
+    out = {"files": {}}
+    for name, data in files:
+        sizes = sorted(avr.slice_payload_sizes(data).tolist(), reverse=True)
+        rec = {"bytes": len(data), "slices": len(sizes), "largest_payloads": sizes[:6]}
+        c = ctx.compress(data, avr.MODEL_PARALLEL)
+        t0 = time.perf_counter()
+        c = ctx.compress(data, avr.MODEL_PARALLEL)
+        t1 = time.perf_counter()
+        d = ctx.decompress(c)
+        t2 = time.perf_counter()
+        assert d == data
+        rec.update(compress_s=t1 - t0, decompress_s=t2 - t1, ratio=len(c) / len(data))
+        out["files"][name] = rec
+        print(name, json.dumps(rec), file=sys.stderr, flush=True)
+    datas = [d for _, d in files]
+    ctx.compress_files(datas, avr.MODEL_PARALLEL)
+    t0 = time.perf_counter()
+    cs = ctx.compress_files(datas, avr.MODEL_PARALLEL)
+    t1 = time.perf_counter()
+    ds = ctx.decompress_files(cs)
+    t2 = time.perf_counter()
+    assert all(a == b for a, b in zip(ds, datas))
+    out["batch"] = {"compress_s": t1 - t0, "decompress_s": t2 - t1,
+                    "MB_s": sum(map(len, datas)) / (t2 - t0) / 1e6}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
