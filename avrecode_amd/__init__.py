@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "avr_hook_begin_sub_mb", "avr_hook_end_sub_mb", "avr_hook_begin_coding_type", "avr_hook_end_coding_type",
     "avr_hooks_end", "avr_hooks_destroy", "avr_neighbor_tables", "avr_last_phase_times",
     "avr_plan_decompress", "avr_splice_container", "avr_roundtrip_files", "avr_slice_kernel",
-    "avr_compress_chain_range", "avr_decompress_chain_range",
+    "avr_compress_chain_range", "avr_decompress_chain_range", "avr_set_split_bytes", "avr_get_split_bytes",
 )
 
 # avr_slice_desc / avr_slice_result (include/avrecode.h), C layout
@@ -205,6 +205,9 @@ def lib() -> ctypes.CDLL:
     L.avr_plan_decompress.argtypes = [vp, sz, pp, pi, pp, psz, psz, pi, pi]
     L.avr_splice_container.argtypes = [vp, sz, i32, vp, vp, sz, vp, vp, pp, psz]
     L.avr_last_phase_times.argtypes = [vp, vp]
+    L.avr_set_split_bytes.argtypes = [vp, sz]
+    L.avr_get_split_bytes.argtypes = [vp]
+    L.avr_get_split_bytes.restype = sz
     for name in EXPORTED_SYMBOLS:   # fails here, not at first use, when the build is stale
         getattr(L, name)
     _lib = L
@@ -538,6 +541,16 @@ class Context:
     def _check(self, r: int, what: str):
         if r != AVR_OK:
             raise AvrError(r, f"{what}: {lib().avr_last_error(self._h).decode(errors='replace')}")
+
+    @property
+    def split_bytes(self) -> int:
+        """The parallel model's long-slice split (avr_set_split_bytes; 0: none): the whole-file
+        compress cuts a progressive slice into pieces of about this many payload bytes."""
+        return int(lib().avr_get_split_bytes(self._h))
+
+    @split_bytes.setter
+    def split_bytes(self, v: int):
+        self._check(lib().avr_set_split_bytes(self._h, int(v)), "avr_set_split_bytes")
 
     # ------------------------------------------------------------------ whole files
     def compress(self, data, model: int = MODEL_REFERENCE) -> bytes:

@@ -27,6 +27,8 @@
 #include <thread>
 #include <vector>
 
+#include <zlib.h>
+
 #include "../../include/avrecode.h"
 #include "avr_engine.h"
 #include "avr_front.h"
@@ -78,6 +80,11 @@ struct avr_ctx {
   DevBuf rm_goff, rm_counts, rm_stop, rm_off, rm_ops;   // parallel reference-model compress
   DevBuf regen, dec_descs, res_d, verdict;               // compress-side roundtrip check
   DevBuf file_first, file_op_off;                        // reference model over several files
+  // the parallel model's long-slice split (split_compress / split_decompress): its own stream, so the
+  // long slices' first pass overlaps the rest of the batch, and its own estimator scratch
+  hipStream_t split_stream = nullptr;
+  DevBuf sp_in, sp_out, sp_descs, sp_res, sp_ctl, sp_recs, sp_snapn, sp_est, sp_in2, sp_out2;
+  size_t split_bytes = 0;   // avr_set_split_bytes / AVR_SPLIT_BYTES (0: no split)
   bool round_robin = false;   // placement probe passed: the CU schedule (order) may be used
   int* order_or_null() { return round_robin ? order.as<int>() : nullptr; }
   // phase breakdown of the current / last whole-file call (avr_phase_times): run_plan adds the
@@ -89,6 +96,7 @@ struct avr_ctx {
   ~avr_ctx() {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    if (split_stream) (void)hipStreamDestroy(split_stream);
   }
 };
 
@@ -590,6 +598,422 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
   return AVR_OK;
 }
 
+// ------------------------------------------------------------------------ the long-slice split
+// The parallel model (on arithmetic_code<uint64_t, uint8_t>) cuts a long progressive slice at
+// macroblock-row starts into pieces re-coded with fresh models, so its decompress runs one workgroup
+// per piece instead of one chain (the reference decodes a slice as one chain, recode.cpp:1411-1520).
+// The format is this library's own, restated and checked by the oracle (oracle/oracle_seams.c,
+// avr_oracle.h):
+//   - a cut candidate every 8 split_bytes CABAC bits decoded (at a row start, half a piece still
+//     ahead); it becomes a cut where the re-encoder's state can be placed (seam_encoder) -- the
+//     byte form of the arithmetic's low L = V - codIOffset, V the payload's first bitpos bits;
+//   - each piece has its own re-coded stream (Block.cabac holds them one after the other) and starts
+//     with a fresh model whose upper row of model bytes is zero;
+//   - Block field 16 ("seams", zlib) carries, per cut, what the piece after it needs: its first
+//     macroblock, its first output byte q, the re-encoder state, the CABAC contexts, last_dqp_nz
+//     and the upper row's edges (the parse's neighbour fields).
+// Compress takes the long slices through the split kernel twice (avr_k_split.hip): a whole-slice
+// pass that records the candidates (on its own stream, beside the rest of the batch), then the
+// pieces.  Decompress runs the pieces side by side and splices them: piece i's bytes up to cut i's q.
+constexpr size_t kSplitBytesDefault = 131072;
+
+bool split_candidate(const avr_slice_desc& d, size_t split_bytes) {
+  return split_bytes && split_bytes < ((size_t)1 << 28) && d.structure == AVR_STRUCT_FRAME &&
+         2 * (uint64_t)d.payload_size >= 3 * (uint64_t)split_bytes;
+}
+
+struct SeamCe {
+  uint32_t q, low, outstanding, cache, range;
+  int32_t queue;
+};
+// The re-encoder where the decoder stands after bitpos bits with codIOffset `offset` (the oracle's
+// avr_seam_encoder): m = (bitpos - 10) / 8 whole bytes have left the window; the last byte of L
+// below m that is not 0xFF (q) is the cache, the 0xFF bytes after it outstanding, the rest in low.
+bool seam_encoder(const uint8_t* pay, size_t n, uint64_t bitpos, uint32_t offset, uint32_t range, SeamCe* s) {
+  if (bitpos < 26) return false;
+  const uint64_t m = (bitpos - 10) / 8, sb = m > 12 ? m - 12 : 0, e = (bitpos + 7) / 8;
+  unsigned __int128 x = 0;
+  for (uint64_t j = sb; j < e; j++) x = x << 8 | (j < n ? pay[j] : 0);
+  x >>= 8 * e - bitpos;
+  if (x < offset) return false;
+  const unsigned __int128 y = x - offset;
+  for (uint64_t j = m; j-- > sb;) {
+    const uint32_t b = (uint32_t)(y >> (bitpos - 8 * j - 8)) & 0xff;
+    if (b == 0xff) continue;
+    const unsigned lowbits = (unsigned)(bitpos - 8 * m);
+    s->q = (uint32_t)j;
+    s->cache = b;
+    s->outstanding = (uint32_t)(m - 1 - j);
+    s->low = (uint32_t)(y & (((unsigned __int128)1 << lowbits) - 1));
+    s->queue = (int32_t)lowbits - 18;
+    s->range = range;
+    return true;
+  }
+  return false;
+}
+
+void put_le32(std::vector<uint8_t>* o, uint32_t v) {
+  for (int k = 0; k < 4; k++) o->push_back((uint8_t)(v >> (8 * k)));
+}
+uint32_t get_le32(const uint8_t* p) {
+  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+// Block field 16: u32 raw length, then zlib (level 9) of { u32 1, u32 cuts, u32 mb_width,
+// u32 piece_len[cuts + 1], per cut { u32 first_mb, q, last_dqp_nz, ce_low, ce_queue,
+// ce_outstanding, ce_cache, ce_range, u8 state[1024], u8 edges[40 mb_width] } } (little-endian)
+bool seams_encode(const std::vector<const avr::SeamRec*>& recs, const std::vector<SeamCe>& ce, int mb_width,
+                  const std::vector<uint32_t>& piece_len, std::vector<uint8_t>* out) {
+  std::vector<uint8_t> raw;
+  put_le32(&raw, 1);
+  put_le32(&raw, (uint32_t)recs.size());
+  put_le32(&raw, (uint32_t)mb_width);
+  for (uint32_t l : piece_len) put_le32(&raw, l);
+  for (size_t i = 0; i < recs.size(); i++) {
+    put_le32(&raw, recs[i]->first_mb);
+    put_le32(&raw, ce[i].q);
+    put_le32(&raw, recs[i]->last_dqp_nz);
+    put_le32(&raw, ce[i].low);
+    put_le32(&raw, (uint32_t)ce[i].queue);
+    put_le32(&raw, ce[i].outstanding);
+    put_le32(&raw, ce[i].cache);
+    put_le32(&raw, ce[i].range);
+    raw.insert(raw.end(), recs[i]->state, recs[i]->state + 1024);
+    const uint8_t* e = (const uint8_t*)(recs[i] + 1);
+    raw.insert(raw.end(), e, e + (size_t)avr::kEdgeBytes * mb_width);
+  }
+  uLongf zl = compressBound(raw.size());
+  out->assign(4 + zl, 0);
+  if (compress2(out->data() + 4, &zl, raw.data(), raw.size(), 9) != Z_OK) return false;
+  out->resize(4 + zl);
+  for (int k = 0; k < 4; k++) (*out)[k] = (uint8_t)(raw.size() >> (8 * k));
+  return true;
+}
+
+// the pieces of a split block: per cut a device record (decompress fields), the pieces' streams
+struct SeamsDecoded {
+  int cuts = 0;
+  std::vector<uint32_t> piece_len, first_mb, q;
+  std::vector<uint8_t> recs;   // cuts records of rec_stride bytes
+};
+bool seams_decode(const uint8_t* p, size_t n, int mb_width, size_t rec_stride, SeamsDecoded* sd) {
+  if (n < 4) return false;
+  const uint32_t rl = get_le32(p);
+  if (rl < 12 || rl > (1u << 30)) return false;
+  std::vector<uint8_t> raw(rl);
+  uLongf got = rl;
+  if (uncompress(raw.data(), &got, p + 4, n - 4) != Z_OK || got != rl || get_le32(raw.data()) != 1) return false;
+  const uint32_t k = get_le32(raw.data() + 4), w = get_le32(raw.data() + 8);
+  const size_t per = 32 + 1024 + (size_t)avr::kEdgeBytes * w;
+  if ((int)w != mb_width || k == 0 || k > 65536 || 12 + 4 * ((size_t)k + 1) + per * k != rl) return false;
+  sd->cuts = (int)k;
+  const uint8_t* q = raw.data() + 12;
+  sd->piece_len.resize(k + 1);
+  for (uint32_t i = 0; i <= k; i++, q += 4) sd->piece_len[i] = get_le32(q);
+  sd->recs.assign((size_t)k * rec_stride, 0);
+  sd->first_mb.resize(k);
+  sd->q.resize(k);
+  for (uint32_t i = 0; i < k; i++, q += per) {
+    avr::SeamRec* r = (avr::SeamRec*)(sd->recs.data() + (size_t)i * rec_stride);
+    r->first_mb = sd->first_mb[i] = get_le32(q);
+    sd->q[i] = get_le32(q + 4);
+    r->last_dqp_nz = get_le32(q + 8);
+    r->ce_low = get_le32(q + 12);
+    r->ce_queue = (int32_t)get_le32(q + 16);
+    r->ce_outstanding = get_le32(q + 20);
+    r->ce_cache = get_le32(q + 24);
+    r->ce_range = get_le32(q + 28);
+    if (r->ce_queue < -8 || r->ce_queue > -1 || r->ce_cache > 0xff || r->ce_range < 256 || r->ce_range > 510 ||
+        r->ce_low >= (1u << (r->ce_queue + 18)) || (i && sd->q[i] <= sd->q[i - 1]) ||
+        (i && sd->first_mb[i] <= sd->first_mb[i - 1]) || sd->first_mb[i] % w)
+      return false;
+    memcpy(r->state, q + 32, 1024);
+    memcpy(r + 1, q + 32 + 1024, (size_t)avr::kEdgeBytes * w);
+  }
+  return true;
+}
+
+// Compress of the long slices, in two calls around the rest of the batch: begin uploads them and
+// launches the whole-slice pass with the cut records on the split stream; finish takes the cuts,
+// compresses the pieces and (verify) decompresses them and compares.
+struct SplitOut {
+  int32_t status = 0;
+  std::vector<uint8_t> recoded, seams;   // seams empty: no cut (recoded = the unsplit stream)
+  avr_slice_result bill{};
+};
+struct SplitJob {
+  std::vector<const avr::SliceInfo*> sl;
+  std::vector<avr_slice_desc> d;
+  std::vector<avr::PieceCtl> ctl;
+  Bytes arena;
+  uint64_t out_total = 0;
+  uint32_t nrec = 0, split_bits = 0;
+  size_t stride = 0;
+  int max_w = 1;
+  uint32_t flags = 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+int split_begin(avr_ctx* c, SplitJob* j, size_t split_bytes, uint32_t flags) {
+  const int n = (int)j->sl.size();
+  if (!n) return AVR_OK;
+  j->flags = flags & avr::kFlagBill;
+  j->split_bits = (uint32_t)(8 * split_bytes);
+  j->d.resize(n);
+  j->ctl.resize(n);
+  for (int k = 0; k < n; k++) {
+    const avr::SliceInfo& s = *j->sl[k];
+    avr_slice_desc& d = j->d[k];
+    d = desc_from_header(s);
+    append_aligned(&j->arena, s.payload(), s.read_limit, 16, &d.payload_offset);
+    d.payload_size = (uint32_t)s.size;
+    d.read_limit = (uint32_t)s.read_limit;
+    d.out_capacity = (uint32_t)(s.size * 2 + 256);
+    d.out_offset = j->out_total;
+    j->out_total += ((uint64_t)d.out_capacity + 15) & ~15ull;
+    j->max_w = std::max(j->max_w, d.mb_width);
+    const uint32_t cap = (uint32_t)(8ull * s.size / j->split_bits) + 1;
+    j->ctl[k] = avr::PieceCtl{-1, 0, (int32_t)j->nrec, cap};
+    j->nrec += cap;
+  }
+  j->stride = avr::seam_rec_bytes(j->max_w);
+  const int grid = avr::split_grid(n, j->max_w);
+  HIP_TRY(c, c->sp_in.reserve(j->arena.size() + 4096));
+  HIP_TRY(c, c->sp_out.reserve(j->out_total + 4096));
+  HIP_TRY(c, c->sp_descs.reserve(sizeof(avr_slice_desc) * n));
+  HIP_TRY(c, c->sp_res.reserve(sizeof(avr_slice_result) * n));
+  HIP_TRY(c, c->sp_ctl.reserve(sizeof(avr::PieceCtl) * n));
+  HIP_TRY(c, c->sp_recs.reserve(j->stride * j->nrec + 64));
+  HIP_TRY(c, c->sp_snapn.reserve(sizeof(uint32_t) * n));
+  HIP_TRY(c, c->sp_est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * std::max(1, grid), true));
+  HIP_TRY(c, hipEventCreate(&j->e0));
+  HIP_TRY(c, hipEventCreate(&j->e1));
+  hipStream_t st = c->split_stream;
+  HIP_TRY(c, hipMemcpyAsync(c->sp_in.p, j->arena.data(), j->arena.size(), hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(c->sp_descs.p, j->d.data(), sizeof(avr_slice_desc) * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(c->sp_ctl.p, j->ctl.data(), sizeof(avr::PieceCtl) * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemsetAsync(c->sp_snapn.p, 0, sizeof(uint32_t) * n, st));
+  avr::SplitArgs sa;
+  sa.ctl = c->sp_ctl.as<avr::PieceCtl>();
+  sa.recs = c->sp_recs.as<uint8_t>();
+  sa.rec_stride = (uint32_t)j->stride;
+  sa.split_bits = j->split_bits;
+  sa.snap_n = c->sp_snapn.as<uint32_t>();
+  HIP_TRY(c, hipEventRecord(j->e0, st));
+  HIP_TRY(c, avr::launch_split(0, c->tables.as<avr::EngineTables>(), c->sp_descs.as<avr_slice_desc>(), n, j->max_w,
+                               c->sp_in.as<uint8_t>(), c->sp_out.as<uint8_t>(), c->sp_res.as<avr_slice_result>(),
+                               c->sp_est.as<uint16_t>(), sa, j->flags, st));
+  HIP_TRY(c, hipEventRecord(j->e1, st));
+  return AVR_OK;
+}
+
+// One launch of pieces on the split stream: descs / ctl uploaded, records already in sp_recs,
+// results and outputs downloaded.
+int split_launch(avr_ctx* c, int mode, std::vector<avr_slice_desc>& d, const std::vector<avr::PieceCtl>& ctl,
+                 const uint8_t* in_dev, int max_w, size_t stride, uint32_t flags, std::vector<avr_slice_result>* res,
+                 Bytes* out, DevBuf* out_dev) {
+  const int n = (int)d.size();
+  uint64_t total = 0;
+  for (auto& x : d) {
+    x.out_offset = total;
+    total += ((uint64_t)x.out_capacity + 15) & ~15ull;
+  }
+  res->assign(n, avr_slice_result{});
+  out->resize(total);
+  if (!n) return AVR_OK;
+  hipStream_t st = c->split_stream;
+  HIP_TRY(c, out_dev->reserve(total + 4096));
+  HIP_TRY(c, c->sp_descs.reserve(sizeof(avr_slice_desc) * n));
+  HIP_TRY(c, c->sp_res.reserve(sizeof(avr_slice_result) * n));
+  HIP_TRY(c, c->sp_ctl.reserve(sizeof(avr::PieceCtl) * n));
+  HIP_TRY(c, c->sp_est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * std::max(1, avr::split_grid(n, max_w)), true));
+  HIP_TRY(c, hipMemcpyAsync(c->sp_descs.p, d.data(), sizeof(avr_slice_desc) * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(c->sp_ctl.p, ctl.data(), sizeof(avr::PieceCtl) * n, hipMemcpyHostToDevice, st));
+  avr::SplitArgs sa;
+  sa.ctl = c->sp_ctl.as<avr::PieceCtl>();
+  sa.recs = c->sp_recs.as<uint8_t>();
+  sa.rec_stride = (uint32_t)stride;
+  hipEvent_t e0, e1;
+  HIP_TRY(c, hipEventCreate(&e0));
+  HIP_TRY(c, hipEventCreate(&e1));
+  HIP_TRY(c, hipEventRecord(e0, st));
+  HIP_TRY(c, avr::launch_split(mode, c->tables.as<avr::EngineTables>(), c->sp_descs.as<avr_slice_desc>(), n, max_w,
+                               in_dev, out_dev->as<uint8_t>(), c->sp_res.as<avr_slice_result>(), c->sp_est.as<uint16_t>(),
+                               sa, flags, st));
+  HIP_TRY(c, hipEventRecord(e1, st));
+  HIP_TRY(c, hipMemcpyAsync(res->data(), c->sp_res.p, sizeof(avr_slice_result) * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(out->data(), out_dev->p, total, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  float ms = 0;
+  HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+  c->phase.kernel_s += 1e-3 * ms;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return AVR_OK;
+}
+
+// the regenerated bytes of a split slice: piece i's bytes up to cut i's q (the cut's first byte),
+// the last piece whole; false if a piece failed or came out short
+bool splice_pieces(const std::vector<const uint8_t*>& p, const std::vector<uint32_t>& len,
+                   const std::vector<int32_t>& status, const std::vector<uint32_t>& q, std::vector<uint8_t>* o) {
+  o->clear();
+  for (size_t i = 0; i < p.size(); i++) {
+    if (status[i]) return false;
+    const size_t start = i ? q[i - 1] : 0;
+    if (o->size() != start) return false;
+    size_t keep = len[i];
+    if (i < q.size()) {
+      if (q[i] < start || q[i] - start > len[i]) return false;
+      keep = q[i] - start;
+    }
+    o->insert(o->end(), p[i], p[i] + keep);
+  }
+  return true;
+}
+// recode.cpp:1345-1356 on a regenerated slice (before it: the trailing 0x80 already dropped)
+void last_byte_patch(std::vector<uint8_t>* o, const uint8_t* payload, size_t size) {
+  if (size <= 1) return;
+  if ((int)(size & 1) != (int)(o->size() & 1)) o->push_back(payload[size - 1]);
+  else if (!o->empty()) o->back() = payload[size - 1];
+}
+
+int split_finish(avr_ctx* c, SplitJob* j, bool verify, std::vector<SplitOut>* out) {
+  const int n = (int)j->sl.size();
+  out->assign(n, SplitOut());
+  if (!n) return AVR_OK;
+  hipStream_t st = c->split_stream;
+  // 1) the whole-slice pass: statuses, unsplit streams, cut records
+  std::vector<avr_slice_result> r1(n);
+  std::vector<uint32_t> snapn(n);
+  Bytes out1(j->out_total), recs((size_t)j->stride * j->nrec);
+  HIP_TRY(c, hipMemcpyAsync(r1.data(), c->sp_res.p, sizeof(avr_slice_result) * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(snapn.data(), c->sp_snapn.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(out1.data(), c->sp_out.p, j->out_total, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(recs.data(), c->sp_recs.p, recs.size(), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  float ms = 0;
+  HIP_TRY(c, hipEventElapsedTime(&ms, j->e0, j->e1));
+  c->phase.kernel_s += 1e-3 * ms;
+  (void)hipEventDestroy(j->e0);
+  (void)hipEventDestroy(j->e1);
+  j->e0 = j->e1 = nullptr;
+  // 2) the cuts: records whose re-encoder state can be placed, q moving forward
+  std::vector<std::vector<uint32_t>> cut_rec(n);
+  std::vector<std::vector<SeamCe>> cut_ce(n);
+  for (int k = 0; k < n; k++) {
+    SplitOut& so = (*out)[k];
+    so.status = r1[k].status;
+    so.bill = r1[k];
+    if (so.status) continue;
+    const avr::SliceInfo& s = *j->sl[k];
+    for (uint32_t i = 0; i < std::min(snapn[k], j->ctl[k].snap_cap); i++) {
+      const uint32_t ri = (uint32_t)j->ctl[k].snap + i;
+      avr::SeamRec* r = (avr::SeamRec*)(recs.data() + (size_t)ri * j->stride);
+      SeamCe ce;
+      const uint64_t bitpos = 8ull * r->cd_next - r->cd_k;
+      if (!seam_encoder(s.payload(), s.size, bitpos, r->cd_low >> r->cd_k, r->cd_range, &ce)) continue;
+      if (!cut_ce[k].empty() && ce.q <= cut_ce[k].back().q) continue;
+      r->ce_low = ce.low;
+      r->ce_range = ce.range;
+      r->ce_outstanding = ce.outstanding;
+      r->ce_cache = ce.cache;
+      r->ce_queue = ce.queue;
+      cut_rec[k].push_back(ri);
+      cut_ce[k].push_back(ce);
+    }
+    if (cut_rec[k].empty())   // no cut: the unsplit stream
+      so.recoded.assign(out1.begin() + j->d[k].out_offset, out1.begin() + j->d[k].out_offset + r1[k].out_len);
+  }
+  // 3) the pieces, compressed (records: the decoder fields the first pass wrote)
+  std::vector<avr_slice_desc> pd;
+  std::vector<avr::PieceCtl> pc;
+  std::vector<int> first_piece(n, -1);
+  for (int k = 0; k < n; k++) {
+    if (cut_rec[k].empty()) continue;
+    first_piece[k] = (int)pd.size();
+    const size_t np = cut_rec[k].size() + 1;
+    for (size_t i = 0; i < np; i++) {
+      avr_slice_desc d = j->d[k];
+      const avr::SeamRec* r = i ? (const avr::SeamRec*)(recs.data() + (size_t)cut_rec[k][i - 1] * j->stride) : nullptr;
+      if (r) d.first_mb = (int32_t)r->first_mb;
+      const uint32_t next = i + 1 < np ? ((const avr::SeamRec*)(recs.data() + (size_t)cut_rec[k][i] * j->stride))->first_mb : 0;
+      pc.push_back(avr::PieceCtl{r ? (int32_t)cut_rec[k][i - 1] : -1, next ? next - (uint32_t)d.first_mb : 0u, -1, 0});
+      pd.push_back(d);
+    }
+  }
+  if (pd.empty()) return AVR_OK;
+  std::vector<avr_slice_result> r2;
+  Bytes out2;
+  if (int e = split_launch(c, 0, pd, pc, c->sp_in.as<uint8_t>(), j->max_w, j->stride, j->flags, &r2, &out2, &c->sp_out))
+    return e;
+  // 4) verify: the pieces decompressed from the records as a container would give them, spliced and
+  //    compared with the payload
+  std::vector<char> ok(n, 1);
+  if (verify) {
+    HIP_TRY(c, hipMemcpyAsync(c->sp_recs.p, recs.data(), recs.size(), hipMemcpyHostToDevice, st));
+    Bytes arena;
+    std::vector<avr_slice_desc> dd(pd.size());
+    for (size_t i = 0; i < pd.size(); i++) {
+      dd[i] = pd[i];
+      append_aligned(&arena, out2.data() + pd[i].out_offset, r2[i].out_len, 16, &dd[i].payload_offset);
+      dd[i].payload_size = dd[i].read_limit = r2[i].out_len;
+      dd[i].out_capacity = pd[i].payload_size + 4096;
+    }
+    HIP_TRY(c, c->sp_in2.reserve(arena.size() + 4096));
+    HIP_TRY(c, hipMemcpyAsync(c->sp_in2.p, arena.data(), arena.size(), hipMemcpyHostToDevice, st));
+    std::vector<avr_slice_result> r3;
+    Bytes out3;
+    if (int e = split_launch(c, 1, dd, pc, c->sp_in2.as<uint8_t>(), j->max_w, j->stride, 0, &r3, &out3, &c->sp_out2))
+      return e;
+    for (int k = 0; k < n; k++) {
+      if (first_piece[k] < 0) continue;
+      const avr::SliceInfo& s = *j->sl[k];
+      const size_t np = cut_rec[k].size() + 1;
+      std::vector<const uint8_t*> p(np);
+      std::vector<uint32_t> len(np), q(np - 1);
+      std::vector<int32_t> stt(np);
+      for (size_t i = 0; i < np; i++) {
+        const int x = first_piece[k] + (int)i;
+        p[i] = out3.data() + dd[x].out_offset;
+        len[i] = r3[x].out_len;
+        stt[i] = r3[x].status | r2[x].status;
+        if (i + 1 < np) q[i] = cut_ce[k][i].q;
+      }
+      std::vector<uint8_t> regen;
+      ok[k] = splice_pieces(p, len, stt, q, &regen);
+      if (ok[k]) {
+        last_byte_patch(&regen, s.payload(), s.size);
+        ok[k] = regen.size() == s.size && memcmp(regen.data(), s.payload(), s.size) == 0;
+      }
+    }
+  }
+  // 5) the blocks: the pieces' streams one after the other, the seams field
+  for (int k = 0; k < n; k++) {
+    if (first_piece[k] < 0) continue;
+    SplitOut& so = (*out)[k];
+    const size_t np = cut_rec[k].size() + 1;
+    std::vector<uint32_t> plen(np);
+    so.recoded.clear();
+    so.bill = avr_slice_result{};
+    for (size_t i = 0; i < np; i++) {
+      const int x = first_piece[k] + (int)i;
+      if (r2[x].status && !so.status) so.status = r2[x].status;
+      plen[i] = r2[x].out_len;
+      so.recoded.insert(so.recoded.end(), out2.begin() + pd[x].out_offset, out2.begin() + pd[x].out_offset + r2[x].out_len);
+      so.bill.bins += r2[x].bins;
+      so.bill.mbs += r2[x].mbs;
+      for (int b = 0; b < 6; b++) so.bill.bill[b] += r2[x].bill[b];
+    }
+    so.bill.out_len = (uint32_t)so.recoded.size();
+    if (!so.status && !ok[k]) so.status = AVR_SLICE_NO_ROUNDTRIP;
+    if (so.status) continue;
+    std::vector<const avr::SeamRec*> rr;
+    for (uint32_t ri : cut_rec[k]) rr.push_back((const avr::SeamRec*)(recs.data() + (size_t)ri * j->stride));
+    if (!seams_encode(rr, cut_ce[k], j->d[k].mb_width, plen, &so.seams)) return fail(c, AVR_ERR_DEVICE, "zlib failed");
+  }
+  return AVR_OK;
+}
+
 struct ParsedFile {
   std::vector<avr::SliceInfo> slices;
 };
@@ -905,7 +1329,8 @@ void parallel_files(int nf, F&& fn) {
 // into one exactly sized buffer allocated here (*out).
 int emit_container(const uint8_t* in, size_t n, const std::vector<SliceView>& sv, const std::vector<const uint8_t*>& found,
                    const std::vector<std::pair<const uint8_t*, size_t>>& recoded, int model, uint8_t** out,
-                   size_t* out_len, uint8_t* dst = nullptr, size_t cap = 0) {
+                   size_t* out_len, uint8_t* dst = nullptr, size_t cap = 0,
+                   const std::vector<std::pair<const uint8_t*, size_t>>* seams = nullptr) {
   std::vector<avr::PbBlock> blocks;
   blocks.reserve(2 * sv.size() + 1);
   size_t prev_end = 0;
@@ -927,6 +1352,7 @@ int emit_container(const uint8_t* in, size_t n, const std::vector<SliceView>& sv
       b.has_cabac = true;
       b.cabac = recoded[i].first;
       b.cabac_len = recoded[i].second;
+      if (seams && (*seams)[i].second) b.has_seams = true, b.seams = (*seams)[i].first, b.seams_len = (*seams)[i].second;
     } else {
       b.has_skip = true;
       b.skip_coded = true;
@@ -1020,6 +1446,10 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   //    carry the same parse / restore verdict) and demotes the failures, so a well-formed file
   //    costs one reference-model pass, not a parallel-model pass before it.
   Plan plan;
+  // the parallel model's long slices (split_candidate): the split job, its first pass on the split
+  // stream beside the batch (cand_of = -2 - index there)
+  SplitJob sj;
+  const size_t split_bytes = model == AVR_MODEL_PARALLEL ? c->split_bytes : 0;
   std::vector<std::vector<int>> cand_of(nf);
   for (int f = 0; f < nf; f++) {
     cand_of[f].assign(pf[f].slices.size(), -1);
@@ -1028,6 +1458,12 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
       const avr::SliceInfo& s = pf[f].slices[i];
       if (!recodable_candidate(s)) continue;
       avr_slice_desc d = desc_from_header(s);
+      d.payload_size = (uint32_t)s.size;
+      if (split_candidate(d, split_bytes)) {
+        cand_of[f][i] = -2 - (int)sj.sl.size();
+        sj.sl.push_back(&s);
+        continue;
+      }
       append_aligned(&plan.arena, s.payload(), s.read_limit, 16, &d.payload_offset);
       d.payload_size = (uint32_t)s.size;
       d.read_limit = (uint32_t)s.read_limit;
@@ -1040,9 +1476,18 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
   std::vector<avr_slice_result> res;
   Bytes outb;
   pc.mark_demux();
+  if (int r = split_begin(c, &sj, split_bytes, bills ? avr::kFlagBill : 0u)) return r;
   if (int r = run_plan(c, 0, false, plan, &res, &outb, verify,
-                       (bills ? avr::kFlagBill : 0u) | coder_flag(model)))
+                       (bills ? avr::kFlagBill : 0u) | coder_flag(model))) {
+    (void)hipStreamSynchronize(c->split_stream);   // its first pass still reads sj's buffers
     return r;
+  }
+  std::vector<SplitOut> so;
+  {
+    const double t = now_s();
+    if (int r = split_finish(c, &sj, verify, &so)) return r;
+    c->plan_wall += now_s() - t;
+  }
   // 2) segmentation (find_next_coded_block_and_emit_literal, recode.cpp:1275-1297)
   std::vector<std::vector<char>> ok(nf);
   std::vector<std::vector<const uint8_t*>> found(nf);
@@ -1050,13 +1495,17 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
     ok[f].assign(pf[f].slices.size(), 0);
     for (size_t i = 0; i < pf[f].slices.size(); i++)
       ok[f][i] = reference_model(model) ? st[f] == AVR_OK && recodable_candidate(pf[f].slices[i])
-                                              : cand_of[f][i] >= 0 && res[cand_of[f][i]].status == 0;
+                 : cand_of[f][i] >= 0    ? res[cand_of[f][i]].status == 0
+                 : cand_of[f][i] <= -2   ? so[-2 - cand_of[f][i]].status == 0
+                                         : false;
   }
   parallel_files(nf, [&](int f) { found[f] = segment(in[f], in_len[f], pf[f], ok[f]); });
   // 3) reference model: the coded slices of every file in file order, estimators per file; a
   //    slice that fails there is demoted to skip_coded and its file's pass repeated
   std::vector<std::vector<std::vector<uint8_t>>> recoded(nf);
   for (int f = 0; f < nf; f++) recoded[f].resize(pf[f].slices.size());
+  std::vector<std::vector<std::pair<const uint8_t*, size_t>>> seams_of(nf);
+  for (int f = 0; f < nf; f++) seams_of[f].assign(pf[f].slices.size(), {nullptr, 0});
   if (reference_model(model)) {
     std::vector<char> todo(nf, 0);
     for (int f = 0; f < nf; f++) todo[f] = st[f] == AVR_OK;
@@ -1125,6 +1574,13 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
       for (size_t i = 0; i < pf[f].slices.size(); i++)
         if (found[f][i]) {
           const int k = cand_of[f][i];
+          if (k <= -2) {   // a split slice: its pieces' streams and seams
+            SplitOut& x = so[-2 - k];
+            recoded[f][i].swap(x.recoded);
+            seams_of[f][i] = {x.seams.data(), x.seams.size()};
+            if (bills) add_bill(&(*bills)[f], x.bill);
+            continue;
+          }
           recoded[f][i].assign(outb.begin() + plan.descs[k].out_offset,
                                outb.begin() + plan.descs[k].out_offset + res[k].out_len);
           if (bills) add_bill(&(*bills)[f], res[k]);
@@ -1136,7 +1592,8 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
     if (st[f] != AVR_OK) return;
     std::vector<std::pair<const uint8_t*, size_t>> blobs(pf[f].slices.size(), {nullptr, 0});
     for (size_t i = 0; i < pf[f].slices.size(); i++) blobs[i] = {recoded[f][i].data(), recoded[f][i].size()};
-    st[f] = emit_container(in[f], in_len[f], views_of(pf[f]), found[f], blobs, model, &out[f], &out_len[f]);
+    st[f] = emit_container(in[f], in_len[f], views_of(pf[f]), found[f], blobs, model, &out[f], &out_len[f], nullptr, 0,
+                           &seams_of[f]);
   });
   for (int f = 0; f < nf; f++) {
     if (status) status[f] = st[f];
@@ -1149,15 +1606,34 @@ int compress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t* i
 // decompressor::run (recode.cpp:1312-1357) for several files at once: the slices of every
 // parallel-model file go to one parallel launch, every reference-model file to one workgroup of a
 // sequential launch.
+// A split block (the parallel model's long-slice split): its pieces in the split plan, the cuts' q
+// (piece i's bytes end at q[i]), the spliced regenerated bytes after the run
+struct SplitBlock {
+  int block = -1, first = 0, pieces = 0;
+  std::vector<uint32_t> q;
+  std::vector<uint8_t> regen;
+  int32_t status = 0;
+  avr_slice_result bill{};
+};
+struct SplitPlan {
+  Plan plan;                        // the pieces (descs, their re-coded streams in the arena)
+  std::vector<avr::PieceCtl> ctl;
+  Bytes recs;                       // the cut records, rec_stride apart
+  size_t stride = avr::seam_rec_bytes(kMringCols);
+  static constexpr int kMringCols = avr::kMringCols;   // widest picture a record holds
+};
 struct DecJob {
   std::vector<avr::PbBlock> blocks;
   Bytes stream;                      // read_packet's stream: literals + surrogate blocks
   bool parallel = false;
   int model = AVR_MODEL_REFERENCE;   // from Recoded.Metadata.version
-  std::vector<int> desc_of_block;    // plan index per coded block (-1: none)
+  std::vector<int> desc_of_block;    // plan index per coded block (-1: none; <= -2: split block -2 - k)
+  std::vector<SplitBlock> splits;
 };
 
-int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* plan) {
+// sp: where the pieces of split blocks go (nullptr: such a container is refused -- the sharded and
+// hooks paths decompress slices, not pieces)
+int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* plan, SplitPlan* sp = nullptr) {
   const bool tm = getenv("AVR_ASM_TIMING") != nullptr;
   double t0 = now_s();
   std::string version;
@@ -1237,6 +1713,42 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
     } else {
       d.coded = 0;
     }
+    if (b.has_cabac && b.has_seams) {   // a split block: its pieces go to the split plan
+      if (!sp) return fail(c, AVR_ERR_UNSUPPORTED, "split slices (block field 16) decompress through the whole-file calls only");
+      if (j->model != AVR_MODEL_PARALLEL || d.structure != AVR_STRUCT_FRAME || d.mb_width > SplitPlan::kMringCols)
+        return fail(c, AVR_ERR_FORMAT, "seams on a block that cannot be split");
+      SeamsDecoded sd;
+      if (!seams_decode(b.seams, b.seams_len, d.mb_width, sp->stride, &sd))
+        return fail(c, AVR_ERR_FORMAT, "Invalid seams field in coded block.");
+      uint64_t tot = 0;
+      for (uint32_t l : sd.piece_len) tot += l;
+      if (tot != b.cabac_len || sd.q.back() >= (uint64_t)b.size || sd.first_mb[0] <= (uint32_t)d.first_mb)
+        return fail(c, AVR_ERR_FORMAT, "Invalid seams field in coded block.");
+      SplitBlock x;
+      x.block = (int)next_coded;
+      x.first = (int)sp->plan.descs.size();
+      x.pieces = sd.cuts + 1;
+      x.q = sd.q;
+      const uint32_t rec0 = (uint32_t)(sp->recs.size() / sp->stride);
+      sp->recs.insert(sp->recs.end(), sd.recs.begin(), sd.recs.end());
+      uint64_t off = 0;
+      for (int i = 0; i <= sd.cuts; i++) {
+        avr_slice_desc pd = d;
+        if (i) pd.first_mb = (int32_t)sd.first_mb[i - 1];
+        append_aligned(&sp->plan.arena, b.cabac + off, sd.piece_len[i], 16, &pd.payload_offset);
+        off += sd.piece_len[i];
+        pd.payload_size = pd.read_limit = sd.piece_len[i];
+        pd.out_capacity = (uint32_t)((i < sd.cuts ? sd.q[i] : (uint32_t)b.size) - (i ? sd.q[i - 1] : 0u) + 4096);
+        sp->plan.max_w = std::max(sp->plan.max_w, pd.mb_width);
+        sp->plan.descs.push_back(pd);
+        sp->ctl.push_back(avr::PieceCtl{i ? (int32_t)(rec0 + i - 1) : -1,
+                                        i < sd.cuts ? sd.first_mb[i] - (uint32_t)pd.first_mb : 0u, -1, 0});
+      }
+      j->desc_of_block[next_coded] = -2 - (int)j->splits.size();
+      j->splits.push_back(std::move(x));
+      next_coded++;
+      continue;
+    }
     if (j->parallel && !d.coded) {   // the parallel model has no cross-slice state: skip it
       next_coded++;
       continue;
@@ -1306,7 +1818,7 @@ int splice_job(avr_ctx* c, const DecJob& j, Slice&& slice, std::vector<uint8_t>*
     }
     if (!b.has_cabac) continue;
     const int k = j.desc_of_block[i];
-    if (k < 0) return fail(c, AVR_ERR_FORMAT, "Not all blocks were decoded.");
+    if (k == -1) return fail(c, AVR_ERR_FORMAT, "Not all blocks were decoded.");
     const uint8_t* p = nullptr;
     size_t len = 0;
     if (int stt = slice(k, &p, &len))
@@ -1334,6 +1846,7 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
   // u64 coder; on the P32 coder
   Plan plans[3];   // indexed by plan_of(model): the chained model's chains go to the reference plan
   Plan& rp = plans[AVR_MODEL_REFERENCE];
+  SplitPlan sp;    // the pieces of split blocks
   auto plan_of = [](int m) { return parallel_model(m) ? m : (int)AVR_MODEL_REFERENCE; };
   for (int f = 0; f < nf; f++) {
     out[f] = nullptr;
@@ -1345,9 +1858,14 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
     Plan* plan = &plans[plan_of(m)];
     const size_t n0 = plan->descs.size();
     if (!parallel) rp.file_first.push_back((int)n0);
-    st[f] = decompress_setup(c, in[f], in_len[f], &jobs[f], plan);
-    if (st[f]) {   // drop whatever the failed file left (nothing: setup appends only on success)
+    const size_t s_descs = sp.plan.descs.size(), s_recs = sp.recs.size(), s_arena = sp.plan.arena.size();
+    st[f] = decompress_setup(c, in[f], in_len[f], &jobs[f], plan, &sp);
+    if (st[f]) {   // drop whatever the failed file left
       plan->descs.resize(n0);
+      sp.plan.descs.resize(s_descs);
+      sp.ctl.resize(s_descs);
+      sp.recs.resize(s_recs);
+      sp.plan.arena.resize(s_arena);
       if (!parallel) rp.file_first.pop_back();
     } else if (jobs[f].model == AVR_MODEL_CHAINED) {
       // one workgroup per chain: a new "file" of the sequential launch before every
@@ -1370,6 +1888,38 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
     rp.file_first.push_back((int)rp.descs.size());
     if (int r = run_plan(c, 1, true, rp, &res_of[0], &out_of[0], false, flags)) return r;
   }
+  if (!sp.plan.descs.empty()) {   // the pieces of split blocks, then each block spliced
+    const double t = now_s();
+    hipStream_t ss = c->split_stream;
+    HIP_TRY(c, c->sp_in.reserve(sp.plan.arena.size() + 4096));
+    HIP_TRY(c, c->sp_recs.reserve(sp.recs.size() + 64));
+    HIP_TRY(c, hipMemcpyAsync(c->sp_in.p, sp.plan.arena.data(), sp.plan.arena.size(), hipMemcpyHostToDevice, ss));
+    HIP_TRY(c, hipMemcpyAsync(c->sp_recs.p, sp.recs.data(), sp.recs.size(), hipMemcpyHostToDevice, ss));
+    std::vector<avr_slice_result> pr;
+    Bytes po;
+    if (int r = split_launch(c, 1, sp.plan.descs, sp.ctl, c->sp_in.as<uint8_t>(), sp.plan.max_w, sp.stride, flags, &pr,
+                             &po, &c->sp_out))
+      return r;
+    for (int f = 0; f < nf; f++) {
+      if (st[f]) continue;
+      for (SplitBlock& x : jobs[f].splits) {
+        std::vector<const uint8_t*> pp(x.pieces);
+        std::vector<uint32_t> len(x.pieces);
+        std::vector<int32_t> stt(x.pieces);
+        for (int i = 0; i < x.pieces; i++) {
+          const int k = x.first + i;
+          pp[i] = po.data() + sp.plan.descs[k].out_offset;
+          len[i] = pr[k].out_len;
+          stt[i] = pr[k].status;
+          if (pr[k].status == 0)
+            for (int b = 0; b < 6; b++) x.bill.bill[b] += pr[k].bill[b];
+        }
+        x.status = splice_pieces(pp, len, stt, x.q, &x.regen) ? 0 : AVR_SLICE_NO_END;
+        for (int i = 0; i < x.pieces && !x.status; i++) x.status = stt[i];
+      }
+    }
+    c->plan_wall += now_s() - t;
+  }
   int first_err = AVR_OK;
   for (int f = 0; f < nf; f++) {
     DecJob& j = jobs[f];
@@ -1379,6 +1929,13 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
     std::vector<uint8_t> o;
     if (st[f] == AVR_OK)
       st[f] = splice_job(c, j, [&](int k, const uint8_t** p, size_t* len) {
+        if (k <= -2) {   // a split block, spliced from its pieces
+          const SplitBlock& x = j.splits[-2 - k];
+          *p = x.regen.data();
+          *len = x.regen.size();
+          if (bills && x.status == 0) add_bill(&(*bills)[f], x.bill);
+          return (int)x.status;
+        }
         *p = outb.data() + plan.descs[k].out_offset;
         *len = res[k].out_len;
         if (bills && res[k].status == 0) add_bill(&(*bills)[f], res[k]);
@@ -1629,6 +2186,11 @@ int avr_create(int device, avr_ctx** out) {
   c->device = device;
   if (hipSetDevice(device) != hipSuccess) return AVR_ERR_DEVICE;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return AVR_ERR_DEVICE;
+  if (hipStreamCreateWithFlags(&c->split_stream, hipStreamNonBlocking) != hipSuccess) return AVR_ERR_DEVICE;
+  {
+    const char* e = getenv("AVR_SPLIT_BYTES");
+    c->split_bytes = e ? (size_t)strtoull(e, nullptr, 10) : kSplitBytesDefault;
+  }
   avr::EngineTables t;
   build_tables(&t);
   if (!check_reciprocals(t)) return AVR_ERR_DEVICE;
@@ -1650,6 +2212,13 @@ void avr_destroy(avr_ctx* c) {
 }
 
 const char* avr_last_error(const avr_ctx* c) { return c ? c->err.c_str() : "no context"; }
+
+int avr_set_split_bytes(avr_ctx* c, size_t bytes) {
+  if (!c || bytes >= ((size_t)1 << 28)) return AVR_ERR_INVALID_ARGUMENT;
+  c->split_bytes = bytes;
+  return AVR_OK;
+}
+size_t avr_get_split_bytes(const avr_ctx* c) { return c ? c->split_bytes : 0; }
 
 void avr_free(void* p) { free(p); }
 
@@ -2405,6 +2974,7 @@ int avr_container_describe(const uint8_t* in, size_t n, char** json, uint8_t** r
     if (b.has_cabac) add("\"cabac\": \"" + hex(b.cabac, b.cabac_len) + "\"");
     if (b.has_parity) add(std::string("\"length_parity\": ") + (b.length_parity ? "true" : "false"));
     if (b.has_last_byte) add("\"last_byte\": \"" + hex((const uint8_t*)b.last_byte.data(), b.last_byte.size()) + "\"");
+    if (b.has_seams) add("\"seams\": \"" + hex(b.seams, b.seams_len) + "\"");
     j += (i ? ", {" : "{") + e + "}";
     avr::pb_put_block(&o, b);
   }

@@ -681,6 +681,7 @@ void pb_put_block(std::vector<uint8_t>* o, const PbBlock& b) {
   if (b.has_cabac) bytes_field(&m, 4, b.cabac, b.cabac_len);
   if (b.has_parity) varint(&m, 5 << 3), varint(&m, b.length_parity ? 1 : 0);
   if (b.has_last_byte) bytes_field(&m, 6, (const uint8_t*)b.last_byte.data(), b.last_byte.size());
+  if (b.has_seams) bytes_field(&m, 16, b.seams, b.seams_len);
   bytes_field(o, 2, m.data(), m.size());
 }
 
@@ -699,6 +700,7 @@ size_t block_inner_size(const PbBlock& b) {
   if (b.has_cabac) m += bytes_field_size(4, b.cabac_len);
   if (b.has_parity) m += varint_size(5 << 3) + 1;
   if (b.has_last_byte) m += bytes_field_size(6, b.last_byte.size());
+  if (b.has_seams) m += bytes_field_size(16, b.seams_len);
   return m;
 }
 size_t put_varint(uint8_t* o, size_t at, uint64_t v) {
@@ -730,6 +732,7 @@ size_t pb_write_block(uint8_t* o, size_t at, const PbBlock& b, std::vector<PbCop
   if (b.has_cabac) at = put_bytes(o, at, 4, b.cabac, b.cabac_len, copies);
   if (b.has_parity) at = put_varint(o, at, 5 << 3), at = put_varint(o, at, b.length_parity ? 1 : 0);
   if (b.has_last_byte) at = put_bytes(o, at, 6, (const uint8_t*)b.last_byte.data(), b.last_byte.size(), nullptr);
+  if (b.has_seams) at = put_bytes(o, at, 16, b.seams, b.seams_len, copies);
   return at;
 }
 
@@ -808,11 +811,12 @@ bool pb_parse(const uint8_t* in, size_t n, std::vector<PbBlock>* blocks, std::st
         if (f2 == 1) b.has_size = true, b.size = (int64_t)v;
         if (f2 == 3) b.has_skip = true, b.skip_coded = v != 0;
         if (f2 == 5) b.has_parity = true, b.length_parity = v != 0;
-      } else if (w2 == 2 && (f2 == 2 || f2 == 4 || f2 == 6)) {
+      } else if (w2 == 2 && (f2 == 2 || f2 == 4 || f2 == 6 || f2 == 16)) {
         if (!rd_varint(&q, qe, &v) || (uint64_t)(qe - q) < v) return false;
         if (f2 == 2) b.has_literal = true, b.literal = q, b.literal_len = v;
         if (f2 == 4) b.has_cabac = true, b.cabac = q, b.cabac_len = v;
         if (f2 == 6) b.has_last_byte = true, b.last_byte.assign((const char*)q, v);
+        if (f2 == 16) b.has_seams = true, b.seams = q, b.seams_len = v;
         q += v;
       } else if (!skip_field(&q, qe, w2)) {
         return false;

@@ -111,6 +111,11 @@ struct PbBlock {
   const uint8_t* cabac = nullptr;
   size_t cabac_len = 0;
   std::string last_byte;
+  // field 16, this library's own (not in recode.proto): the parallel model's long-slice split of a
+  // coded block (avr_api.cpp "seams"; zlib, the layout oracle/avr_oracle.h avr_seams_encode names)
+  bool has_seams = false;
+  const uint8_t* seams = nullptr;
+  size_t seams_len = 0;
 };
 void pb_put_block(std::vector<uint8_t>* o, const PbBlock& b);
 // The same bytes written into a buffer sized beforehand: pb_block_size(b) bytes at o + at (returns

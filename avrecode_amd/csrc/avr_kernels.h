@@ -56,6 +56,45 @@ struct SeqFiles {
   int n_files = 1;
   uint64_t frame_stride = 0;
 };
+// ------------------------------------------------------------------ the long-slice split
+// The parallel model may cut a long progressive slice at macroblock-row starts into pieces re-coded
+// with fresh models (the oracle's restatement in oracle/oracle_seams.c), so its
+// decompress runs on one workgroup per piece.  One record per cut ("seam") in device memory:
+struct SeamRec {
+  uint32_t first_mb, last_dqp_nz;
+  uint32_t cd_low, cd_range, cd_k, cd_next;   // compress: the CABAC decoder at the cut (CabacDecoder)
+  uint32_t ce_low, ce_range, ce_outstanding, ce_cache;   // decompress: the re-encoder (CabacEncoder,
+  int32_t ce_queue;                                     //   a cache byte always present)
+  uint32_t pad[5];
+  uint8_t state[1024];                        // CABAC context bytes
+  // then the upper row's EdgeCore records (kEdgeBytes per macroblock column)
+};
+constexpr int kEdgeBytes = 40;
+static_assert(sizeof(SeamRec) == 64 + 1024, "SeamRec layout");
+inline size_t seam_rec_bytes(int max_mb_width) {
+  return (sizeof(SeamRec) + (size_t)kEdgeBytes * max_mb_width + 15) & ~(size_t)15;
+}
+// per descriptor of a split launch
+struct PieceCtl {
+  int32_t seam;        // its start: record index in SplitArgs::recs, -1 = the slice's own start
+  uint32_t n_mbs;      // macroblocks in the piece, 0 = to end_of_slice (the slice's last piece)
+  int32_t snap;        // compress: the first record index for the cuts this slice may take (-1: none)
+  uint32_t snap_cap;   // records from there
+};
+struct SplitArgs {
+  const PieceCtl* ctl = nullptr;
+  uint8_t* recs = nullptr;      // rec_stride bytes per record
+  uint32_t rec_stride = 0;
+  uint32_t split_bits = 0;      // compress: a cut candidate every split_bits decoded bits
+  uint32_t* snap_n = nullptr;   // compress: records written per descriptor
+};
+// compress (mode 0) / decompress (1) of a batch of slices and pieces of progressive frames with the
+// parallel model on arithmetic_code<uint64_t, uint8_t> (avr_k_split.hip): one workgroup per
+// descriptor, min(n, resident slots) workgroups; est holds that many estimator scratches
+int split_grid(int n, int max_mb_width);
+hipError_t launch_split(int mode, const EngineTables* T, const avr_slice_desc* descs, int n, int max_mb_width,
+                        const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est, const SplitArgs& sp,
+                        uint32_t flags, hipStream_t stream);
 // flags: kFlagBill (1) = the coders bill per CodingType into avr_slice_result.bill
 hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
                          int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,

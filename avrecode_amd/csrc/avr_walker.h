@@ -639,7 +639,9 @@ AVR_FI void est_table_reset(uint16_t* est_g, Shared* sh) {
 // only when a batch may hold such slices: kFlagFields), so that the progressive walker carries no
 // field tests in its per-bin and per-macroblock code
 
-template <int MODE, bool RM, bool FLD = false, bool P32 = false>
+// SPL: the long-slice split's kernels (slices_split_kernel): a piece may start from a seam record
+// and stop after n macroblocks, and compress takes the cut records (avr_kernels.h SeamRec)
+template <int MODE, bool RM, bool FLD = false, bool P32 = false, bool SPL = false>
 struct Walker {
   static constexpr bool DEC = MODE == MODE_COMPRESS || MODE == MODE_TRACE;  // CABAC decoding side
   const HotTables* T;     // LDS copy
@@ -697,6 +699,39 @@ struct Walker {
   uint32_t bins;
   int target_mbs, mbs_done, last_mb;
   int nref0, nref1, d8x8inf, x264_build, first_mb;
+  // the long-slice split (SPL): the piece's start record (nullptr: the slice's own start) and
+  // macroblock count (0: to end_of_slice); compress: where the cut records go (snap, snap_cap of
+  // them, rec_stride apart; snap_n written, count to *snap_count), a candidate every split_bits
+  // decoded bits (snap_last: the previous one)
+  const SeamRec* seam;
+  uint8_t* snap;
+  uint32_t* snap_count;
+  uint32_t snap_cap, snap_n, snap_last, split_bits, rec_stride, piece_mbs;
+  int cut;                // the walk stopped at the piece's end (not at end_of_slice)
+  // A cut candidate at this row start (compress, SPL): the rule of oracle/oracle_recode.c
+  // c_row_start -- at least split_bits decoded bits since the last candidate and half of that still
+  // ahead in the payload.  The record: the decoder, the contexts (the cached lanes written back
+  // first), last_dqp_nz and the ring (the upper row's edges, model-row flag cleared).
+  AVR_FI void seam_snapshot(int addr) {
+    const uint32_t pos = cd_bitpos(cd);
+    if (pos - snap_last < split_bits || (uint64_t)pos + split_bits / 2 > 8ull * d->payload_size) return;
+    snap_last = pos;
+    if (snap_n >= snap_cap) return;
+    rc_writeback();
+    mc_store();
+    uint32_t* r32 = (uint32_t*)(snap + (size_t)snap_n * rec_stride);
+    const uint32_t lane = __lane_id();
+    if (lane < 16) {
+      const uint32_t v = lane == 0 ? (uint32_t)addr : lane == 1 ? (uint32_t)last_dqp_nz : lane == 2 ? cd.low
+                       : lane == 3 ? cd.range : lane == 4 ? (uint32_t)cd.k : lane == 5 ? cd.next : 0u;
+      r32[lane] = v;
+    }
+    const uint32_t* st = (const uint32_t*)sh->state;
+    for (uint32_t i = lane; i < 256; i += 64) r32[16 + i] = st[i];
+    const uint32_t* e = (const uint32_t*)ring;
+    for (uint32_t i = lane; i < (uint32_t)W * 10; i += 64) r32[16 + 256 + i] = i % 10 ? e[i] : e[i] & ~kEdgeMringNz;
+    snap_n++;
+  }
   uint32_t prio_cell, prio_cur;   // this slice's cell on the CU board, current priority
   AVR_FI void update_prio() {
     const uint32_t pos = MODE == MODE_DECOMPRESS ? rd.next : cd.next;
@@ -2099,14 +2134,21 @@ struct Walker {
 };
 
 // ---------------------------------------------------------------------------------------
-template <int MODE, bool RM, bool FLD, bool P32>
-AVR_FI void init_slice_state(Walker<MODE, RM, FLD, P32>& w, const EngineTables* T) {
+template <int MODE, bool RM, bool FLD, bool P32, bool SPL>
+AVR_FI void init_slice_state(Walker<MODE, RM, FLD, P32, SPL>& w, const EngineTables* T) {
   const int lane = threadIdx.x, nt = blockDim.x;  // every wave of the workgroup takes part
   const avr_slice_desc* d = w.d;
   // cabac contexts: 9.3.1.1
   const int tbl = d->slice_type == 2 ? 0 : 1 + d->cabac_init_idc;
   const int qp = d->slice_qp < 0 ? 0 : d->slice_qp > 51 ? 51 : d->slice_qp;
-  for (int i = lane; i < 1024; i += nt) {
+  const SeamRec* seam = nullptr;
+  if constexpr (SPL) seam = w.seam;
+  if (seam) {   // a piece after a cut: the contexts as they stood there
+    const uint32_t* s32 = (const uint32_t*)seam->state;
+    uint32_t* st32 = (uint32_t*)w.sh->state;
+    for (int i = lane; i < 256; i += nt) st32[i] = s32[i];
+  }
+  for (int i = seam ? 1024 : lane; i < 1024; i += nt) {
     int m = T->mn[tbl][i][0], n = T->mn[tbl][i][1];
     int pre = ((m * qp) >> 4) + n;
     pre = pre < 1 ? 1 : pre > 126 ? 126 : pre;
@@ -2128,7 +2170,14 @@ AVR_FI void init_slice_state(Walker<MODE, RM, FLD, P32>& w, const EngineTables* 
   // progressive model row needs no clear: a column's model bytes are read only under a decoded
   // upper macroblock of this slice (top_ok), which wrote them.
   const int cols = (FLD && d->structure == AVR_STRUCT_MBAFF && (int)w.ring_cols >= 3 * w.W + 7) ? 3 * w.W + 7 : w.W;
-  for (int i = lane; i < cols * (int)sizeof(typename Walker<MODE, RM, FLD, P32>::ERec) / 4; i += nt) ring32[i] = 0;
+  if (seam) {   // the upper row's edges from the cut, and a model row of zeros (a fresh model sees none)
+    const uint32_t* e32 = (const uint32_t*)(seam + 1);
+    for (int i = lane; i < w.W * kEdgeBytes / 4; i += nt) ring32[i] = i % 10 ? e32[i] : e32[i] & ~kEdgeMringNz;
+    if (!w.mring_global)
+      for (int i = lane; i < w.W * kMringDwords; i += nt) w.mring[i] = 0;
+  } else {
+    for (int i = lane; i < cols * (int)sizeof(typename Walker<MODE, RM, FLD, P32, SPL>::ERec) / 4; i += nt) ring32[i] = 0;
+  }
   if (lane < 2) {
     w.sh->fifo_head[lane] = 0;
     w.sh->fifo_tail[lane] = 0;
@@ -2136,8 +2185,8 @@ AVR_FI void init_slice_state(Walker<MODE, RM, FLD, P32>& w, const EngineTables* 
   __syncthreads();
 }
 
-template <int MODE, bool RM, bool FLD, bool P32>
-AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
+template <int MODE, bool RM, bool FLD, bool P32, bool SPL>
+AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32, SPL>& w) {
   const avr_slice_desc* d = w.d;
   w.W = d->mb_width;
   // a field picture is a picture of half the frame's rows (d->mb_height is the frame's)
@@ -2152,6 +2201,9 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
   w.x264_build = d->x264_build;
   w.first_mb = d->first_mb;
   w.last_dqp_nz = 0;
+  if constexpr (SPL) {
+    if (w.seam) w.last_dqp_nz = (int)w.seam->last_dqp_nz;
+  }
   w.err = 0;
   w.finished = 0;
   w.bins = 0;
@@ -2184,13 +2236,16 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
   }
   for (;;) {
     if (addr >= npic) { w.err = AVR_SLICE_BAD_MB_ADDR; break; }
+    if constexpr (SPL && MODE == MODE_COMPRESS) {
+      if (w.snap && w.mb_x == 0 && w.mbs_done > 0) w.seam_snapshot(addr);
+    }
     PROF_BEGINW(ps0);
     if (!(FLD && w.mbaff)) {
       w.left_ok = w.mb_x > 0 && addr - 1 >= w.first_mb;
       // the upper neighbour's flags + cbp: the first dword of its edge record
       w.tf = *(const uint32_t*)&w.ring[w.mb_x];
       w.top_ok = (w.tf & F_DEC) != 0;
-    } else if (!(w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT)) {
+    } else if (!(w.pst & Walker<MODE, RM, FLD, P32, SPL>::PST_BOT)) {
       w.mbaff_pair_start();
     }
     w.cf = 0;
@@ -2244,7 +2299,7 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
         }
         w.lf = w.cf;
       } else {   // the pair edge of this macroblock; the pair's records move left after its bottom
-        const int bot = (w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT) != 0;
+        const int bot = (w.pst & Walker<MODE, RM, FLD, P32, SPL>::PST_BOT) != 0;
         uint32_t* e32 = (uint32_t*)&w.pair_edge(bot)[w.mb_x];
         if (lane < 23) e32[lane] = lane == 0 ? (w.cf & 0xffff017fu) : ev;
         uint32_t* pr = (uint32_t*)w.pair_rec();
@@ -2270,16 +2325,23 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
       QTRACE(4, (uint32_t)w.mbs_done);
     }
     // MBAFF: end_of_slice_flag follows the bottom macroblock of a pair only (7.3.4)
-    const int eos = (!(FLD && w.mbaff) || (w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
+    const int eos = (!(FLD && w.mbaff) || (w.pst & Walker<MODE, RM, FLD, P32, SPL>::PST_BOT)) ? w.terminate(SE_EOS) : 0;
     SPROF_ENDW(7, ps7);
     if (eos) break;
-    if (Walker<MODE, RM, FLD, P32>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = AVR_SLICE_OVERREAD; break; }
+    if constexpr (SPL) {   // the piece ends at the next cut (its last macroblock's end_of_slice_flag was 0)
+      if (w.piece_mbs && (uint32_t)w.mbs_done >= w.piece_mbs) {
+        w.finished = 1;
+        w.cut = 1;
+        break;
+      }
+    }
+    if (Walker<MODE, RM, FLD, P32, SPL>::DEC && w.in.limit && w.cd.next > w.in.limit + 8) { w.err = AVR_SLICE_OVERREAD; break; }
     // a parallel-model decoder reads at most 8 bytes past its stream (the recoded decoder's 63-bit
     // window; P32: 4): a damaged stream is stopped within a macroblock of running off its end
     if (MODE == MODE_DECOMPRESS && !RM && w.in.limit && w.rd.next > w.in.limit + 16) { w.err = AVR_SLICE_OVERREAD; break; }
     addr++;
-    if ((FLD && w.mbaff) && !(w.pst & Walker<MODE, RM, FLD, P32>::PST_BOT)) {
-      w.pst |= Walker<MODE, RM, FLD, P32>::PST_BOT;
+    if ((FLD && w.mbaff) && !(w.pst & Walker<MODE, RM, FLD, P32, SPL>::PST_BOT)) {
+      w.pst |= Walker<MODE, RM, FLD, P32, SPL>::PST_BOT;
       w.my++;
       continue;
     }
@@ -2298,8 +2360,8 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32>& w) {
 // Run f on the walker instantiation of the slice's structure: w itself for a progressive frame,
 // a field-capable copy (FLD = true, set up from w) for field pictures and MBAFF frames.
 // --------------------------------------------------------------------------- kernel bodies
-template <int MODE, bool RM, bool FLD, bool P32>
-AVR_FI void begin_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out) {
+template <int MODE, bool RM, bool FLD, bool P32, bool SPL>
+AVR_FI void begin_slice(Walker<MODE, RM, FLD, P32, SPL>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out) {
   w.d = d;
   w.in.g = in + d->payload_offset;
   w.in.limit = MODE == MODE_GENERATE ? 0 : d->read_limit;
@@ -2328,6 +2390,14 @@ AVR_FI void begin_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, 
   }
   if (MODE == MODE_COMPRESS || MODE == MODE_TRACE) {
     cd_init(w.cd, w.in);
+    if constexpr (SPL) {
+      if (w.seam) {   // a piece after a cut: the decoder where the cut left it
+        w.cd.low = w.seam->cd_low;
+        w.cd.range = w.seam->cd_range;
+        w.cd.k = (int)w.seam->cd_k;
+        w.cd.next = w.seam->cd_next;
+      }
+    }
   } else if (MODE == MODE_DECOMPRESS) {
     rd_init(w.rd, w.in);
   } else {
@@ -2340,8 +2410,8 @@ AVR_FI void begin_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, 
 #endif
 }
 
-template <int MODE, bool RM, bool FLD, bool P32>
-AVR_FI void profile_slice(Walker<MODE, RM, FLD, P32>& w) {
+template <int MODE, bool RM, bool FLD, bool P32, bool SPL>
+AVR_FI void profile_slice(Walker<MODE, RM, FLD, P32, SPL>& w) {
 #ifdef AVR_PROFILE
   w.bins = 0;
   const uint64_t t0 = PROF_T();
@@ -2363,10 +2433,15 @@ AVR_FI void profile_slice(Walker<MODE, RM, FLD, P32>& w) {
 
 // The walker wave of a pipelined slice: parse + model, one op per bin into the ring, OP_END at
 // the end whatever happened.  Leaves its status in LDS for finish_slice.
-template <int MODE, bool RM, bool FLD, bool P32>
-AVR_FI void walker_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
+template <int MODE, bool RM, bool FLD, bool P32, bool SPL>
+AVR_FI void walker_slice(Walker<MODE, RM, FLD, P32, SPL>& w, const avr_slice_desc* d, const uint8_t* in, avr_slice_result* res) {
   begin_slice(w, d, in, nullptr);
   profile_slice(w);
+  if constexpr (SPL) {
+    // a piece that ends at a cut: its own re-coded stream ends there (encoder::finish)
+    if (MODE == MODE_COMPRESS && w.cut) w.push(OP_FINISH);
+    if (MODE == MODE_COMPRESS && w.snap && __lane_id() == 0) *w.snap_count = w.snap_n;
+  }
   if (!RM) cu_post(w.prio_cell, 0);   // leave the CU board
   w.rc_writeback();  // estimators persist across slices in the reference model
   w.mc_store();
@@ -2378,8 +2453,13 @@ AVR_FI void walker_slice(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d,
   w.publish();
   int status = w.err;
   if (!status && !w.finished) status = AVR_SLICE_NO_END;
+  bool cut = false;
+  if constexpr (SPL) {
+    cut = w.cut;
+    if (!status && w.piece_mbs && !cut) status = AVR_SLICE_NO_END;   // end_of_slice inside a non-last piece
+  }
   int stop_ok = 1;
-  if (MODE == MODE_COMPRESS && !status) {
+  if (MODE == MODE_COMPRESS && !status && !cut) {
     // predicted decompressor output (recode.cpp:1345-1356, 1503-1505): the regenerated CABAC
     // bytes equal the payload through the stop bit, then zero bits
     const uint32_t sbi = cd_bitpos(w.cd) - 1;
@@ -2546,8 +2626,12 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
 // walker up): the level / mvd prefixes on one context with the state in a register, and the map
 // loops unswitched by block kind.  The slice batch keeps the plain loops (measured: the variants
 // cost the batch 0.3-0.8 % and gain R-mode 1-2 %, profiles/r04o_coder2_ab.log, r04q_crunmvd_ab.log).
-template <int MODE, bool P32, bool SEQ = false>
-AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out, uint32_t flags) {
+// SPL (decompress): a piece after a cut starts the re-encoder from the seam record; a piece that ends
+// at a cut (seam_end) writes its pending bytes out at the end instead of a flush (the oracle's
+// avr_ce_seam_flush): the bytes of the arithmetic's low up to the next piece's first byte
+template <int MODE, bool P32, bool SEQ = false, bool SPL = false>
+AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out, uint32_t flags,
+                        const SeamRec* seam = nullptr, bool seam_end = false) {
   const bool billing = (flags & kFlagBill) != 0;
   uint32_t bill[6] = {0, 0, 0, 0, 0, 0};
   uint32_t bill_pend = 0;
@@ -2573,6 +2657,16 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
 #endif
   } else {
     ce_init(ce);
+    if constexpr (SPL) {
+      if (seam) {
+        ce.low = seam->ce_low;
+        ce.range = seam->ce_range;
+        ce.queue = seam->ce_queue;
+        ce.outstanding = seam->ce_outstanding;
+        ce.cache = seam->ce_cache;
+        ce.have_cache = 1;
+      }
+    }
     vtab_load(vt, T);
   }
   const int r = MODE == MODE_COMPRESS ? 1 : 0;
@@ -2796,6 +2890,18 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
     atomicAdd(&avr_prof[21], (unsigned long long)(PROF_T() - t_start));
   }
 #endif
+  if constexpr (SPL) {
+    if (MODE == MODE_DECOMPRESS && seam_end) {
+      const uint32_t carry = ce.low >> (ce.queue + 18);
+      if (ce.have_cache) {
+        if (ce.cache + carry > 0xff) ce.err = 1;
+        out_byte(o, ce.cache + carry);
+      } else if (carry) {
+        ce.err = 1;
+      }
+      if (ce.outstanding) out_repeat(o, (0xff + carry) & 0xff, ce.outstanding);
+    }
+  }
   if (__lane_id() == 0) {
     sh->c_err = MODE == MODE_COMPRESS ? re.err : ce.err;
     sh->c_len = out_total(o);
@@ -2805,8 +2911,9 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
 }
 
 // Combine the two waves' results (after a workgroup barrier), with run_slice_inline's semantics.
+// seam_end: a piece that ends at a cut (its last byte is not the slice's)
 template <int MODE>
-AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_result* res) {
+AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_result* res, bool seam_end = false) {
   int status = sh->p_status;
   if (sh->c_err) status = AVR_SLICE_CODER;
   if (MODE == MODE_COMPRESS && !status && !sh->p_stop_ok) status = AVR_SLICE_NO_STOP;
@@ -2815,15 +2922,15 @@ AVR_FI void finish_slice(const Shared* sh, const avr_slice_desc* d, avr_slice_re
     status = AVR_SLICE_OVERFLOW;
     len = d->out_capacity;
   }
-  if (MODE == MODE_DECOMPRESS && !status && len && sh->c_last == 0x80) len--;  // recode.cpp:1503-1505
+  if (MODE == MODE_DECOMPRESS && !status && len && sh->c_last == 0x80 && !seam_end) len--;  // recode.cpp:1503-1505
   res->out_len = len;
   res->status = status;
   for (int i = 0; i < 6; i++) res->bill[i] = sh->bill[i];
 }
 
 // Single-wave slice (the generator: CABAC encode inline, no coder wave).
-template <int MODE, bool RM, bool FLD, bool P32>
-AVR_FI void run_slice_inline(Walker<MODE, RM, FLD, P32>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
+template <int MODE, bool RM, bool FLD, bool P32, bool SPL>
+AVR_FI void run_slice_inline(Walker<MODE, RM, FLD, P32, SPL>& w, const avr_slice_desc* d, const uint8_t* in, uint8_t* out,
                              avr_slice_result* res) {
   begin_slice(w, d, in, out);
   profile_slice(w);
@@ -2861,14 +2968,29 @@ constexpr int slice_threads() {
 // register one).
 // MG: the launch may keep the model row in global scratch (the persistent kernel, which every wide
 // launch uses); the resident kernel's row is always in LDS (a constant: no branch at its accesses).
-template <int MODE, bool FLD, bool P32, bool MG>
+template <int MODE, bool FLD, bool P32, bool MG, bool SPL = false>
 AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice_desc* descs, int s, const uint8_t* in,
                            uint8_t* out, avr_slice_result* res, uint16_t* est_g, uint32_t flags, uint32_t cell,
-                           uint32_t qiter = 0) {
+                           uint32_t qiter = 0, const SplitArgs* sp = nullptr) {
   const avr_slice_desc* d = &descs[s];
-  Walker<MODE, false, FLD, P32> w;
+  Walker<MODE, false, FLD, P32, SPL> w;
   w.sh = (Shared*)smem;
-  w.ring = (typename Walker<MODE, false, FLD, P32>::ERec*)(smem + sizeof(Shared));
+  w.ring = (typename Walker<MODE, false, FLD, P32, SPL>::ERec*)(smem + sizeof(Shared));
+  bool seam_end = false;
+  if constexpr (SPL) {
+    const PieceCtl c = sp->ctl[s];
+    w.seam = c.seam >= 0 ? (const SeamRec*)(sp->recs + (size_t)c.seam * sp->rec_stride) : nullptr;
+    w.piece_mbs = c.n_mbs;
+    w.cut = 0;
+    seam_end = c.n_mbs != 0;
+    w.snap = MODE == MODE_COMPRESS && c.snap >= 0 ? sp->recs + (size_t)c.snap * sp->rec_stride : nullptr;
+    w.snap_cap = c.snap_cap;
+    w.snap_n = 0;
+    w.snap_last = 0;
+    w.split_bits = sp->split_bits;
+    w.rec_stride = sp->rec_stride;
+    w.snap_count = sp->snap_n ? sp->snap_n + s : nullptr;
+  }
   w.mring_global = MG && !FLD && (flags & kFlagMringGlobal);
   w.mring = w.mring_global ? (uint32_t*)(est_g + kEstMring)
                            : (uint32_t*)(smem + sizeof(Shared) + (size_t)(flags >> kFlagRingShift) * sizeof(EdgeCore));
@@ -2913,11 +3035,38 @@ AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice
     AVR_PLACE_T(s, 1);
   }
   else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
+  else if constexpr (SPL) coder_slice<MODE, P32, false, true>(w.sh, w.T, d, out, flags, w.seam, seam_end);
   else coder_slice<MODE, P32>(w.sh, w.T, d, out, flags);
   if (MG) QTRACE(wave, qiter << 8 | 4);
   __syncthreads();
   if (MG) QTRACE(wave, qiter << 8 | 5);
-  if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s]);
+  if (threadIdx.x == 0) finish_slice<MODE>(w.sh, d, &res[s], seam_end);
+}
+
+// The long-slice split's launches (avr_kernels.h SplitArgs): progressive frame slices and pieces of
+// the parallel model on arithmetic_code<uint64_t, uint8_t>, the model row in LDS; each workgroup
+// takes descriptors blockIdx.x, blockIdx.x + gridDim.x, ... (a grid of at most the resident slots:
+// one estimator scratch per workgroup).  Compress: a descriptor with PieceCtl::snap >= 0 is a whole
+// long slice whose cut records are taken (its own output is the unsplit stream); the other
+// descriptors are the pieces (seam >= 0: started from a record, n_mbs > 0: stopped at the next cut).
+// Decompress: the pieces, from records the host wrote (the container's seams).
+template <int MODE>
+__global__ __launch_bounds__(192, 4) void slices_split_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
+                                                             const uint8_t* in, uint8_t* out, avr_slice_result* res,
+                                                             uint16_t* est_scratch, SplitArgs sp, uint32_t flags) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  uint32_t cell = kNoCell;
+  bool loaded = false;
+  for (int s = blockIdx.x; s < n; s += gridDim.x) {
+    __syncthreads();   // the previous descriptor's finish_slice has read the workgroup's LDS
+    if (!loaded) {
+      load_hot_tables((Shared*)smem, G);
+      loaded = true;
+      if (threadIdx.x < 64) cell = cu_cell();
+    }
+    parallel_slice<MODE, false, false, false, true>(smem, G, descs, s, in, out, res,
+                                                    est_scratch + (size_t)blockIdx.x * kEstGlobal, flags, cell, 0, &sp);
+  }
 }
 
 // FLD = false: the progressive frames of the batch; FLD = true: its field pictures and MBAFF frames

@@ -79,6 +79,21 @@ const char* avr_last_error(const avr_ctx* ctx);
 /* free a buffer returned by the library */
 void avr_free(void* p);
 
+/* The parallel model's long-slice split (this library's own format; not in the reference, which
+ * decodes a slice as one chain, recode.cpp:1411-1520).  The whole-file compress of AVR_MODEL_PARALLEL
+ * cuts a progressive-frame slice at macroblock-row starts into pieces -- a cut candidate every
+ * 8 * split_bytes decoded CABAC bits with half a piece still ahead -- each re-coded with a fresh
+ * model, so the slice decompresses one workgroup per piece.  Block.cabac holds the pieces' streams
+ * one after the other; Block field 16 ("seams", zlib) what each piece's decompress needs from before
+ * it (its first macroblock and output byte, the CABAC re-encoder's state, the context states, the
+ * upper row's neighbour fields).  Such containers decompress through the whole-file calls
+ * (avr_decompress_file(s), avr_roundtrip_file(s)); the per-slice paths (avr_plan_decompress,
+ * avr_dec_plan_load, the hooks sessions) refuse them with AVR_ERR_UNSUPPORTED.  split_bytes = 0: no
+ * split.  Default: the environment's AVR_SPLIT_BYTES, else 131072.  Checked by the oracle's
+ * restatement (oracle/oracle_seams.c). */
+int avr_set_split_bytes(avr_ctx* ctx, size_t split_bytes);
+size_t avr_get_split_bytes(const avr_ctx* ctx);
+
 /* ------------------------------------------------------------------ whole files (host memory) */
 /* in: an MP4 (avcC) or Annex-B H.264 file.  *out: serialized Recoded protobuf (recode.proto). */
 int avr_compress_file(avr_ctx* ctx, const uint8_t* in, size_t n, int model, uint8_t** out, size_t* out_len);

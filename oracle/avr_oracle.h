@@ -325,9 +325,9 @@ typedef struct {
   uint8_t *edge;                   /* AVR_EDGE_BYTES * mb_width (malloc'd) */
 } avr_seam_t;
 /* split_bytes of the whole-file compress (0: no split): AVR_SPLIT_BYTES from the environment, else
- * AVR_SPLIT_BYTES_DEFAULT; avr_set_split_bytes overrides both */
-size_t avr_split_bytes(void);
-void avr_set_split_bytes(size_t bytes);
+ * AVR_SPLIT_BYTES_DEFAULT; avr_oracle_set_split_bytes overrides both */
+size_t avr_oracle_split_bytes(void);
+void avr_oracle_set_split_bytes(size_t bytes);
 /* The re-encoder's state where the CABAC decoder stands after `bitpos` bits (9 + renormalisation
  * shifts) with codIOffset `offset` and codIRange `range` on this payload: 0, or -1 when the cut
  * cannot be placed there (the arithmetic's pending digits reach too far back). */

@@ -138,7 +138,7 @@ int main(int argc, char **argv) {
   if (!strcmp(cmd, "slices")) return cmd_slices(file, n);
   if (!strcmp(cmd, "pieces")) {   /* the parallel model's long-slice split, piece by piece */
     int ns = 0, np = 0;
-    int bad = avr_check_pieces(file, n, avr_split_bytes(), &ns, &np);
+    int bad = avr_check_pieces(file, n, avr_oracle_split_bytes(), &ns, &np);
     printf("split slices %d pieces %d mismatches %d\n", ns, np, bad);
     return bad != 0;
   }

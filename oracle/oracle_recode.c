@@ -844,7 +844,7 @@ int avr_compress(const uint8_t *file, size_t n, int mode, uint8_t **out, size_t 
       avr_model_t *m = ref ? model : model_new_p(mode == AVR_MODE_P32);
       obuf_t rc, seams;
       size_t bins = 0;
-      int r = compress_slice_split(m, &s, &rc, &bins, mode == AVR_MODE_P ? avr_split_bytes() : 0, &seams);
+      int r = compress_slice_split(m, &s, &rc, &bins, mode == AVR_MODE_P ? avr_oracle_split_bytes() : 0, &seams);
       if (!ref) {
         size_t unused[8] = {0};
         avr_model_bills(m, avr_last_bill, unused);

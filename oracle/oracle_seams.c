@@ -24,12 +24,12 @@
 
 static long split_override = -1;
 
-size_t avr_split_bytes(void) {
+size_t avr_oracle_split_bytes(void) {
   if (split_override >= 0) return (size_t)split_override;
   const char *e = getenv("AVR_SPLIT_BYTES");
   return e ? (size_t)strtoull(e, NULL, 10) : (size_t)AVR_SPLIT_BYTES_DEFAULT;
 }
-void avr_set_split_bytes(size_t bytes) { split_override = (long)bytes; }
+void avr_oracle_set_split_bytes(size_t bytes) { split_override = (long)bytes; }
 
 int avr_seam_encoder(const uint8_t *payload, size_t n, size_t bitpos, uint32_t offset, uint32_t range,
                      avr_seam_t *s) {

@@ -66,13 +66,17 @@ def lps_table():
     return list((ctypes.c_uint8 * 512).in_dll(L, "avr_lps_range"))
 
 
-def oracle_cli(cmd, path, mode="R", out=None):
-    """Run recode_oracle; returns stdout bytes (or the output file's bytes)."""
+def oracle_cli(cmd, path, mode="R", out=None, split_bytes=None):
+    """Run recode_oracle; returns stdout bytes (or the output file's bytes).  split_bytes: the parallel
+    model's long-slice split for this run (AVR_SPLIT_BYTES; None: the environment's / the default)."""
     _, cli = build_oracle()
+    env = dict(os.environ)
+    if split_bytes is not None:
+        env["AVR_SPLIT_BYTES"] = str(int(split_bytes))
     with tempfile.TemporaryDirectory() as td:
         o = Path(td) / "out.bin"
         args = [str(cli), cmd] + {"R": [], "P": ["-p"], "P32": ["-p32"], "C": ["-c"]}[mode] + [str(path), str(o)]
-        r = subprocess.run(args, capture_output=True)
+        r = subprocess.run(args, capture_output=True, env=env)
         if r.returncode != 0:
             raise RuntimeError(f"recode_oracle {cmd} failed: {r.stderr.decode()}")
         if cmd == "roundtrip":

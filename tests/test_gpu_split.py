@@ -1,0 +1,82 @@
+"""The parallel model's long-slice split on the device (avr_k_split.hip; include/avrecode.h
+avr_set_split_bytes; the format restated by the oracle, oracle/oracle_seams.c).
+
+* x264 fixtures at small split sizes: the device's containers equal the oracle's byte for byte
+  (pieces' streams, seams fields: cut positions, re-encoder states, context states, upper-row edges),
+  through the checked single-file compress and the batched one, and decompress on the device (one
+  workgroup per piece) to the input;
+* a 4K 4:4:4 intra slice (the configs[4] corpus's floor) at the default split size: cut into pieces,
+  equal to the oracle's container, restored by the device, and the oracle's sequential decompress of
+  the device's container restores it too;
+* split off (0): no seams, the plain parallel-model container."""
+import tempfile
+from pathlib import Path
+
+import pytest
+
+from _oracle import ROOT, oracle_cli
+
+torch = pytest.importorskip("torch")
+import avrecode_amd as avr  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+FIX = ROOT / "tests" / "fixtures"
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = avr.Context(0)
+    yield c
+    c.close()
+
+
+def _cut_blocks(avrc):
+    info, _ = avr.describe_container(avrc)
+    return [b for b in info["blocks"] if "seams" in b]
+
+
+@pytest.mark.parametrize("split_bytes", [512, 2048])
+@pytest.mark.parametrize("name", ["realshort.mp4", "cockatoo.mp4"])
+def test_fixture_split_matches_oracle(ctx, name, split_bytes):
+    data = (FIX / name).read_bytes()
+    ctx.split_bytes = split_bytes
+    try:
+        avrc = ctx.compress(data, avr.MODEL_PARALLEL)          # checked: pieces decompressed and compared
+        assert _cut_blocks(avrc)
+        assert avrc == oracle_cli("compress", FIX / name, mode="P", split_bytes=split_bytes)
+        assert ctx.decompress(avrc) == data
+        outs = ctx.compress_files([data, data], avr.MODEL_PARALLEL)
+        assert outs == [avrc, avrc]
+        back, _ = ctx.roundtrip_files([data], avr.MODEL_PARALLEL)   # unchecked first pass
+        assert back == [avrc]
+    finally:
+        ctx.split_bytes = 131072
+
+
+def test_split_off_is_the_plain_container(ctx):
+    data = (FIX / "realshort.mp4").read_bytes()
+    ctx.split_bytes = 0
+    try:
+        avrc = ctx.compress(data, avr.MODEL_PARALLEL)
+        assert not _cut_blocks(avrc)
+        assert avrc == oracle_cli("compress", FIX / "realshort.mp4", mode="P", split_bytes=0)
+    finally:
+        ctx.split_bytes = 131072
+
+
+def test_4k_444_intra_slice_is_split(ctx):
+    data = ctx.synthesize(avr.SynthParams(mb_width=240, mb_height=135, slice_type=2, slice_qp=30, chroma_format_idc=3,
+                                          transform_8x8_mode=1, seed=4006, slices_per_picture=1, gop_length=1), 1)
+    assert ctx.split_bytes == 131072
+    avrc = ctx.compress(data, avr.MODEL_PARALLEL)
+    cut = _cut_blocks(avrc)
+    assert len(cut) == 1
+    assert ctx.decompress(avrc) == data
+    with tempfile.TemporaryDirectory() as td:
+        f = Path(td) / "k.264"
+        f.write_bytes(data)
+        assert avrc == oracle_cli("compress", f, mode="P", split_bytes=131072)
+        g = Path(td) / "k.avrc"
+        g.write_bytes(avrc)
+        assert oracle_cli("decompress", g) == data
+
