@@ -612,9 +612,11 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
 //   - Block field 16 ("seams", zlib) carries, per cut, what the piece after it needs: its first
 //     macroblock, its first output byte q, the re-encoder state, the CABAC contexts, last_dqp_nz
 //     and the upper row's edges (the parse's neighbour fields).
-// Compress takes the long slices through the split kernel twice (avr_k_split.hip): a whole-slice
-// pass that records the candidates (on its own stream, beside the rest of the batch), then the
-// pieces.  Decompress runs the pieces side by side and splices them: piece i's bytes up to cut i's q.
+// Compress takes the long slices through the split kernels twice (avr_k_split.hip): the cut scan --
+// the CABAC parse of each whole slice alone (a trace walk without output: no model, one wave),
+// recording the candidates, on its own stream beside the rest of the batch -- then the pieces (a
+// slice without a cut: one piece).  Decompress runs the pieces side by side and splices them: piece
+// i's bytes up to cut i's q.
 constexpr size_t kSplitBytesDefault = 131072;
 
 bool split_candidate(const avr_slice_desc& d, size_t split_bytes) {
@@ -734,11 +736,12 @@ bool seams_decode(const uint8_t* p, size_t n, int mb_width, size_t rec_stride, S
 }
 
 // Compress of the long slices, in two calls around the rest of the batch: begin uploads them and
-// launches the whole-slice pass with the cut records on the split stream; finish takes the cuts,
-// compresses the pieces and (verify) decompresses them and compares.
+// launches the split compress on the split stream (each slice cut as it is walked: the records,
+// the pieces' streams one after the other, their ends); finish checks every cut against the host's
+// restatement of the re-encoder state, and (verify) decompresses the pieces and compares.
 struct SplitOut {
   int32_t status = 0;
-  std::vector<uint8_t> recoded, seams;   // seams empty: no cut (recoded = the unsplit stream)
+  std::vector<uint8_t> recoded, seams;   // seams empty: no cut
   avr_slice_result bill{};
 };
 struct SplitJob {
@@ -768,11 +771,11 @@ int split_begin(avr_ctx* c, SplitJob* j, size_t split_bytes, uint32_t flags) {
     append_aligned(&j->arena, s.payload(), s.read_limit, 16, &d.payload_offset);
     d.payload_size = (uint32_t)s.size;
     d.read_limit = (uint32_t)s.read_limit;
-    d.out_capacity = (uint32_t)(s.size * 2 + 256);
+    const uint32_t cap = (uint32_t)(8ull * s.size / j->split_bits) + 1;
+    d.out_capacity = (uint32_t)(s.size * 2 + 256 + 64 * (size_t)cap);
     d.out_offset = j->out_total;
     j->out_total += ((uint64_t)d.out_capacity + 15) & ~15ull;
     j->max_w = std::max(j->max_w, d.mb_width);
-    const uint32_t cap = (uint32_t)(8ull * s.size / j->split_bits) + 1;
     j->ctl[k] = avr::PieceCtl{-1, 0, (int32_t)j->nrec, cap};
     j->nrec += cap;
   }
@@ -784,7 +787,7 @@ int split_begin(avr_ctx* c, SplitJob* j, size_t split_bytes, uint32_t flags) {
   HIP_TRY(c, c->sp_res.reserve(sizeof(avr_slice_result) * n));
   HIP_TRY(c, c->sp_ctl.reserve(sizeof(avr::PieceCtl) * n));
   HIP_TRY(c, c->sp_recs.reserve(j->stride * j->nrec + 64));
-  HIP_TRY(c, c->sp_snapn.reserve(sizeof(uint32_t) * n));
+  HIP_TRY(c, c->sp_snapn.reserve(sizeof(uint32_t) * ((size_t)n + j->nrec)));
   HIP_TRY(c, c->sp_est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * std::max(1, grid), true));
   HIP_TRY(c, hipEventCreate(&j->e0));
   HIP_TRY(c, hipEventCreate(&j->e1));
@@ -792,13 +795,14 @@ int split_begin(avr_ctx* c, SplitJob* j, size_t split_bytes, uint32_t flags) {
   HIP_TRY(c, hipMemcpyAsync(c->sp_in.p, j->arena.data(), j->arena.size(), hipMemcpyHostToDevice, st));
   HIP_TRY(c, hipMemcpyAsync(c->sp_descs.p, j->d.data(), sizeof(avr_slice_desc) * n, hipMemcpyHostToDevice, st));
   HIP_TRY(c, hipMemcpyAsync(c->sp_ctl.p, j->ctl.data(), sizeof(avr::PieceCtl) * n, hipMemcpyHostToDevice, st));
-  HIP_TRY(c, hipMemsetAsync(c->sp_snapn.p, 0, sizeof(uint32_t) * n, st));
+  HIP_TRY(c, hipMemsetAsync(c->sp_snapn.p, 0, sizeof(uint32_t) * ((size_t)n + j->nrec), st));
   avr::SplitArgs sa;
   sa.ctl = c->sp_ctl.as<avr::PieceCtl>();
   sa.recs = c->sp_recs.as<uint8_t>();
   sa.rec_stride = (uint32_t)j->stride;
   sa.split_bits = j->split_bits;
   sa.snap_n = c->sp_snapn.as<uint32_t>();
+  sa.piece_end = sa.snap_n + n;
   HIP_TRY(c, hipEventRecord(j->e0, st));
   HIP_TRY(c, avr::launch_split(0, c->tables.as<avr::EngineTables>(), c->sp_descs.as<avr_slice_desc>(), n, j->max_w,
                                c->sp_in.as<uint8_t>(), c->sp_out.as<uint8_t>(), c->sp_res.as<avr_slice_result>(),
@@ -808,10 +812,36 @@ int split_begin(avr_ctx* c, SplitJob* j, size_t split_bytes, uint32_t flags) {
 }
 
 // One launch of pieces on the split stream: descs / ctl uploaded, records already in sp_recs,
-// results and outputs downloaded.
+// results and outputs downloaded -- waited for, or (pending != nullptr) left in flight for
+// split_wait, so the rest of a batch runs beside it.
+// (The downloads wait for split_wait: a copy into pageable host memory would block the host until
+// the kernel before it is done, and with it the launches meant to run beside it.)
+struct SplitPending {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  void* res = nullptr;
+  void* out = nullptr;
+  const void* res_dev = nullptr;
+  const void* out_dev = nullptr;
+  size_t res_bytes = 0, out_bytes = 0;
+};
+bool split_timing() { return getenv("AVR_SPLIT_TIMING") != nullptr; }
+int split_wait(avr_ctx* c, SplitPending* pend) {
+  if (!pend->e0) return AVR_OK;
+  HIP_TRY(c, hipStreamSynchronize(c->split_stream));
+  HIP_TRY(c, hipMemcpy(pend->res, pend->res_dev, pend->res_bytes, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(pend->out, pend->out_dev, pend->out_bytes, hipMemcpyDeviceToHost));
+  float ms = 0;
+  HIP_TRY(c, hipEventElapsedTime(&ms, pend->e0, pend->e1));
+  if (split_timing()) fprintf(stderr, "split: pieces kernel %.3f s\n", 1e-3 * ms);
+  c->phase.kernel_s += 1e-3 * ms;
+  (void)hipEventDestroy(pend->e0);
+  (void)hipEventDestroy(pend->e1);
+  pend->e0 = pend->e1 = nullptr;
+  return AVR_OK;
+}
 int split_launch(avr_ctx* c, int mode, std::vector<avr_slice_desc>& d, const std::vector<avr::PieceCtl>& ctl,
                  const uint8_t* in_dev, int max_w, size_t stride, uint32_t flags, std::vector<avr_slice_result>* res,
-                 Bytes* out, DevBuf* out_dev) {
+                 Bytes* out, DevBuf* out_dev, SplitPending* pending = nullptr) {
   const int n = (int)d.size();
   uint64_t total = 0;
   for (auto& x : d) {
@@ -833,23 +863,22 @@ int split_launch(avr_ctx* c, int mode, std::vector<avr_slice_desc>& d, const std
   sa.ctl = c->sp_ctl.as<avr::PieceCtl>();
   sa.recs = c->sp_recs.as<uint8_t>();
   sa.rec_stride = (uint32_t)stride;
-  hipEvent_t e0, e1;
-  HIP_TRY(c, hipEventCreate(&e0));
-  HIP_TRY(c, hipEventCreate(&e1));
-  HIP_TRY(c, hipEventRecord(e0, st));
+  SplitPending local;
+  SplitPending* pend = pending ? pending : &local;
+  HIP_TRY(c, hipEventCreate(&pend->e0));
+  HIP_TRY(c, hipEventCreate(&pend->e1));
+  HIP_TRY(c, hipEventRecord(pend->e0, st));
   HIP_TRY(c, avr::launch_split(mode, c->tables.as<avr::EngineTables>(), c->sp_descs.as<avr_slice_desc>(), n, max_w,
                                in_dev, out_dev->as<uint8_t>(), c->sp_res.as<avr_slice_result>(), c->sp_est.as<uint16_t>(),
                                sa, flags, st));
-  HIP_TRY(c, hipEventRecord(e1, st));
-  HIP_TRY(c, hipMemcpyAsync(res->data(), c->sp_res.p, sizeof(avr_slice_result) * n, hipMemcpyDeviceToHost, st));
-  HIP_TRY(c, hipMemcpyAsync(out->data(), out_dev->p, total, hipMemcpyDeviceToHost, st));
-  HIP_TRY(c, hipStreamSynchronize(st));
-  float ms = 0;
-  HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
-  c->phase.kernel_s += 1e-3 * ms;
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  return AVR_OK;
+  HIP_TRY(c, hipEventRecord(pend->e1, st));
+  pend->res = res->data();
+  pend->res_dev = c->sp_res.p;
+  pend->res_bytes = sizeof(avr_slice_result) * n;
+  pend->out = out->data();
+  pend->out_dev = out_dev->p;
+  pend->out_bytes = total;
+  return pending ? AVR_OK : split_wait(c, pend);
 }
 
 // the regenerated bytes of a split slice: piece i's bytes up to cut i's q (the cut's first byte),
@@ -882,134 +911,113 @@ int split_finish(avr_ctx* c, SplitJob* j, bool verify, std::vector<SplitOut>* ou
   out->assign(n, SplitOut());
   if (!n) return AVR_OK;
   hipStream_t st = c->split_stream;
-  // 1) the whole-slice pass: statuses, unsplit streams, cut records
+  // 1) the split compress: statuses, streams, cut records, piece ends
   std::vector<avr_slice_result> r1(n);
-  std::vector<uint32_t> snapn(n);
+  std::vector<uint32_t> cnt((size_t)n + j->nrec);
   Bytes out1(j->out_total), recs((size_t)j->stride * j->nrec);
   HIP_TRY(c, hipMemcpyAsync(r1.data(), c->sp_res.p, sizeof(avr_slice_result) * n, hipMemcpyDeviceToHost, st));
-  HIP_TRY(c, hipMemcpyAsync(snapn.data(), c->sp_snapn.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(cnt.data(), c->sp_snapn.p, sizeof(uint32_t) * cnt.size(), hipMemcpyDeviceToHost, st));
   HIP_TRY(c, hipMemcpyAsync(out1.data(), c->sp_out.p, j->out_total, hipMemcpyDeviceToHost, st));
   HIP_TRY(c, hipMemcpyAsync(recs.data(), c->sp_recs.p, recs.size(), hipMemcpyDeviceToHost, st));
   HIP_TRY(c, hipStreamSynchronize(st));
   float ms = 0;
   HIP_TRY(c, hipEventElapsedTime(&ms, j->e0, j->e1));
+  if (split_timing()) fprintf(stderr, "split: compress kernel %.3f s (%d slices)\n", 1e-3 * ms, n);
   c->phase.kernel_s += 1e-3 * ms;
   (void)hipEventDestroy(j->e0);
   (void)hipEventDestroy(j->e1);
   j->e0 = j->e1 = nullptr;
-  // 2) the cuts: records whose re-encoder state can be placed, q moving forward
-  std::vector<std::vector<uint32_t>> cut_rec(n);
-  std::vector<std::vector<SeamCe>> cut_ce(n);
+  const uint32_t* piece_end = cnt.data() + n;
+  // 2) every cut checked against the host's restatement (seam_encoder), the pieces' lengths
+  std::vector<std::vector<const avr::SeamRec*>> cuts(n);
+  std::vector<std::vector<SeamCe>> ces(n);
+  std::vector<std::vector<uint32_t>> plen(n);
   for (int k = 0; k < n; k++) {
     SplitOut& so = (*out)[k];
     so.status = r1[k].status;
     so.bill = r1[k];
     if (so.status) continue;
     const avr::SliceInfo& s = *j->sl[k];
-    for (uint32_t i = 0; i < std::min(snapn[k], j->ctl[k].snap_cap); i++) {
-      const uint32_t ri = (uint32_t)j->ctl[k].snap + i;
-      avr::SeamRec* r = (avr::SeamRec*)(recs.data() + (size_t)ri * j->stride);
+    const uint32_t nc = cnt[k], base = (uint32_t)j->ctl[k].snap;
+    if (nc >= j->ctl[k].snap_cap || piece_end[base + nc] != r1[k].out_len) {
+      so.status = AVR_SLICE_CODER;
+      continue;
+    }
+    for (uint32_t i = 0; i < nc && !so.status; i++) {
+      const avr::SeamRec* r = (const avr::SeamRec*)(recs.data() + (size_t)(base + i) * j->stride);
       SeamCe ce;
       const uint64_t bitpos = 8ull * r->cd_next - r->cd_k;
-      if (!seam_encoder(s.payload(), s.size, bitpos, r->cd_low >> r->cd_k, r->cd_range, &ce)) continue;
-      if (!cut_ce[k].empty() && ce.q <= cut_ce[k].back().q) continue;
-      r->ce_low = ce.low;
-      r->ce_range = ce.range;
-      r->ce_outstanding = ce.outstanding;
-      r->ce_cache = ce.cache;
-      r->ce_queue = ce.queue;
-      cut_rec[k].push_back(ri);
-      cut_ce[k].push_back(ce);
+      if (!seam_encoder(s.payload(), s.size, bitpos, r->cd_low >> r->cd_k, r->cd_range, &ce) || ce.q != r->q ||
+          ce.low != r->ce_low || ce.range != r->ce_range || ce.outstanding != r->ce_outstanding ||
+          ce.cache != r->ce_cache || ce.queue != r->ce_queue)
+        so.status = AVR_SLICE_CODER;
+      cuts[k].push_back(r);
+      ces[k].push_back(ce);
     }
-    if (cut_rec[k].empty())   // no cut: the unsplit stream
+    for (uint32_t i = 0; i <= nc; i++) plen[k].push_back(piece_end[base + i] - (i ? piece_end[base + i - 1] : 0u));
+    if (!so.status)
       so.recoded.assign(out1.begin() + j->d[k].out_offset, out1.begin() + j->d[k].out_offset + r1[k].out_len);
   }
-  // 3) the pieces, compressed (records: the decoder fields the first pass wrote)
-  std::vector<avr_slice_desc> pd;
-  std::vector<avr::PieceCtl> pc;
-  std::vector<int> first_piece(n, -1);
-  for (int k = 0; k < n; k++) {
-    if (cut_rec[k].empty()) continue;
-    first_piece[k] = (int)pd.size();
-    const size_t np = cut_rec[k].size() + 1;
-    for (size_t i = 0; i < np; i++) {
-      avr_slice_desc d = j->d[k];
-      const avr::SeamRec* r = i ? (const avr::SeamRec*)(recs.data() + (size_t)cut_rec[k][i - 1] * j->stride) : nullptr;
-      if (r) d.first_mb = (int32_t)r->first_mb;
-      const uint32_t next = i + 1 < np ? ((const avr::SeamRec*)(recs.data() + (size_t)cut_rec[k][i] * j->stride))->first_mb : 0;
-      pc.push_back(avr::PieceCtl{r ? (int32_t)cut_rec[k][i - 1] : -1, next ? next - (uint32_t)d.first_mb : 0u, -1, 0});
-      pd.push_back(d);
-    }
-  }
-  if (pd.empty()) return AVR_OK;
-  std::vector<avr_slice_result> r2;
-  Bytes out2;
-  if (int e = split_launch(c, 0, pd, pc, c->sp_in.as<uint8_t>(), j->max_w, j->stride, j->flags, &r2, &out2, &c->sp_out))
-    return e;
-  // 4) verify: the pieces decompressed from the records as a container would give them, spliced and
-  //    compared with the payload
-  std::vector<char> ok(n, 1);
+  // 3) verify: the pieces decompressed from the records as a container gives them, spliced, compared
   if (verify) {
-    HIP_TRY(c, hipMemcpyAsync(c->sp_recs.p, recs.data(), recs.size(), hipMemcpyHostToDevice, st));
+    std::vector<avr_slice_desc> dd;
+    std::vector<avr::PieceCtl> pc;
+    std::vector<int> first(n, -1);
     Bytes arena;
-    std::vector<avr_slice_desc> dd(pd.size());
-    for (size_t i = 0; i < pd.size(); i++) {
-      dd[i] = pd[i];
-      append_aligned(&arena, out2.data() + pd[i].out_offset, r2[i].out_len, 16, &dd[i].payload_offset);
-      dd[i].payload_size = dd[i].read_limit = r2[i].out_len;
-      dd[i].out_capacity = pd[i].payload_size + 4096;
-    }
-    HIP_TRY(c, c->sp_in2.reserve(arena.size() + 4096));
-    HIP_TRY(c, hipMemcpyAsync(c->sp_in2.p, arena.data(), arena.size(), hipMemcpyHostToDevice, st));
-    std::vector<avr_slice_result> r3;
-    Bytes out3;
-    if (int e = split_launch(c, 1, dd, pc, c->sp_in2.as<uint8_t>(), j->max_w, j->stride, 0, &r3, &out3, &c->sp_out2))
-      return e;
     for (int k = 0; k < n; k++) {
-      if (first_piece[k] < 0) continue;
-      const avr::SliceInfo& s = *j->sl[k];
-      const size_t np = cut_rec[k].size() + 1;
-      std::vector<const uint8_t*> p(np);
-      std::vector<uint32_t> len(np), q(np - 1);
-      std::vector<int32_t> stt(np);
+      if ((*out)[k].status) continue;
+      first[k] = (int)dd.size();
+      uint64_t off = 0;
+      const size_t np = cuts[k].size() + 1;
       for (size_t i = 0; i < np; i++) {
-        const int x = first_piece[k] + (int)i;
-        p[i] = out3.data() + dd[x].out_offset;
-        len[i] = r3[x].out_len;
-        stt[i] = r3[x].status | r2[x].status;
-        if (i + 1 < np) q[i] = cut_ce[k][i].q;
+        avr_slice_desc d = j->d[k];
+        if (i) d.first_mb = (int32_t)cuts[k][i - 1]->first_mb;
+        append_aligned(&arena, (*out)[k].recoded.data() + off, plen[k][i], 16, &d.payload_offset);
+        off += plen[k][i];
+        d.payload_size = d.read_limit = plen[k][i];
+        d.out_capacity = (uint32_t)j->sl[k]->size + 4096;
+        const uint32_t next = i + 1 < np ? cuts[k][i]->first_mb : 0u;
+        pc.push_back(avr::PieceCtl{i ? j->ctl[k].snap + (int32_t)i - 1 : -1, next ? next - (uint32_t)d.first_mb : 0u,
+                                   -1, 0});
+        dd.push_back(d);
       }
-      std::vector<uint8_t> regen;
-      ok[k] = splice_pieces(p, len, stt, q, &regen);
-      if (ok[k]) {
-        last_byte_patch(&regen, s.payload(), s.size);
-        ok[k] = regen.size() == s.size && memcmp(regen.data(), s.payload(), s.size) == 0;
+    }
+    if (!dd.empty()) {
+      HIP_TRY(c, c->sp_in2.reserve(arena.size() + 4096));
+      HIP_TRY(c, hipMemcpyAsync(c->sp_in2.p, arena.data(), arena.size(), hipMemcpyHostToDevice, st));
+      std::vector<avr_slice_result> r3;
+      Bytes out3;
+      if (int e = split_launch(c, 1, dd, pc, c->sp_in2.as<uint8_t>(), j->max_w, j->stride, 0, &r3, &out3, &c->sp_out2))
+        return e;
+      for (int k = 0; k < n; k++) {
+        if (first[k] < 0) continue;
+        const avr::SliceInfo& s = *j->sl[k];
+        const size_t np = cuts[k].size() + 1;
+        std::vector<const uint8_t*> p(np);
+        std::vector<uint32_t> len(np), q(np - 1);
+        std::vector<int32_t> stt(np);
+        for (size_t i = 0; i < np; i++) {
+          const int x = first[k] + (int)i;
+          p[i] = out3.data() + dd[x].out_offset;
+          len[i] = r3[x].out_len;
+          stt[i] = r3[x].status;
+          if (i + 1 < np) q[i] = ces[k][i].q;
+        }
+        std::vector<uint8_t> regen;
+        bool ok = splice_pieces(p, len, stt, q, &regen);
+        if (ok) {
+          last_byte_patch(&regen, s.payload(), s.size);
+          ok = regen.size() == s.size && memcmp(regen.data(), s.payload(), s.size) == 0;
+        }
+        if (!ok) (*out)[k].status = AVR_SLICE_NO_ROUNDTRIP;
       }
     }
   }
-  // 5) the blocks: the pieces' streams one after the other, the seams field
+  // 4) the seams fields
   for (int k = 0; k < n; k++) {
-    if (first_piece[k] < 0) continue;
     SplitOut& so = (*out)[k];
-    const size_t np = cut_rec[k].size() + 1;
-    std::vector<uint32_t> plen(np);
-    so.recoded.clear();
-    so.bill = avr_slice_result{};
-    for (size_t i = 0; i < np; i++) {
-      const int x = first_piece[k] + (int)i;
-      if (r2[x].status && !so.status) so.status = r2[x].status;
-      plen[i] = r2[x].out_len;
-      so.recoded.insert(so.recoded.end(), out2.begin() + pd[x].out_offset, out2.begin() + pd[x].out_offset + r2[x].out_len);
-      so.bill.bins += r2[x].bins;
-      so.bill.mbs += r2[x].mbs;
-      for (int b = 0; b < 6; b++) so.bill.bill[b] += r2[x].bill[b];
-    }
-    so.bill.out_len = (uint32_t)so.recoded.size();
-    if (!so.status && !ok[k]) so.status = AVR_SLICE_NO_ROUNDTRIP;
-    if (so.status) continue;
-    std::vector<const avr::SeamRec*> rr;
-    for (uint32_t ri : cut_rec[k]) rr.push_back((const avr::SeamRec*)(recs.data() + (size_t)ri * j->stride));
-    if (!seams_encode(rr, cut_ce[k], j->d[k].mb_width, plen, &so.seams)) return fail(c, AVR_ERR_DEVICE, "zlib failed");
+    if (so.status || cuts[k].empty()) continue;
+    if (!seams_encode(cuts[k], ces[k], j->d[k].mb_width, plen[k], &so.seams)) return fail(c, AVR_ERR_DEVICE, "zlib failed");
   }
   return AVR_OK;
 }
@@ -1881,25 +1889,42 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
   std::vector<avr_slice_result> res_of[3];
   std::vector<uint8_t> out_of[3];
   pc.mark_demux();
-  for (int m = AVR_MODEL_PARALLEL; m <= AVR_MODEL_PARALLEL32; m++)
-    if (!plans[m].descs.empty())
-      if (int r = run_plan(c, 1, false, plans[m], &res_of[m], &out_of[m], false, flags | coder_flag(m))) return r;
-  if (!rp.file_first.empty()) {
-    rp.file_first.push_back((int)rp.descs.size());
-    if (int r = run_plan(c, 1, true, rp, &res_of[0], &out_of[0], false, flags)) return r;
-  }
-  if (!sp.plan.descs.empty()) {   // the pieces of split blocks, then each block spliced
+  // the pieces of split blocks on the split stream, beside the other plans
+  std::vector<avr_slice_result> pr;
+  Bytes po;
+  SplitPending pend;
+  double t_split = 0;
+  if (!sp.plan.descs.empty()) {
     const double t = now_s();
     hipStream_t ss = c->split_stream;
     HIP_TRY(c, c->sp_in.reserve(sp.plan.arena.size() + 4096));
     HIP_TRY(c, c->sp_recs.reserve(sp.recs.size() + 64));
     HIP_TRY(c, hipMemcpyAsync(c->sp_in.p, sp.plan.arena.data(), sp.plan.arena.size(), hipMemcpyHostToDevice, ss));
     HIP_TRY(c, hipMemcpyAsync(c->sp_recs.p, sp.recs.data(), sp.recs.size(), hipMemcpyHostToDevice, ss));
-    std::vector<avr_slice_result> pr;
-    Bytes po;
     if (int r = split_launch(c, 1, sp.plan.descs, sp.ctl, c->sp_in.as<uint8_t>(), sp.plan.max_w, sp.stride, flags, &pr,
-                             &po, &c->sp_out))
+                             &po, &c->sp_out, &pend)) {
+      (void)hipStreamSynchronize(ss);
       return r;
+    }
+    t_split += now_s() - t;
+  }
+  auto drain = [&]() { (void)hipStreamSynchronize(c->split_stream); };
+  for (int m = AVR_MODEL_PARALLEL; m <= AVR_MODEL_PARALLEL32; m++)
+    if (!plans[m].descs.empty())
+      if (int r = run_plan(c, 1, false, plans[m], &res_of[m], &out_of[m], false, flags | coder_flag(m))) {
+        drain();
+        return r;
+      }
+  if (!rp.file_first.empty()) {
+    rp.file_first.push_back((int)rp.descs.size());
+    if (int r = run_plan(c, 1, true, rp, &res_of[0], &out_of[0], false, flags)) {
+      drain();
+      return r;
+    }
+  }
+  if (!sp.plan.descs.empty()) {   // the pieces of split blocks, then each block spliced
+    const double t = now_s();
+    if (int r = split_wait(c, &pend)) return r;
     for (int f = 0; f < nf; f++) {
       if (st[f]) continue;
       for (SplitBlock& x : jobs[f].splits) {
@@ -1918,7 +1943,7 @@ int decompress_files(avr_ctx* c, int nf, const uint8_t* const* in, const size_t*
         for (int i = 0; i < x.pieces && !x.status; i++) x.status = stt[i];
       }
     }
-    c->plan_wall += now_s() - t;
+    c->plan_wall += t_split + (now_s() - t);
   }
   int first_err = AVR_OK;
   for (int f = 0; f < nf; f++) {

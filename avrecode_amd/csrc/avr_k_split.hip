@@ -1,6 +1,6 @@
 // The long-slice split's kernels (avr_walker.h slices_split_kernel, avr_kernels.h SplitArgs): the
-// parallel model on arithmetic_code<uint64_t, uint8_t>, compress and decompress, in one translation
-// unit with its own CU board.
+// parallel model on arithmetic_code<uint64_t, uint8_t>, compress (whole slices, cut as they are
+// walked) and decompress (the pieces), in one translation unit with its own CU board.
 #include "avr_walker.h"
 
 namespace avr {

@@ -65,7 +65,8 @@ struct SeamRec {
   uint32_t cd_low, cd_range, cd_k, cd_next;   // compress: the CABAC decoder at the cut (CabacDecoder)
   uint32_t ce_low, ce_range, ce_outstanding, ce_cache;   // decompress: the re-encoder (CabacEncoder,
   int32_t ce_queue;                                     //   a cache byte always present)
-  uint32_t pad[5];
+  uint32_t q;                                 // the piece's first byte in the slice's CABAC bytes
+  uint32_t pad[4];
   uint8_t state[1024];                        // CABAC context bytes
   // then the upper row's EdgeCore records (kEdgeBytes per macroblock column)
 };
@@ -86,9 +87,11 @@ struct SplitArgs {
   uint8_t* recs = nullptr;      // rec_stride bytes per record
   uint32_t rec_stride = 0;
   uint32_t split_bits = 0;      // compress: a cut candidate every split_bits decoded bits
-  uint32_t* snap_n = nullptr;   // compress: records written per descriptor
+  uint32_t* snap_n = nullptr;   // compress: cuts made (records written) per descriptor
+  uint32_t* piece_end = nullptr;   // compress: the re-coded stream's length at the end of each piece,
+                                   //   one entry per record (from PieceCtl::snap)
 };
-// compress (mode 0) / decompress (1) of a batch of slices and pieces of progressive frames with the
+// compress (mode 0: whole long slices, cut as they are walked) / decompress (1: the pieces) with the
 // parallel model on arithmetic_code<uint64_t, uint8_t> (avr_k_split.hip): one workgroup per
 // descriptor, min(n, resident slots) workgroups; est holds that many estimator scratches
 int split_grid(int n, int max_mb_width);

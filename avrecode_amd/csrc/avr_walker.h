@@ -232,6 +232,9 @@ __host__ __device__ inline int op_class_pip_c(uint32_t c) { return c == 1 ? PIPC
 __host__ __device__ inline int op_class_pip_d(uint32_t c) { return c == 1 ? PIPC_SIG_MAP : c == 2 ? PIPC_SIG_EOB : PIPC_UNKNOWN; }
 constexpr uint32_t OP_FINISH = 1u << 30;
 constexpr uint32_t OP_END = 1u << 31;
+// compress rings of the long-slice split (SPL): with OP_FINISH at a cut -- the modeler starts a fresh
+// model after it, the coder a fresh stream (bit 29: no model or coder op reaches it)
+constexpr uint32_t OP_RESTART = 1u << 29;
 enum { OPK_DECISION = 0, OPK_BYPASS = 1, OPK_TERMINATE = 2, OPK_MACRO = 3 };
 
 constexpr uint32_t OPM_CACHE = 2, OPM_THR50 = 4;
@@ -701,29 +704,66 @@ struct Walker {
   int nref0, nref1, d8x8inf, x264_build, first_mb;
   // the long-slice split (SPL): the piece's start record (nullptr: the slice's own start) and
   // macroblock count (0: to end_of_slice); compress: where the cut records go (snap, snap_cap of
-  // them, rec_stride apart; snap_n written, count to *snap_count), a candidate every split_bits
-  // decoded bits (snap_last: the previous one)
+  // them, rec_stride apart; snap_n made, count to *snap_count), a candidate every split_bits decoded
+  // bits (snap_last: the previous one; snap_q: the previous cut's first byte)
   const SeamRec* seam;
   uint8_t* snap;
   uint32_t* snap_count;
-  uint32_t snap_cap, snap_n, snap_last, split_bits, rec_stride, piece_mbs;
+  uint32_t snap_cap, snap_n, snap_last, snap_q, split_bits, rec_stride, piece_mbs;
   int cut;                // the walk stopped at the piece's end (not at end_of_slice)
-  // A cut candidate at this row start (compress, SPL): the rule of oracle/oracle_recode.c
-  // c_row_start -- at least split_bits decoded bits since the last candidate and half of that still
-  // ahead in the payload.  The record: the decoder, the contexts (the cached lanes written back
-  // first), last_dqp_nz and the ring (the upper row's edges, model-row flag cleared).
-  AVR_FI void seam_snapshot(int addr) {
+  // The re-encoder's state where the decoder stands (the oracle's avr_seam_encoder): L = V - offset,
+  // V the payload's first bitpos bits, as bytes Z = F[sb..e) - (offset << r) (r = 8 e - bitpos pad
+  // bits); q = the last byte below m = (bitpos - 10) / 8 that is not 0xFF, the 0xFF bytes after it
+  // outstanding, the bits of L from byte m on in low.  A dozen scalar byte loads, at a cut candidate.
+  AVR_FI bool seam_place(uint32_t bitpos, uint32_t offset, uint32_t* ce) const {
+    if (bitpos < 26) return false;
+    const uint32_t m = (bitpos - 10) >> 3, sb = m > 12 ? m - 12 : 0, e = (bitpos + 7) >> 3, r = 8 * e - bitpos;
+    const uint32_t sub = offset << r;
+    uint32_t borrow = 0, low = 0, q = ~0u, cache = 0;
+    for (uint32_t j = e; j-- > sb;) {
+      const uint32_t t = e - 1 - j;
+      const uint32_t sbyte = t < 4 ? (sub >> (8 * t)) & 0xff : 0u;
+      const uint32_t f = j < in.limit ? (uint32_t)in.g[j] : 0u;
+      const uint32_t v = f - sbyte - borrow;
+      borrow = v >> 31;
+      const uint32_t z = v & 0xff;
+      if (j >= m) low |= z << (8 * t);
+      else if (q == ~0u && z != 0xff) q = j, cache = z;
+    }
+    if (borrow || q == ~0u) return false;
+    const uint32_t lowbits = bitpos - 8 * m;
+    ce[0] = (low >> r) & ((1u << lowbits) - 1);    // ce_low
+    ce[1] = cd.range;                               // ce_range
+    ce[2] = m - 1 - q;                              // ce_outstanding
+    ce[3] = cache;                                  // ce_cache
+    ce[4] = lowbits - 18;                           // ce_queue
+    ce[5] = q;
+    return true;
+  }
+  // A cut candidate at this row start (compress, SPL; the rule of oracle/oracle_recode.c
+  // c_row_start): at least split_bits decoded bits since the last candidate, half of that still ahead
+  // in the payload.  Where the re-encoder's state can be placed (and moves forward), the slice is cut
+  // here: the record (decoder, re-encoder, contexts with the cached lanes written back, last_dqp_nz,
+  // the ring's upper-row edges), then the piece's re-coded stream ends (encoder::finish) and the
+  // modeler starts a fresh model (OP_RESTART, taken alone: the walker waits until the modeler has
+  // retired it), and the model row reads zero for the new piece's first row.
+  AVR_FI void seam_cut(int addr) {
     const uint32_t pos = cd_bitpos(cd);
     if (pos - snap_last < split_bits || (uint64_t)pos + split_bits / 2 > 8ull * d->payload_size) return;
     snap_last = pos;
     if (snap_n >= snap_cap) return;
+    uint32_t ce[6];
+    if (!seam_place(pos, cd.low >> cd.k, ce) || (snap_n && ce[5] <= snap_q)) return;
+    snap_q = ce[5];
     rc_writeback();
     mc_store();
     uint32_t* r32 = (uint32_t*)(snap + (size_t)snap_n * rec_stride);
     const uint32_t lane = __lane_id();
     if (lane < 16) {
       const uint32_t v = lane == 0 ? (uint32_t)addr : lane == 1 ? (uint32_t)last_dqp_nz : lane == 2 ? cd.low
-                       : lane == 3 ? cd.range : lane == 4 ? (uint32_t)cd.k : lane == 5 ? cd.next : 0u;
+                       : lane == 3 ? cd.range : lane == 4 ? (uint32_t)cd.k : lane == 5 ? cd.next
+                       : lane == 6 ? ce[0] : lane == 7 ? ce[1] : lane == 8 ? ce[2] : lane == 9 ? ce[3]
+                       : lane == 10 ? ce[4] : lane == 11 ? ce[5] : 0u;
       r32[lane] = v;
     }
     const uint32_t* st = (const uint32_t*)sh->state;
@@ -731,6 +771,17 @@ struct Walker {
     const uint32_t* e = (const uint32_t*)ring;
     for (uint32_t i = lane; i < (uint32_t)W * 10; i += 64) r32[16 + 256 + i] = i % 10 ? e[i] : e[i] & ~kEdgeMringNz;
     snap_n++;
+    if constexpr (MODE == MODE_COMPRESS) {
+      push(OP_FINISH | OP_RESTART);
+      publish();
+      WD_T0;
+      while (ld_volatile(&sh->fifo_tail[0]) != ring0.head) {
+        WD_POLL(WD_TAKE, ring0.head, 0, sh->qnext);
+        __builtin_amdgcn_s_sleep(1);
+      }
+      for (uint32_t i = lane; i < (uint32_t)W * kMringDwords; i += 64) mring[i] = 0;
+      wave_sync();
+    }
   }
   uint32_t prio_cell, prio_cur;   // this slice's cell on the CU board, current priority
   AVR_FI void update_prio() {
@@ -2237,7 +2288,7 @@ AVR_FI void walk_slice(Walker<MODE, RM, FLD, P32, SPL>& w) {
   for (;;) {
     if (addr >= npic) { w.err = AVR_SLICE_BAD_MB_ADDR; break; }
     if constexpr (SPL && MODE == MODE_COMPRESS) {
-      if (w.snap && w.mb_x == 0 && w.mbs_done > 0) w.seam_snapshot(addr);
+      if (w.snap && w.mb_x == 0 && w.mbs_done > 0) w.seam_cut(addr);
     }
     PROF_BEGINW(ps0);
     if (!(FLD && w.mbaff)) {
@@ -2438,8 +2489,6 @@ AVR_FI void walker_slice(Walker<MODE, RM, FLD, P32, SPL>& w, const avr_slice_des
   begin_slice(w, d, in, nullptr);
   profile_slice(w);
   if constexpr (SPL) {
-    // a piece that ends at a cut: its own re-coded stream ends there (encoder::finish)
-    if (MODE == MODE_COMPRESS && w.cut) w.push(OP_FINISH);
     if (MODE == MODE_COMPRESS && w.snap && __lane_id() == 0) *w.snap_count = w.snap_n;
   }
   if (!RM) cu_post(w.prio_cell, 0);   // leave the CU board
@@ -2497,6 +2546,9 @@ AVR_FI uint32_t vgpr_zero() {
 // ops one by one.
 // lane L of v := x (x, L wave-uniform)
 AVR_FI uint32_t writelane(uint32_t v, uint32_t L, uint32_t x) { return __lane_id() == L ? x : v; }
+// SPL: a batch that holds OP_RESTART (the walker's cut, the batch's last op) ends with a fresh model:
+// the HBM table's logged entries, the LDS hash and the per-context estimators cleared
+template <bool SPL = false>
 AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
   uint32_t tail = 0, head1 = 0, tail1 = 0;
   uint64_t waited = 0;
@@ -2606,6 +2658,26 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
     if (live) sh->fifo[1][(head1 + lane) & (kFifo - 1)] = out_v;
     head1 += n;
     st_volatile(&sh->fifo_head[1], head1);
+    if constexpr (SPL) {
+      if (__ballot(live && (op_v & OP_RESTART))) {
+        const uint32_t nl = *(volatile uint32_t*)(est_g + kEstLogN);
+        if (nl == kEstLogOverflow) {
+          uint4* e4 = (uint4*)est_g;
+          for (uint32_t i = lane; i < (uint32_t)kEstTable / 8; i += 64) e4[i] = make_uint4(0, 0, 0, 0);
+        } else {
+          const uint32_t* lg = (const uint32_t*)(est_g + kEstLog);
+          for (uint32_t i = lane; i < nl; i += 64) est_g[lg[i]] = 0;
+        }
+        if (lane == 0) {
+          *(uint32_t*)(est_g + kEstLogN) = 0;
+          sh->elog_n = 0;
+        }
+        for (uint32_t i = lane; i < (uint32_t)kEstDefault + 2; i += 64) sh->est[i] = 0;
+        for (uint32_t i = lane; i < (uint32_t)kEtabSize + 64; i += 64) sh->etab[i] = 0;
+        __threadfence_block();
+        wave_sync();
+      }
+    }
     tail += n;
     ring_retire(sh, 0, tail);
   }
@@ -2629,9 +2701,12 @@ AVR_FI void model_slice(Shared* sh, uint16_t* est_g) {
 // SPL (decompress): a piece after a cut starts the re-encoder from the seam record; a piece that ends
 // at a cut (seam_end) writes its pending bytes out at the end instead of a flush (the oracle's
 // avr_ce_seam_flush): the bytes of the arithmetic's low up to the next piece's first byte
+// SPL (compress): every OP_FINISH ends a piece's stream -- its length goes to piece_end[k] and a fresh
+// encoder starts the next piece's
 template <int MODE, bool P32, bool SEQ = false, bool SPL = false>
 AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d, uint8_t* out, uint32_t flags,
-                        const SeamRec* seam = nullptr, bool seam_end = false) {
+                        const SeamRec* seam = nullptr, bool seam_end = false, uint32_t* piece_end = nullptr) {
+  uint32_t pieces = 0;
   const bool billing = (flags & kFlagBill) != 0;
   uint32_t bill[6] = {0, 0, 0, 0, 0, 0};
   uint32_t bill_pend = 0;
@@ -2719,6 +2794,16 @@ AVR_FI void coder_slice(Shared* sh, const HotTables* T, const avr_slice_desc* d,
         const uint32_t op = __builtin_amdgcn_readlane(op_v, j);
         if (op & OP_END) { done = true; break; }
         re_finish(re, o);
+        if constexpr (SPL) {
+          if (piece_end && __lane_id() == 0) piece_end[pieces] = out_total(o);
+          pieces++;
+          re_init(re);
+#ifndef AVR_CODER_SALU
+          const uint32_t z = vgpr_zero();
+          re.range += z;
+          re.low += z;
+#endif
+        }
         ctrl &= ctrl - 1;
         j++;
       }
@@ -2977,16 +3062,19 @@ AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice
   w.sh = (Shared*)smem;
   w.ring = (typename Walker<MODE, false, FLD, P32, SPL>::ERec*)(smem + sizeof(Shared));
   bool seam_end = false;
+  uint32_t* piece_end = nullptr;
   if constexpr (SPL) {
     const PieceCtl c = sp->ctl[s];
     w.seam = c.seam >= 0 ? (const SeamRec*)(sp->recs + (size_t)c.seam * sp->rec_stride) : nullptr;
     w.piece_mbs = c.n_mbs;
     w.cut = 0;
     seam_end = c.n_mbs != 0;
+    piece_end = MODE == MODE_COMPRESS && c.snap >= 0 && sp->piece_end ? sp->piece_end + c.snap : nullptr;
     w.snap = MODE == MODE_COMPRESS && c.snap >= 0 ? sp->recs + (size_t)c.snap * sp->rec_stride : nullptr;
     w.snap_cap = c.snap_cap;
     w.snap_n = 0;
     w.snap_last = 0;
+    w.snap_q = 0;
     w.split_bits = sp->split_bits;
     w.rec_stride = sp->rec_stride;
     w.snap_count = sp->snap_n ? sp->snap_n + s : nullptr;
@@ -3034,8 +3122,8 @@ AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice
     walker_slice(w, d, in, &res[s]);
     AVR_PLACE_T(s, 1);
   }
-  else if (MODE == MODE_COMPRESS && wave == 1) model_slice(w.sh, w.est_g);
-  else if constexpr (SPL) coder_slice<MODE, P32, false, true>(w.sh, w.T, d, out, flags, w.seam, seam_end);
+  else if (MODE == MODE_COMPRESS && wave == 1) model_slice<SPL>(w.sh, w.est_g);
+  else if constexpr (SPL) coder_slice<MODE, P32, false, true>(w.sh, w.T, d, out, flags, w.seam, seam_end, piece_end);
   else coder_slice<MODE, P32>(w.sh, w.T, d, out, flags);
   if (MG) QTRACE(wave, qiter << 8 | 4);
   __syncthreads();
@@ -3046,10 +3134,10 @@ AVR_FI void parallel_slice(uint8_t* smem, const EngineTables* G, const avr_slice
 // The long-slice split's launches (avr_kernels.h SplitArgs): progressive frame slices and pieces of
 // the parallel model on arithmetic_code<uint64_t, uint8_t>, the model row in LDS; each workgroup
 // takes descriptors blockIdx.x, blockIdx.x + gridDim.x, ... (a grid of at most the resident slots:
-// one estimator scratch per workgroup).  Compress: a descriptor with PieceCtl::snap >= 0 is a whole
-// long slice whose cut records are taken (its own output is the unsplit stream); the other
-// descriptors are the pieces (seam >= 0: started from a record, n_mbs > 0: stopped at the next cut).
-// Decompress: the pieces, from records the host wrote (the container's seams).
+// one estimator scratch per workgroup).  MODE_TRACE: the cut scan -- the CABAC parse of whole long
+// slices (one wave, no model, no output) taking the cut records (PieceCtl::snap).  Compress: the
+// pieces (seam >= 0: started from a record, n_mbs > 0: stopped at the next cut).  Decompress: the
+// pieces, from records the host wrote (the container's seams).
 template <int MODE>
 __global__ __launch_bounds__(192, 4) void slices_split_kernel(const EngineTables* G, const avr_slice_desc* descs, int n,
                                                              const uint8_t* in, uint8_t* out, avr_slice_result* res,

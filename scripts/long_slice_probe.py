@@ -5,6 +5,7 @@ import json
 import os
 import sys
 import time
+from pathlib import Path
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import avrecode_amd as avr  # noqa: E402
@@ -15,7 +16,10 @@ def main():
     ctx = avr.Context(0)
     files = workloads.corpus(ctx)
     out = {"files": {}}
+    only = os.environ.get("PROBE_ONLY")
     for name, data in files:
+        if only and only not in name:
+            continue
         sizes = sorted(avr.slice_payload_sizes(data).tolist(), reverse=True)
         rec = {"bytes": len(data), "slices": len(sizes), "largest_payloads": sizes[:6]}
         c = ctx.compress(data, avr.MODEL_PARALLEL)
@@ -26,8 +30,17 @@ def main():
         t2 = time.perf_counter()
         assert d == data
         rec.update(compress_s=t1 - t0, decompress_s=t2 - t1, ratio=len(c) / len(data))
+        info, _ = avr.describe_container(c)
+        seams = [len(b["seams"]) // 2 for b in info["blocks"] if "seams" in b]
+        rec.update(split_blocks=len(seams), seams_bytes=sum(seams))
+        if seams and os.environ.get("PROBE_SAVE"):
+            Path(os.environ["PROBE_SAVE"]).mkdir(parents=True, exist_ok=True)
+            (Path(os.environ["PROBE_SAVE"]) / f"{name}.264").write_bytes(data)
         out["files"][name] = rec
         print(name, json.dumps(rec), file=sys.stderr, flush=True)
+    if only:
+        print(json.dumps(out))
+        return
     datas = [d for _, d in files]
     ctx.compress_files(datas, avr.MODEL_PARALLEL)
     t0 = time.perf_counter()
