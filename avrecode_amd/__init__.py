@@ -24,6 +24,7 @@ __all__ = [
     "SLICE_DESC",
     "SLICE_RESULT", "SynthParams", "lib", "parse_stream", "assemble_container", "neighbor_tables",
     "plan_decompress", "splice_container", "container_model", "source_sha", "library_path", "EXPORTED_SYMBOLS",
+    "seams_of_container",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -481,6 +482,48 @@ def assemble_container(data, status: np.ndarray, recoded, offsets: np.ndarray, l
     if r != AVR_OK:
         raise AvrError(r, "avr_assemble_container failed")
     return _take_array(res, olen.value) if as_array else _take(res, olen.value)
+
+
+def _varint(b, i: int) -> tuple[int, int]:
+    v = s = 0
+    while True:
+        c = b[i]
+        i += 1
+        v |= (c & 0x7F) << s
+        s += 7
+        if c < 0x80:
+            return v, i
+
+
+def seams_of_container(avrc) -> list:
+    """The parallel model's long-slice split in a container: (block index, seams field bytes) of every
+    coded block that was cut (Block field 16, include/avrecode.h avr_set_split_bytes).  A plain walk
+    of the wire format (host only, no library call)."""
+    b = memoryview(bytes(avrc))
+    out, i, k = [], 0, 0
+    while i < len(b):
+        tag, i = _varint(b, i)
+        wt = tag & 7
+        if wt == 0:
+            _, i = _varint(b, i)
+            continue
+        if wt != 2:
+            raise ValueError("not a Recoded message")
+        n, i = _varint(b, i)
+        if tag >> 3 == 2:   # a Block: look for field 16
+            j, e = i, i + n
+            while j < e:
+                t2, j = _varint(b, j)
+                if t2 & 7 == 0:
+                    _, j = _varint(b, j)
+                    continue
+                l2, j = _varint(b, j)
+                if t2 >> 3 == 16:
+                    out.append((k, l2))
+                j += l2
+            k += 1
+        i += n
+    return out
 
 
 def describe_container(avrc) -> tuple[dict, bytes]:

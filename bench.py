@@ -316,6 +316,22 @@ def corpus_section(ctx, args):
     rec["ratio_C_over_R"] = rec["C"]["avrc_bytes"] / rec["R"]["avrc_bytes"]
     rec["per_file_ratio"] = {n: {"R": sizes["R"][i] / len(d), "P": sizes["P"][i] / len(d), "C": sizes["C"][i] / len(d)}
                              for i, (n, d) in enumerate(files)}
+    # the parallel model's long-slice split (avr_set_split_bytes): what it cut, what it costs in bytes
+    # (the same corpus compressed without it), per file
+    p_outs = ctx.compress_files(datas, avr.MODEL_PARALLEL)
+    split0 = ctx.split_bytes
+    ctx.split_bytes = 0
+    try:
+        plain = ctx.compress_files(datas, avr.MODEL_PARALLEL)
+    finally:
+        ctx.split_bytes = split0
+    rec["P_split"] = {"split_bytes": split0, "files": {}}
+    for (n, d), o, q in zip(files, p_outs, plain):
+        cut = avr.seams_of_container(o)
+        if cut:
+            rec["P_split"]["files"][n] = {"split_blocks": len(cut), "seams_bytes": sum(x for _, x in cut),
+                                          "ratio": len(o) / len(d), "ratio_unsplit": len(q) / len(d)}
+    rec["P_split"]["ratio_unsplit"] = sum(map(len, plain)) / total
     if not args.no_cpu_baseline:
         tot = 0.0
         for n, d in files:
