@@ -661,13 +661,37 @@ uint32_t get_le32(const uint8_t* p) {
   return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
 }
 
-// Block field 16: u32 raw length, then zlib (level 9) of { u32 1, u32 cuts, u32 mb_width,
+// The slice's initial context states (9.3.1.1), as init_slice_state sets them on the device.
+void cabac_init_states(const avr_slice_desc& d, uint8_t out[1024]) {
+  const int qp = d.slice_qp < 0 ? 0 : d.slice_qp > 51 ? 51 : d.slice_qp;
+  for (int c = 0; c < 1024; c++) {
+    int m, n;
+    avr::mn_for_ctx(d.slice_type == 2 ? -1 : d.cabac_init_idc, c, &m, &n);
+    int pre = ((m * qp) >> 4) + n;
+    pre = pre < 1 ? 1 : pre > 126 ? 126 : pre;
+    out[c] = pre <= 63 ? (uint8_t)((63 - pre) << 1) : (uint8_t)(((pre - 64) << 1) | 1);
+  }
+}
+// an upper-row edge byte as the seams field keeps it: what the parse of the row below reads of it --
+// nnz only as nonzero (coded_block_flag's context), |mvd| only up to 33 (absMvdComp's sum against
+// 3 and 32)
+uint8_t edge_norm(int j, uint8_t b) {
+  if (j >= 4 && j < 16) return b != 0;
+  if (j >= 16 && j < 32) return b > 33 ? 33 : b;
+  return b;
+}
+
+// Block field 16: u32 raw length, then zlib (level 9) of { u32 2, u32 cuts, u32 mb_width,
 // u32 piece_len[cuts + 1], per cut { u32 first_mb, q, last_dqp_nz, ce_low, ce_queue,
-// ce_outstanding, ce_cache, ce_range, u8 state[1024], u8 edges[40 mb_width] } } (little-endian)
-bool seams_encode(const std::vector<const avr::SeamRec*>& recs, const std::vector<SeamCe>& ce, int mb_width,
+// ce_outstanding, ce_cache, ce_range, u8 state[1024] XOR the slice's initial states, u8 edges
+// byte-major (byte j of every column, j = 0..39; edge_norm) } } (little-endian)
+bool seams_encode(const std::vector<const avr::SeamRec*>& recs, const std::vector<SeamCe>& ce, const avr_slice_desc& d,
                   const std::vector<uint32_t>& piece_len, std::vector<uint8_t>* out) {
+  const int mb_width = d.mb_width;
+  uint8_t init[1024];
+  cabac_init_states(d, init);
   std::vector<uint8_t> raw;
-  put_le32(&raw, 1);
+  put_le32(&raw, 2);
   put_le32(&raw, (uint32_t)recs.size());
   put_le32(&raw, (uint32_t)mb_width);
   for (uint32_t l : piece_len) put_le32(&raw, l);
@@ -680,9 +704,10 @@ bool seams_encode(const std::vector<const avr::SeamRec*>& recs, const std::vecto
     put_le32(&raw, ce[i].outstanding);
     put_le32(&raw, ce[i].cache);
     put_le32(&raw, ce[i].range);
-    raw.insert(raw.end(), recs[i]->state, recs[i]->state + 1024);
+    for (int c = 0; c < 1024; c++) raw.push_back((uint8_t)(recs[i]->state[c] ^ init[c]));
     const uint8_t* e = (const uint8_t*)(recs[i] + 1);
-    raw.insert(raw.end(), e, e + (size_t)avr::kEdgeBytes * mb_width);
+    for (int j = 0; j < avr::kEdgeBytes; j++)
+      for (int c = 0; c < mb_width; c++) raw.push_back(edge_norm(j, e[(size_t)avr::kEdgeBytes * c + j]));
   }
   uLongf zl = compressBound(raw.size());
   out->assign(4 + zl, 0);
@@ -698,13 +723,16 @@ struct SeamsDecoded {
   std::vector<uint32_t> piece_len, first_mb, q;
   std::vector<uint8_t> recs;   // cuts records of rec_stride bytes
 };
-bool seams_decode(const uint8_t* p, size_t n, int mb_width, size_t rec_stride, SeamsDecoded* sd) {
+bool seams_decode(const uint8_t* p, size_t n, const avr_slice_desc& d, size_t rec_stride, SeamsDecoded* sd) {
+  const int mb_width = d.mb_width;
+  uint8_t init[1024];
+  cabac_init_states(d, init);
   if (n < 4) return false;
   const uint32_t rl = get_le32(p);
   if (rl < 12 || rl > (1u << 30)) return false;
   std::vector<uint8_t> raw(rl);
   uLongf got = rl;
-  if (uncompress(raw.data(), &got, p + 4, n - 4) != Z_OK || got != rl || get_le32(raw.data()) != 1) return false;
+  if (uncompress(raw.data(), &got, p + 4, n - 4) != Z_OK || got != rl || get_le32(raw.data()) != 2) return false;
   const uint32_t k = get_le32(raw.data() + 4), w = get_le32(raw.data() + 8);
   const size_t per = 32 + 1024 + (size_t)avr::kEdgeBytes * w;
   if ((int)w != mb_width || k == 0 || k > 65536 || 12 + 4 * ((size_t)k + 1) + per * k != rl) return false;
@@ -729,8 +757,10 @@ bool seams_decode(const uint8_t* p, size_t n, int mb_width, size_t rec_stride, S
         r->ce_low >= (1u << (r->ce_queue + 18)) || (i && sd->q[i] <= sd->q[i - 1]) ||
         (i && sd->first_mb[i] <= sd->first_mb[i - 1]) || sd->first_mb[i] % w)
       return false;
-    memcpy(r->state, q + 32, 1024);
-    memcpy(r + 1, q + 32 + 1024, (size_t)avr::kEdgeBytes * w);
+    for (int c = 0; c < 1024; c++) r->state[c] = (uint8_t)(q[32 + c] ^ init[c]);
+    uint8_t* e = (uint8_t*)(r + 1);
+    for (int j = 0; j < avr::kEdgeBytes; j++)
+      for (uint32_t c = 0; c < w; c++) e[(size_t)avr::kEdgeBytes * c + j] = q[32 + 1024 + (size_t)j * w + c];
   }
   return true;
 }
@@ -1017,7 +1047,7 @@ int split_finish(avr_ctx* c, SplitJob* j, bool verify, std::vector<SplitOut>* ou
   for (int k = 0; k < n; k++) {
     SplitOut& so = (*out)[k];
     if (so.status || cuts[k].empty()) continue;
-    if (!seams_encode(cuts[k], ces[k], j->d[k].mb_width, plen[k], &so.seams)) return fail(c, AVR_ERR_DEVICE, "zlib failed");
+    if (!seams_encode(cuts[k], ces[k], j->d[k], plen[k], &so.seams)) return fail(c, AVR_ERR_DEVICE, "zlib failed");
   }
   return AVR_OK;
 }
@@ -1726,7 +1756,7 @@ int decompress_setup(avr_ctx* c, const uint8_t* in, size_t n, DecJob* j, Plan* p
       if (j->model != AVR_MODEL_PARALLEL || d.structure != AVR_STRUCT_FRAME || d.mb_width > SplitPlan::kMringCols)
         return fail(c, AVR_ERR_FORMAT, "seams on a block that cannot be split");
       SeamsDecoded sd;
-      if (!seams_decode(b.seams, b.seams_len, d.mb_width, sp->stride, &sd))
+      if (!seams_decode(b.seams, b.seams_len, d, sp->stride, &sd))
         return fail(c, AVR_ERR_FORMAT, "Invalid seams field in coded block.");
       uint64_t tot = 0;
       for (uint32_t l : sd.piece_len) tot += l;

@@ -333,12 +333,15 @@ void avr_oracle_set_split_bytes(size_t bytes);
  * cannot be placed there (the arithmetic's pending digits reach too far back). */
 int avr_seam_encoder(const uint8_t *payload, size_t n, size_t bitpos, uint32_t offset, uint32_t range,
                      avr_seam_t *s);
-/* the seams blob: zlib of { u32 1, u32 seams, u32 mb_width, u32 piece_len[seams + 1], per seam
- * { u32 first_mb, q, last_dqp_nz, ce_low, ce_queue, ce_outstanding, ce_cache, ce_range,
- * u8 state[1024], u8 edge[40 * mb_width] } }, little-endian */
-int avr_seams_encode(const avr_seam_t *s, int n_seams, int mb_width, const uint32_t *piece_len, obuf_t *out);
+/* the seams blob: u32 raw length, then zlib (level 9) of { u32 2, u32 seams, u32 mb_width,
+ * u32 piece_len[seams + 1], per seam { u32 first_mb, q, last_dqp_nz, ce_low, ce_queue, ce_outstanding,
+ * ce_cache, ce_range, u8 state[1024] XOR the slice's initial context states (9.3.1.1), u8 edges
+ * byte-major (byte j of every column, j = 0..39), nnz as nonzero and |mvd| up to 33 } }, little-endian */
+int avr_seams_encode(const avr_seam_t *s, int n_seams, int mb_width, const uint32_t *piece_len,
+                     const uint8_t init_state[1024], obuf_t *out);
 /* parses a seams blob: 0 and *s (malloc'd, n_seams entries), *piece_len (malloc'd, n_seams + 1); -1 */
-int avr_seams_decode(const uint8_t *p, size_t n, int mb_width, avr_seam_t **s, int *n_seams, uint32_t **piece_len);
+int avr_seams_decode(const uint8_t *p, size_t n, int mb_width, const uint8_t init_state[1024], avr_seam_t **s,
+                     int *n_seams, uint32_t **piece_len);
 void avr_seams_free(avr_seam_t *s, int n_seams);
 /* the device's CABAC re-encoder in byte form (avr_engine.h CabacEncoder), which a piece starts from a
  * seam's state (s == NULL: a slice start) and ends with avr_ce_seam_flush */

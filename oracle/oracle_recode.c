@@ -615,7 +615,9 @@ static int compress_slice_split(avr_model_t *m, const slice_t *s, obuf_t *recode
     uint32_t prev = 0;
     for (int i = 0; i < c.n_seams; i++) { pl[i] = c.piece_end[i] - prev; prev = c.piece_end[i]; }
     pl[c.n_seams] = (uint32_t)c.enc_out.len - prev;
-    if (avr_seams_encode(c.seams, c.n_seams, s->h.mb_width, pl, seams)) ret = -24;
+    uint8_t init[1024];
+    avr_cabac_init_states(init, s->h.slice_type == AVR_SLICE_I ? -1 : s->h.cabac_init_idc, s->h.slice_qp);
+    if (avr_seams_encode(c.seams, c.n_seams, s->h.mb_width, pl, init, seams)) ret = -24;
     free(pl);
   }
   avr_seams_free(c.seams, c.n_seams);
@@ -970,8 +972,10 @@ int avr_decompress(const uint8_t *in, size_t n, uint8_t **out, size_t *out_len) 
       uint32_t *piece_len = NULL;
       int n_seams = 0;
       int r = 0;
+      uint8_t init[1024];
+      avr_cabac_init_states(init, s.h.slice_type == AVR_SLICE_I ? -1 : s.h.cabac_init_idc, s.h.slice_qp);
       if (b->has_seams && (mode != AVR_MODE_P ||
-                           avr_seams_decode(b->seams, b->seams_len, s.h.mb_width, &seams, &n_seams, &piece_len)))
+                           avr_seams_decode(b->seams, b->seams_len, s.h.mb_width, init, &seams, &n_seams, &piece_len)))
         r = -27;
       if (r == 0)
         r = decompress_slice_pieces(m, &s.h, s.picture_id, b->cabac, b->cabac_len, &cab, seams, n_seams, piece_len);
@@ -1045,7 +1049,9 @@ int avr_check_pieces(const uint8_t *file, size_t n, size_t split_bytes, int *n_s
       avr_seam_t *seams = NULL;
       uint32_t *pl = NULL;
       int k = 0;
-      if (r == 0 && sb.len && avr_seams_decode(sb.data, sb.len, s.h.mb_width, &seams, &k, &pl) == 0) {
+      uint8_t init[1024];
+      avr_cabac_init_states(init, s.h.slice_type == AVR_SLICE_I ? -1 : s.h.cabac_init_idc, s.h.slice_qp);
+      if (r == 0 && sb.len && avr_seams_decode(sb.data, sb.len, s.h.mb_width, init, &seams, &k, &pl) == 0) {
         (*n_split)++;
         *n_pieces += k + 1;
         obuf_t all;

@@ -66,10 +66,19 @@ static uint32_t get32(const uint8_t *p) {
   return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
 }
 
-int avr_seams_encode(const avr_seam_t *s, int n_seams, int mb_width, const uint32_t *piece_len, obuf_t *out) {
+/* an edge byte as the seams field keeps it: what the parse of the row below reads of it -- nnz only
+ * as nonzero (coded_block_flag's context), |mvd| only up to 33 (absMvdComp's sum against 3 and 32) */
+static uint8_t edge_norm(int j, uint8_t b) {
+  if (j >= 4 && j < 16) return b != 0;
+  if (j >= 16 && j < 32) return b > 33 ? 33 : b;
+  return b;
+}
+
+int avr_seams_encode(const avr_seam_t *s, int n_seams, int mb_width, const uint32_t *piece_len,
+                     const uint8_t init_state[1024], obuf_t *out) {
   obuf_t raw;
   ob_init(&raw);
-  put32(&raw, 1);
+  put32(&raw, 2);
   put32(&raw, (uint32_t)n_seams);
   put32(&raw, (uint32_t)mb_width);
   for (int i = 0; i <= n_seams; i++) put32(&raw, piece_len[i]);
@@ -83,8 +92,9 @@ int avr_seams_encode(const avr_seam_t *s, int n_seams, int mb_width, const uint3
     put32(&raw, t->ce_outstanding);
     put32(&raw, t->ce_cache);
     put32(&raw, t->ce_range);
-    ob_append(&raw, t->state, 1024);
-    ob_append(&raw, t->edge, (size_t)AVR_EDGE_BYTES * mb_width);
+    for (int c = 0; c < 1024; c++) ob_put(&raw, (uint8_t)(t->state[c] ^ init_state[c]));
+    for (int j = 0; j < AVR_EDGE_BYTES; j++)
+      for (int c = 0; c < mb_width; c++) ob_put(&raw, edge_norm(j, t->edge[(size_t)AVR_EDGE_BYTES * c + j]));
   }
   uLongf zl = compressBound(raw.len);
   uint8_t *z = (uint8_t *)malloc(zl);
@@ -104,7 +114,8 @@ void avr_seams_free(avr_seam_t *s, int n_seams) {
   free(s);
 }
 
-int avr_seams_decode(const uint8_t *p, size_t n, int mb_width, avr_seam_t **out, int *n_seams, uint32_t **piece_len) {
+int avr_seams_decode(const uint8_t *p, size_t n, int mb_width, const uint8_t init_state[1024], avr_seam_t **out,
+                     int *n_seams, uint32_t **piece_len) {
   *out = NULL;
   *piece_len = NULL;
   *n_seams = 0;
@@ -113,7 +124,7 @@ int avr_seams_decode(const uint8_t *p, size_t n, int mb_width, avr_seam_t **out,
   if (rl < 12 || rl > (1u << 30)) return -1;
   uint8_t *raw = (uint8_t *)malloc(rl);
   uLongf got = rl;
-  if (uncompress(raw, &got, p + 4, n - 4) != Z_OK || got != rl || get32(raw) != 1) { free(raw); return -1; }
+  if (uncompress(raw, &got, p + 4, n - 4) != Z_OK || got != rl || get32(raw) != 2) { free(raw); return -1; }
   const uint32_t k = get32(raw + 4), w = get32(raw + 8);
   const size_t per = 32 + 1024 + (size_t)AVR_EDGE_BYTES * w;
   if ((int)w != mb_width || k == 0 || k > 65536 || 12 + 4 * ((size_t)k + 1) + per * k != rl) { free(raw); return -1; }
@@ -131,9 +142,10 @@ int avr_seams_decode(const uint8_t *p, size_t n, int mb_width, avr_seam_t **out,
     t->ce_outstanding = get32(q + 20);
     t->ce_cache = get32(q + 24);
     t->ce_range = get32(q + 28);
-    memcpy(t->state, q + 32, 1024);
+    for (int c = 0; c < 1024; c++) t->state[c] = (uint8_t)(q[32 + c] ^ init_state[c]);
     t->edge = (uint8_t *)malloc((size_t)AVR_EDGE_BYTES * w);
-    memcpy(t->edge, q + 32 + 1024, (size_t)AVR_EDGE_BYTES * w);
+    for (int j = 0; j < AVR_EDGE_BYTES; j++)
+      for (uint32_t c = 0; c < w; c++) t->edge[(size_t)AVR_EDGE_BYTES * c + j] = q[32 + 1024 + (size_t)j * w + c];
     q += per;
   }
   free(raw);

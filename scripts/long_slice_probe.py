@@ -46,8 +46,16 @@ def main():
     t0 = time.perf_counter()
     cs = ctx.compress_files(datas, avr.MODEL_PARALLEL)
     t1 = time.perf_counter()
+    pc = ctx.last_phase_times()
     ds = ctx.decompress_files(cs)
     t2 = time.perf_counter()
+    pd = ctx.last_phase_times()
+    out["batch_phases"] = {"compress": pc, "decompress": pd}
+    rt, tm = ctx.roundtrip_files(datas, avr.MODEL_PARALLEL)
+    t3 = time.perf_counter()
+    rt, tm = ctx.roundtrip_files(datas, avr.MODEL_PARALLEL)
+    t4 = time.perf_counter()
+    out["roundtrip_files"] = {"wall_s": t4 - t3, "MB_s": sum(map(len, datas)) / (t4 - t3) / 1e6, **tm}
     assert all(a == b for a, b in zip(ds, datas))
     out["batch"] = {"compress_s": t1 - t0, "decompress_s": t2 - t1,
                     "MB_s": sum(map(len, datas)) / (t2 - t0) / 1e6}

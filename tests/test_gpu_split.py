@@ -80,3 +80,32 @@ def test_4k_444_intra_slice_is_split(ctx):
         g.write_bytes(avrc)
         assert oracle_cli("decompress", g) == data
 
+
+
+def test_synthetic_corpus_split_matches_oracle(ctx):
+    """Cuts in every slice kind the generator makes: P and B slices (mvd, ref_idx and direct flags in
+    the upper-row edges), 4:2:0 / 4:2:2 / 4:4:4 / monochrome, 8x8 transforms, several slices per
+    picture (slices that start mid-row: the edges of the columns before the start are empty), and
+    field / MBAFF streams, which are never cut."""
+    specs = [(22, 18, 2, 6, 6, 1, 25, 1, 0), (14, 9, 3, 5, 5, 0, 27, 3, 0), (30, 17, 1, 4, 2, 2, 29, 2, 0),
+             (11, 7, 1, 7, 4, 1, 23, 0, 0), (40, 23, 3, 4, 4, 1, 24, 1, 0), (20, 12, 1, 4, 4, 0, 26, 1, 1),
+             (20, 12, 1, 4, 4, 1, 26, 1, 2)]
+    ctx.split_bytes = 700
+    try:
+        with tempfile.TemporaryDirectory() as td:
+            datas = []
+            for k, (w, h, spf, frames, gop, st, qp, cf, structure) in enumerate(specs):
+                p = avr.SynthParams(mb_width=w, mb_height=h, slice_type=st, slice_qp=qp, chroma_format_idc=cf,
+                                    seed=900 + k, slices_per_picture=spf, gop_length=gop, num_ref_idx_l0=2,
+                                    structure=structure)
+                data = ctx.synthesize(p, frames)
+                datas.append(data)
+                f = Path(td) / f"s{k}.264"
+                f.write_bytes(data)
+                avrc = ctx.compress(data, avr.MODEL_PARALLEL)
+                assert avrc == oracle_cli("compress", f, mode="P", split_bytes=700), k
+                assert bool(avr.seams_of_container(avrc)) == (structure == 0), k
+            outs = ctx.compress_files(datas, avr.MODEL_PARALLEL)
+            assert ctx.decompress_files(outs) == datas
+    finally:
+        ctx.split_bytes = 131072
