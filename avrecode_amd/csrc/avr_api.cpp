@@ -621,7 +621,7 @@ constexpr size_t kSplitBytesDefault = 131072;
 
 bool split_candidate(const avr_slice_desc& d, size_t split_bytes) {
   return split_bytes && split_bytes < ((size_t)1 << 28) && d.structure == AVR_STRUCT_FRAME &&
-         2 * (uint64_t)d.payload_size >= 3 * (uint64_t)split_bytes;
+         d.mb_width <= avr::kMringCols && 2 * (uint64_t)d.payload_size >= 3 * (uint64_t)split_bytes;
 }
 
 struct SeamCe {

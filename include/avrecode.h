@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define AVRECODE_ABI_VERSION 5  /* 5: avr_slice_desc.file_offset (96 B), dec-plan handle, ranged parse */
+#define AVRECODE_ABI_VERSION 6  /* 6: the parallel model's long-slice split (avr_set_split_bytes, Block field 16);
+                                 * 5: avr_slice_desc.file_offset (96 B), dec-plan handle, ranged parse */
 
 typedef enum {
   AVR_OK = 0,

@@ -84,11 +84,11 @@ def test_4k_444_intra_slice_is_split(ctx):
 
 def test_synthetic_corpus_split_matches_oracle(ctx):
     """Cuts in every slice kind the generator makes: P and B slices (mvd, ref_idx and direct flags in
-    the upper-row edges), 4:2:0 / 4:2:2 / 4:4:4 / monochrome, 8x8 transforms, several slices per
+    the upper-row edges), 4:2:0 / 4:2:2 / 4:4:4, 8x8 transforms, several slices per
     picture (slices that start mid-row: the edges of the columns before the start are empty), and
     field / MBAFF streams, which are never cut."""
     specs = [(22, 18, 2, 6, 6, 1, 25, 1, 0), (14, 9, 3, 5, 5, 0, 27, 3, 0), (30, 17, 1, 4, 2, 2, 29, 2, 0),
-             (11, 7, 1, 7, 4, 1, 23, 0, 0), (40, 23, 3, 4, 4, 1, 24, 1, 0), (20, 12, 1, 4, 4, 0, 26, 1, 1),
+             (11, 7, 1, 7, 4, 1, 23, 1, 0), (40, 23, 3, 4, 4, 1, 24, 1, 0), (20, 12, 1, 4, 4, 0, 26, 1, 1),
              (20, 12, 1, 4, 4, 1, 26, 1, 2)]
     ctx.split_bytes = 700
     try:
