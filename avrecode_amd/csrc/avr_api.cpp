@@ -753,9 +753,11 @@ bool seams_decode(const uint8_t* p, size_t n, const avr_slice_desc& d, size_t re
     r->ce_outstanding = get_le32(q + 20);
     r->ce_cache = get_le32(q + 24);
     r->ce_range = get_le32(q + 28);
+    // a cut's state is what seam_encoder can produce: the window 12 bytes deep at most
     if (r->ce_queue < -8 || r->ce_queue > -1 || r->ce_cache > 0xff || r->ce_range < 256 || r->ce_range > 510 ||
-        r->ce_low >= (1u << (r->ce_queue + 18)) || (i && sd->q[i] <= sd->q[i - 1]) ||
-        (i && sd->first_mb[i] <= sd->first_mb[i - 1]) || sd->first_mb[i] % w)
+        r->ce_low >= (1u << (r->ce_queue + 18)) || r->ce_outstanding > 12 || (i && sd->q[i] <= sd->q[i - 1]) ||
+        (i && sd->first_mb[i] <= sd->first_mb[i - 1]) || sd->first_mb[i] % w ||
+        sd->first_mb[i] >= (uint32_t)w * (uint32_t)std::max(1, d.mb_height))
       return false;
     for (int c = 0; c < 1024; c++) r->state[c] = (uint8_t)(q[32 + c] ^ init[c]);
     uint8_t* e = (uint8_t*)(r + 1);
