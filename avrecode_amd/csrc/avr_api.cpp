@@ -3631,13 +3631,20 @@ int avr_hooks_decompress_begin(avr_ctx* c, const uint8_t* avrc, size_t n, avr_ho
     // the container's model from its Metadata.version alone (no block list), inside guarded(): no
     // exception crosses the C ABI
     int m = 0;
+    bool split = false;   // a long-slice split container: regenerated whole at begin (its pieces are
+                          // a whole-file launch), as a reference-model one is
     if (int r = guarded(c, [&]() -> int {
           std::string version;
           m = avr::pb_read_version(avrc, n, &version) ? avr::model_of_version(version) : 0;
+          if (m == AVR_MODEL_PARALLEL) {
+            std::vector<avr::PbBlock> blocks;
+            if (avr::pb_parse(avrc, n, &blocks, &version))
+              for (const auto& b : blocks) split = split || b.has_seams;
+          }
           return AVR_OK;
         }))
       return r;
-    if (parallel_model(m) && !getenv("AVR_HOOKS_EAGER")) {
+    if (parallel_model(m) && !split && !getenv("AVR_HOOKS_EAGER")) {
       // the parallel model's slices are independent: plan the container now, regenerate on demand
       if (int r = guarded(c, [&]() -> int {
             hs->lazy = true;

@@ -109,3 +109,19 @@ def test_synthetic_corpus_split_matches_oracle(ctx):
             assert ctx.decompress_files(outs) == datas
     finally:
         ctx.split_bytes = 131072
+
+
+def test_hooks_decompress_reads_a_split_container(ctx):
+    """The libavcodec-hooks decompress session over a split container: the callbacks of every
+    slice are served (the driver's parse walks them all) and avr_hooks_end returns the file."""
+    from test_hooks import _call
+    data = (FIX / "cockatoo.mp4").read_bytes()
+    ctx.split_bytes = 1024
+    try:
+        avrc = ctx.compress(data, avr.MODEL_PARALLEL)
+    finally:
+        ctx.split_bytes = 131072
+    assert avr.seams_of_container(avrc)
+    r, back, walked = _call("hooks_decompress", avrc, len(avrc))
+    assert r == 0, r
+    assert back == data and walked > 0
