@@ -125,3 +125,22 @@ def test_hooks_decompress_reads_a_split_container(ctx):
     r, back, walked = _call("hooks_decompress", avrc, len(avrc))
     assert r == 0, r
     assert back == data and walked > 0
+
+
+def test_damaged_seams_are_refused(ctx):
+    """A seams field that does not parse or describes impossible cuts fails the file with
+    AVR_ERR_FORMAT (-3) instead of launching pieces from it; a damaged piece stream fails too."""
+    data = (FIX / "realshort.mp4").read_bytes()
+    ctx.split_bytes = 1024
+    try:
+        avrc = ctx.compress(data, avr.MODEL_PARALLEL)
+    finally:
+        ctx.split_bytes = 131072
+    info, _ = avr.describe_container(avrc)
+    blob = bytes.fromhex(next(b["seams"] for b in info["blocks"] if "seams" in b))
+    i = avrc.index(blob)
+    bad = bytearray(avrc)
+    bad[i + len(blob) // 2] ^= 0x55          # inside the zlib stream
+    back = ctx.decompress_files([bytes(bad), avrc])
+    assert isinstance(back[0], avr.AvrError) and back[0].code == -3
+    assert back[1] == data                   # the batch's other file is unaffected
