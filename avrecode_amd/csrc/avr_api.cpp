@@ -85,6 +85,15 @@ struct avr_ctx {
   hipStream_t split_stream = nullptr;
   DevBuf sp_in, sp_out, sp_descs, sp_res, sp_ctl, sp_recs, sp_snapn, sp_est, sp_in2, sp_out2;
   size_t split_bytes = 0;   // avr_set_split_bytes / AVR_SPLIT_BYTES (0: no split)
+  // a batch holding both progressive and field slices runs its field kernel beside the progressive
+  // one (avr::FieldLane); AVR_FIELD_LANE=0 keeps the two in one stream, one after the other
+  hipStream_t fld_stream = nullptr;
+  hipEvent_t fld_ev[2] = {nullptr, nullptr};
+  avr::FieldLane field_lane() const {
+    avr::FieldLane l;
+    if (fld_stream) l.stream = fld_stream, l.fork = fld_ev[0], l.join = fld_ev[1];
+    return l;
+  }
   bool round_robin = false;   // placement probe passed: the CU schedule (order) may be used
   int* order_or_null() { return round_robin ? order.as<int>() : nullptr; }
   // phase breakdown of the current / last whole-file call (avr_phase_times): run_plan adds the
@@ -97,6 +106,9 @@ struct avr_ctx {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     if (split_stream) (void)hipStreamDestroy(split_stream);
+    for (auto& e : fld_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (fld_stream) (void)hipStreamDestroy(fld_stream);
   }
 };
 
@@ -305,6 +317,12 @@ struct Plan {
       if (d.structure != AVR_STRUCT_FRAME) return true;
     return false;
   }
+  // both kinds of slice: the field kernel has work beside the progressive one (avr::FieldLane)
+  bool mixed() const {
+    bool f = false, p = false;
+    for (const auto& d : descs) (d.structure != AVR_STRUCT_FRAME ? f : p) = true;
+    return f && p;
+  }
 };
 
 template <class V>
@@ -488,8 +506,8 @@ int run_rmode_compress(avr_ctx* c, Plan& plan, uint64_t out_total, uint32_t flag
 
 // Device scratch of a parallel launch of n slices: the estimator tables (one per slice of a resident
 // batch, one per workgroup of a persistent one: avr::est_slots), the CU schedule and the slice queue.
-hipError_t reserve_parallel(avr_ctx* c, int n, int max_w) {
-  const int slots = std::max(1, avr::est_slots(n, max_w));
+hipError_t reserve_parallel(avr_ctx* c, int n, int max_w, bool field_lane = false) {
+  const int slots = std::max(1, avr::est_slots(n, max_w, field_lane));
   hipError_t e = c->est.reserve(sizeof(uint16_t) * (size_t)avr::kEstGlobal * slots, true);
   if (e == hipSuccess) e = c->order.reserve(sizeof(int) * (size_t)std::max(1, n));
   if (e == hipSuccess) e = c->queue.reserve(std::max<size_t>(256, avr::queue_scratch_bytes(n)));
@@ -508,6 +526,8 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
              HostBuf* out_host, bool verify = false, uint32_t flags = 0) {
   const int n = (int)plan.descs.size();
   if (plan.fields()) flags |= avr::kFlagFields;
+  // a parallel batch of progressive and field slices: the two kernels side by side
+  const avr::FieldLane lane = !sequential && plan.mixed() ? c->field_lane() : avr::FieldLane();
   res->assign(n, avr_slice_result{0, 0, 0, 0, {0, 0, 0, 0, 0, 0}});
   uint64_t out_total = 0;
   for (auto& d : plan.descs) {
@@ -557,11 +577,11 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
                                   c->est.as<uint16_t>(), c->frames.as<uint8_t>(), c->frame_meta.as<int>(), nullptr,
                                   c->stream, sf, flags));
   } else {
-    HIP_TRY(c, reserve_parallel(c, n, plan.max_w));
+    HIP_TRY(c, reserve_parallel(c, n, plan.max_w, lane.stream != nullptr));
     HIP_TRY(c, avr::launch_slices(mode, false, c->tables.as<avr::EngineTables>(), c->descs.as<avr_slice_desc>(), n,
                                   plan.max_w, c->in.as<uint8_t>(), c->out.as<uint8_t>(), c->res.as<avr_slice_result>(),
                                   c->est.as<uint16_t>(), nullptr, nullptr, c->order_or_null(), c->stream,
-                                  avr::SeqFiles(), flags, c->queue.p));
+                                  avr::SeqFiles(), flags, c->queue.p, &lane));
   }
   std::vector<int32_t> verdict;
   if (verify && mode == 0 && !sequential) {
@@ -576,7 +596,8 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
     HIP_TRY(c, avr::launch_slices(1, false, c->tables.as<avr::EngineTables>(), dd, n, plan.max_w, c->out.as<uint8_t>(),
                                   c->regen.as<uint8_t>(), rd, c->est.as<uint16_t>(), nullptr, nullptr,
                                   c->order_or_null(), c->stream, avr::SeqFiles(),
-                                  (plan.fields() ? avr::kFlagFields : 0u) | (flags & avr::kFlagP32), c->queue.p));
+                                  (plan.fields() ? avr::kFlagFields : 0u) | (flags & avr::kFlagP32), c->queue.p,
+                                  &lane));
     HIP_TRY(c, avr::launch_verify(c->descs.as<avr_slice_desc>(), c->res.as<avr_slice_result>(), rd, n,
                                   c->in.as<uint8_t>(), c->regen.as<uint8_t>(), c->verdict.as<int32_t>(), c->stream));
     verdict.resize(n);
@@ -2247,6 +2268,11 @@ int avr_create(int device, avr_ctx** out) {
   {
     const char* e = getenv("AVR_SPLIT_BYTES");
     c->split_bytes = e ? (size_t)strtoull(e, nullptr, 10) : kSplitBytesDefault;
+  }
+  if (const char* e = getenv("AVR_FIELD_LANE"); !e || strcmp(e, "0") != 0) {
+    if (hipStreamCreateWithFlags(&c->fld_stream, hipStreamNonBlocking) != hipSuccess) return AVR_ERR_DEVICE;
+    for (auto& ev : c->fld_ev)
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return AVR_ERR_DEVICE;
   }
   avr::EngineTables t;
   build_tables(&t);

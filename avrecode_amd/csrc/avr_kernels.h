@@ -56,6 +56,16 @@ struct SeqFiles {
   int n_files = 1;
   uint64_t frame_stride = 0;
 };
+// The field-capable kernel of a parallel launch beside the progressive one instead of after it (a
+// batch holding both, e.g. a corpus with interlaced files): launch_parallel records `fork` on the
+// launch's stream once the shared setup (queue, CU board) is queued, runs the field kernel on
+// `stream` after it, and makes the launch's stream wait for `join` recorded there.  The persistent
+// field kernel then takes the estimator scratches after the progressive kernel's (est_slots with
+// fields).  Null stream: the field kernel follows the progressive one on the launch's stream.
+struct FieldLane {
+  hipStream_t stream = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
 // ------------------------------------------------------------------ the long-slice split
 // The parallel model may cut a long progressive slice at macroblock-row starts into pieces re-coded
 // with fresh models (the oracle's restatement in oracle/oracle_seams.c), so its
@@ -102,37 +112,39 @@ hipError_t launch_split(int mode, const EngineTables* T, const avr_slice_desc* d
 hipError_t launch_slices(int mode, bool sequential, const EngineTables* T, const avr_slice_desc* descs, int n,
                          int max_mb_width, const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                          uint8_t* frames, int* frame_meta, int* order, hipStream_t stream,
-                         const SeqFiles& files = SeqFiles(), uint32_t flags = 0, void* qscratch = nullptr);
+                         const SeqFiles& files = SeqFiles(), uint32_t flags = 0, void* qscratch = nullptr,
+                         const FieldLane* lane = nullptr);
 // Parallel compress / decompress batches larger than the chip holds at once (more than
 // resident_slices) run as one persistent launch over a largest-first queue when launch_slices gets
 // a queue scratch of queue_scratch_bytes(n) (device); est then needs est_slots(n, max_mb_width)
-// estimator scratches of kEstGlobal u16 (one per resident workgroup), else n.
+// estimator scratches of kEstGlobal u16 (one per resident workgroup), else n; with a FieldLane,
+// est_slots(n, max_mb_width, true) (the field kernel's workgroups too).
 size_t queue_scratch_bytes(int n);
 int slots_per_cu(size_t lds);
 int resident_slices(size_t lds);
-int est_slots(int n, int max_mb_width);
+int est_slots(int n, int max_mb_width, bool field_lane = false);
 int parallel_kernel_kind(int mode, int n, int max_mb_width);
 // one per kernel translation unit (avr_k_*.hip); lds = shared_bytes(max_mb_width)
 hipError_t launch_parallel_compress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                     const int* order, uint32_t flags, hipStream_t stream,
                                     uint32_t* qhead = nullptr, int qgrid = 0, int qgrid_fld = 0,
-                                    size_t lds_fld = 0);
+                                    size_t lds_fld = 0, const FieldLane* lane = nullptr);
 hipError_t launch_parallel_decompress(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                       const int* order, uint32_t flags, hipStream_t stream,
                                     uint32_t* qhead = nullptr, int qgrid = 0, int qgrid_fld = 0,
-                                    size_t lds_fld = 0);
+                                    size_t lds_fld = 0, const FieldLane* lane = nullptr);
 hipError_t launch_parallel_compress32(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                       const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                       const int* order, uint32_t flags, hipStream_t stream,
                                     uint32_t* qhead = nullptr, int qgrid = 0, int qgrid_fld = 0,
-                                    size_t lds_fld = 0);
+                                    size_t lds_fld = 0, const FieldLane* lane = nullptr);
 hipError_t launch_parallel_decompress32(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                         const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                         const int* order, uint32_t flags, hipStream_t stream,
                                     uint32_t* qhead = nullptr, int qgrid = 0, int qgrid_fld = 0,
-                                    size_t lds_fld = 0);
+                                    size_t lds_fld = 0, const FieldLane* lane = nullptr);
 hipError_t launch_parallel_generate(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                     const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                     const int* order, uint32_t flags, hipStream_t stream);

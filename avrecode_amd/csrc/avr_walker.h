@@ -3261,33 +3261,54 @@ __global__ __launch_bounds__(192, 4) void slices_queue_kernel(const EngineTables
 // progressive slices return at once).  The board starts empty on every launch (cu_cell's slot
 // counter must not carry a previous launch's residue).  q.head: the persistent queue launch
 // (slices_parallel_kernel) over q.grid workgroups, q.head[0] for the progressive kernel and
-// q.head[1] for the field one (both zero on entry).
+// q.head[1] for the field one (both zero on entry).  q.lane (FieldLane): the field kernel runs on a
+// stream of its own beside the progressive one, so a mixed batch takes the longer of the two
+// kernels instead of their sum.  The two kernels share the board (it ranks the slices of a CU
+// whichever kernel walks them; one reset before both) and touch disjoint slices; their persistent
+// workgroups take disjoint estimator scratches (the field kernel's after the q.grid progressive ones).
 struct QueueLaunch {
   uint32_t* head = nullptr;
   int grid = 0, grid_fld = 0;   // persistent grids of the progressive and the field kernel
   size_t lds_fld = 0;           // LDS of the field kernel (0: the progressive kernel's)
+  const FieldLane* lane = nullptr;
 };
 template <int MODE, bool P32>
 inline hipError_t launch_parallel(const EngineTables* T, const avr_slice_desc* descs, int n, size_t lds,
                                   const uint8_t* in, uint8_t* out, avr_slice_result* res, uint16_t* est,
                                   const int* order, uint32_t flags, hipStream_t stream, QueueLaunch q = QueueLaunch()) {
   const size_t lds_fld = q.lds_fld ? q.lds_fld : lds;
+  const bool fields = (flags & kFlagFields) != 0;
+  const bool side = fields && q.lane && q.lane->stream;
   if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
+  hipStream_t fs = stream;
+  if (side) {
+    fs = q.lane->stream;
+    if (hipError_t e = hipEventRecord(q.lane->fork, stream); e != hipSuccess) return e;
+    if (hipError_t e = hipStreamWaitEvent(fs, q.lane->fork, 0); e != hipSuccess) return e;
+  }
   if (q.head)
     hipLaunchKernelGGL((slices_queue_kernel<MODE, false, P32>), dim3(q.grid), dim3(slice_threads<MODE>()), lds, stream,
                        T, descs, n, in, out, res, est, order, q.head, flags);
   else
     hipLaunchKernelGGL((slices_parallel_kernel<MODE, false, P32>), dim3(n), dim3(slice_threads<MODE>()), lds, stream,
                        T, descs, n, in, out, res, est, order, flags);
-  if (flags & kFlagFields) {
+  if (fields) {
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-    if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
+    if (!side)
+      if (hipError_t e = reset_cu_board(stream); e != hipSuccess) return e;
+    // beside the progressive kernel, the persistent field workgroups take the scratches after its grid
+    uint16_t* est_f = side && q.head ? est + (size_t)q.grid * kEstGlobal : est;
     if (q.head)
       hipLaunchKernelGGL((slices_queue_kernel<MODE, true, P32>), dim3(q.grid_fld), dim3(slice_threads<MODE>()), lds_fld,
-                         stream, T, descs, n, in, out, res, est, order, q.head + 1, flags & ~kFlagMringGlobal);
+                         fs, T, descs, n, in, out, res, est_f, order, q.head + 1, flags & ~kFlagMringGlobal);
     else
       hipLaunchKernelGGL((slices_parallel_kernel<MODE, true, P32>), dim3(n), dim3(slice_threads<MODE>()), lds_fld,
-                         stream, T, descs, n, in, out, res, est, order, flags & ~kFlagMringGlobal);
+                         fs, T, descs, n, in, out, res, est_f, order, flags & ~kFlagMringGlobal);
+    if (side) {
+      if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+      if (hipError_t e = hipEventRecord(q.lane->join, fs); e != hipSuccess) return e;
+      if (hipError_t e = hipStreamWaitEvent(stream, q.lane->join, 0); e != hipSuccess) return e;
+    }
   }
   return hipGetLastError();
 }

@@ -262,3 +262,28 @@ def test_damaged_field_slices_are_contained(ctx, structure):
     for model in (avr.MODEL_REFERENCE, avr.MODEL_PARALLEL):
         avrc = ctx.compress(raw, model)
         assert ctx.decompress(avrc) == raw
+
+
+def test_field_lane_matches_serial_launch(ctx, monkeypatch):
+    """A parallel batch of progressive and field slices runs the field kernel on a stream of its own
+    beside the progressive one (the context's field lane, avr::FieldLane); AVR_FIELD_LANE=0 runs the
+    two one after the other.  Both give the same containers, which decompress back: with the resident
+    kernels (three files) and with the persistent queue kernels (more slices than resident slots, where
+    the field kernel's workgroups take the estimator scratches after the progressive ones)."""
+    prog = ctx.synthesize(avr.SynthParams(mb_width=8, mb_height=4, slice_type=0, slice_qp=26, seed=21, gop_length=3,
+                                          slices_per_picture=4), 8)
+    fld = _paff(ctx, 4, mb_width=8, mb_height=4, slice_type=0, seed=22, gop_length=3, slices_per_picture=4)
+    mbf = _mbaff(ctx, 4, mb_width=8, mb_height=4, slice_type=1, seed=23, gop_length=3, slices_per_picture=2)
+    small = [prog, fld, mbf]
+    per_set = sum(len(avr.parse_stream(d).descs) for d in small)
+    sets = 1
+    while ctx.slice_kernel(sets * per_set, 8, False).startswith("slices_parallel_kernel"):
+        sets *= 2
+    assert sets > 1
+    for files in (small, small * sets):
+        on = ctx.compress_files(files, avr.MODEL_PARALLEL)
+        assert ctx.decompress_files(on) == files
+        monkeypatch.setenv("AVR_FIELD_LANE", "0")
+        with avr.Context(0) as serial:
+            assert serial.compress_files(files, avr.MODEL_PARALLEL) == on
+        monkeypatch.delenv("AVR_FIELD_LANE")
