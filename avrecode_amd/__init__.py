@@ -38,6 +38,7 @@ MODEL_PARALLEL = 1
 MODEL_PARALLEL32 = 2
 MODEL_CHAINED = 3   # the reference model in chains of CHAIN_SLICES coded slices ("avrecode-amd:R16")
 CHAIN_SLICES = 16
+SPLIT_BYTES_DEFAULT = 98304   # the parallel model's long-slice split (Context.split_bytes), unless AVR_SPLIT_BYTES
 MODEL_NAMES = {MODEL_REFERENCE: "R", MODEL_PARALLEL: "P", MODEL_PARALLEL32: "P32", MODEL_CHAINED: "C"}
 
 AVR_OK = 0

@@ -638,7 +638,7 @@ int run_plan(avr_ctx* c, int mode, bool sequential, Plan& plan, std::vector<avr_
 // recording the candidates, on its own stream beside the rest of the batch -- then the pieces (a
 // slice without a cut: one piece).  Decompress runs the pieces side by side and splices them: piece
 // i's bytes up to cut i's q.
-constexpr size_t kSplitBytesDefault = 131072;
+constexpr size_t kSplitBytesDefault = 98304;
 
 bool split_candidate(const avr_slice_desc& d, size_t split_bytes) {
   return split_bytes && split_bytes < ((size_t)1 << 28) && d.structure == AVR_STRUCT_FRAME &&

@@ -90,7 +90,7 @@ void avr_free(void* p);
  * upper row's neighbour fields).  Such containers decompress through the whole-file calls
  * (avr_decompress_file(s), avr_roundtrip_file(s)) and the hooks sessions (which regenerate one
  * whole at begin, as a reference-model container); the per-slice plans (avr_plan_decompress,
- * avr_dec_plan_load) refuse them with AVR_ERR_UNSUPPORTED.  split_bytes = 0: no split.  Default: the environment's AVR_SPLIT_BYTES, else 131072.  Checked by the oracle's
+ * avr_dec_plan_load) refuse them with AVR_ERR_UNSUPPORTED.  split_bytes = 0: no split.  Default: the environment's AVR_SPLIT_BYTES, else 98304.  Checked by the oracle's
  * restatement (oracle/oracle_seams.c). */
 int avr_set_split_bytes(avr_ctx* ctx, size_t split_bytes);
 size_t avr_get_split_bytes(const avr_ctx* ctx);

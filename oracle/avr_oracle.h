@@ -312,7 +312,7 @@ long avr_oracle_slices_p(const uint8_t *file, size_t n, long lo, long hi, int ch
 /* re-coded streams one after the other.                                                         */
 #define AVR_EDGE_BYTES 40          /* one column of the upper row: flags | cbp << 16, nnz[3][4] (bottom
                                     * rows), mvd[2][4][2], ref[2][2], direct8[2], 2 zero bytes */
-#define AVR_SPLIT_BYTES_DEFAULT 131072
+#define AVR_SPLIT_BYTES_DEFAULT 98304
 typedef struct {
   uint32_t first_mb;               /* the piece's first macroblock (a row start) */
   uint32_t q;                      /* where its regenerated bytes begin in the slice's CABAC bytes */

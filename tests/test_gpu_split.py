@@ -50,7 +50,7 @@ def test_fixture_split_matches_oracle(ctx, name, split_bytes):
         back, _ = ctx.roundtrip_files([data], avr.MODEL_PARALLEL)   # unchecked first pass
         assert back == [avrc]
     finally:
-        ctx.split_bytes = 131072
+        ctx.split_bytes = avr.SPLIT_BYTES_DEFAULT
 
 
 def test_split_off_is_the_plain_container(ctx):
@@ -61,13 +61,13 @@ def test_split_off_is_the_plain_container(ctx):
         assert not _cut_blocks(avrc)
         assert avrc == oracle_cli("compress", FIX / "realshort.mp4", mode="P", split_bytes=0)
     finally:
-        ctx.split_bytes = 131072
+        ctx.split_bytes = avr.SPLIT_BYTES_DEFAULT
 
 
 def test_4k_444_intra_slice_is_split(ctx):
     data = ctx.synthesize(avr.SynthParams(mb_width=240, mb_height=135, slice_type=2, slice_qp=30, chroma_format_idc=3,
                                           transform_8x8_mode=1, seed=4006, slices_per_picture=1, gop_length=1), 1)
-    assert ctx.split_bytes == 131072
+    assert ctx.split_bytes == avr.SPLIT_BYTES_DEFAULT
     avrc = ctx.compress(data, avr.MODEL_PARALLEL)
     cut = _cut_blocks(avrc)
     assert len(cut) == 1
@@ -75,7 +75,7 @@ def test_4k_444_intra_slice_is_split(ctx):
     with tempfile.TemporaryDirectory() as td:
         f = Path(td) / "k.264"
         f.write_bytes(data)
-        assert avrc == oracle_cli("compress", f, mode="P", split_bytes=131072)
+        assert avrc == oracle_cli("compress", f, mode="P", split_bytes=avr.SPLIT_BYTES_DEFAULT)
         g = Path(td) / "k.avrc"
         g.write_bytes(avrc)
         assert oracle_cli("decompress", g) == data
@@ -108,7 +108,7 @@ def test_synthetic_corpus_split_matches_oracle(ctx):
             outs = ctx.compress_files(datas, avr.MODEL_PARALLEL)
             assert ctx.decompress_files(outs) == datas
     finally:
-        ctx.split_bytes = 131072
+        ctx.split_bytes = avr.SPLIT_BYTES_DEFAULT
 
 
 def test_hooks_decompress_reads_a_split_container(ctx):
@@ -120,7 +120,7 @@ def test_hooks_decompress_reads_a_split_container(ctx):
     try:
         avrc = ctx.compress(data, avr.MODEL_PARALLEL)
     finally:
-        ctx.split_bytes = 131072
+        ctx.split_bytes = avr.SPLIT_BYTES_DEFAULT
     assert avr.seams_of_container(avrc)
     r, back, walked = _call("hooks_decompress", avrc, len(avrc))
     assert r == 0, r
@@ -135,7 +135,7 @@ def test_damaged_seams_are_refused(ctx):
     try:
         avrc = ctx.compress(data, avr.MODEL_PARALLEL)
     finally:
-        ctx.split_bytes = 131072
+        ctx.split_bytes = avr.SPLIT_BYTES_DEFAULT
     info, _ = avr.describe_container(avrc)
     blob = bytes.fromhex(next(b["seams"] for b in info["blocks"] if "seams" in b))
     i = avrc.index(blob)

@@ -47,8 +47,8 @@ def test_oracle_roundtrip_with_split(tmp_path, name):
     f = tmp_path / "s.avrc"
     f.write_bytes(split)
     assert oracle_cli("decompress", f) == data
-    # the default split (128 KiB) leaves these small slices whole: the container is the plain one
-    assert oracle_cli("compress", FIX / name, mode="P", split_bytes=131072) == plain
+    # the default split (96 KiB) leaves these small slices whole: the container is the plain one
+    assert oracle_cli("compress", FIX / name, mode="P", split_bytes=98304) == plain
 
 
 def test_split_container_has_seams_fields(tmp_path):
